@@ -1,0 +1,129 @@
+/*
+ * syncr_cdc.h -- C ABI of the MI355X-native Bup content-defined chunker.
+ *
+ * Drop-in boundary for szilu/syncr's chunk scan.  The reference has no plugin
+ * API for this path; its seam is the inline call pair
+ *     Bup::new_with_chunk_bits(CHUNK_BITS)          src/protocol/file_operations.rs:748
+ *     bup.find_chunk_edge(&buf[..endofs])           src/protocol/file_operations.rs:754-755
+ * inside the driver loop compute_file_chunks()     src/protocol/file_operations.rs:721-788
+ * (and its dead duplicate get_file_chunks(), :190-248).  The entry points below
+ * replace that loop: bytes in, chunk boundaries (offset, size) out, bit-exact.
+ * The caller keeps hashing each returned chunk (util::hash_binary, src/util.rs:57-59)
+ * and feeding DumpState::add_chunk (src/serve.rs:36-42) exactly as before.
+ *
+ * Conventions: every function returns 0 on success or a negative errno-style
+ * code (SYNCR_CDC_E*); no C++ exception crosses this boundary.  Inputs and
+ * outputs are caller-allocated; the handle owns its device scratch.  A handle is
+ * single-threaded (one per device / host thread).  `stream` arguments are HIP
+ * streams passed as void* (NULL = the handle's own stream).
+ */
+#ifndef SYNCR_CDC_H
+#define SYNCR_CDC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SYNCR_CDC_ABI_VERSION 1
+
+/* error codes (negative errno values) */
+#define SYNCR_CDC_OK 0
+#define SYNCR_CDC_EINVAL (-22) /* bad argument / parameter out of range          */
+#define SYNCR_CDC_ENOMEM (-12) /* host or device allocation failed               */
+#define SYNCR_CDC_ERANGE (-34) /* output capacity too small; *n_out = required   */
+#define SYNCR_CDC_ENODEV (-19) /* no such HIP device / HIP runtime unavailable   */
+#define SYNCR_CDC_EIO (-5)     /* HIP runtime error while running                 */
+#define SYNCR_CDC_ESTATE (-71) /* call out of order (e.g. launch before plan)    */
+
+/* Chunker parameters.  Defaults mirror src/chunking.rs:7-13 and the production
+ * read path of file_operations.rs:737-776. */
+typedef struct syncr_cdc_params {
+    uint32_t chunk_bits; /* CHUNK_BITS, 1..31 (default 20; reference validates 8..32) */
+    uint32_t flags;      /* reserved, must be 0                                       */
+    uint64_t max_chunk;  /* MAX_CHUNK_SIZE, 1..2^32-1 (default 16 MiB)                  */
+    uint64_t read_cap;   /* bytes per tokio File::read (default 2 MiB); 0 = "ideal"
+                            in-memory semantics of tests/chunking_test.rs:170-192       */
+} syncr_cdc_params;
+
+/* One chunk: the (offset, size) pair of ChunkInfo (src/protocol/types.rs:24-29)
+ * plus the index of the file it belongs to within the call's batch. */
+typedef struct syncr_cut {
+    uint64_t offset; /* byte offset within its file */
+    uint32_t len;    /* chunk size (<= max_chunk)   */
+    uint32_t file;   /* file index in the batch     */
+} syncr_cut;
+
+typedef struct syncr_cdc syncr_cdc;
+
+int32_t syncr_cdc_abi_version(void);
+const char *syncr_cdc_strerror(int32_t code);
+/* chunk_bits=20, max_chunk=16 MiB, read_cap=2 MiB (production semantics) */
+void syncr_cdc_default_params(syncr_cdc_params *p);
+int32_t syncr_cdc_device_count(int32_t *n);
+
+/* Replaces Bup::new_with_chunk_bits: one handle per device, parameters fixed. */
+int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **out);
+void syncr_cdc_close(syncr_cdc *h);
+int32_t syncr_cdc_get_params(const syncr_cdc *h, syncr_cdc_params *p);
+
+/* --- host-memory entry points (end to end: H2D, scan, resolve, D2H) ---------- */
+/* One file (compute_file_chunks' loop, file_operations.rs:746-784).  Empty input
+ * gives 0 chunks.  If cap is too small returns SYNCR_CDC_ERANGE, *n_out = needed. */
+int32_t syncr_cdc_chunk_host(syncr_cdc *h, const uint8_t *data, uint64_t len,
+                             syncr_cut *out, uint64_t cap, uint64_t *n_out);
+/* Many files laid out in one host buffer of `span` bytes.  Chunks are written
+ * file by file (file order of the table); per_file_count[i] gets file i's count. */
+int32_t syncr_cdc_chunk_batch_host(syncr_cdc *h, const uint8_t *data, uint64_t span,
+                                   const uint64_t *file_off, const uint64_t *file_len,
+                                   uint32_t nfiles, syncr_cut *out, uint64_t cap,
+                                   uint64_t *per_file_count, uint64_t *n_out);
+
+/* --- device-resident entry points (what the throughput metric times) ------- */
+/* plan: validate + upload the file table (host arrays) for bytes that will be
+ * resident in device memory at [d_bytes, d_bytes+span).  Files must not overlap.
+ * Synchronous; reusable for any number of launches. */
+int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *file_len,
+                       uint32_t nfiles, uint64_t span);
+/* launch: scan + resolve on `stream`, asynchronous, no host sync, no allocation
+ * (graph-capturable).  d_bytes must be 16-byte aligned device memory. */
+int32_t syncr_cdc_launch(syncr_cdc *h, const uint8_t *d_bytes, void *stream);
+/* fetch: wait for the last launch, copy cuts to the host (file by file). */
+int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap,
+                        uint64_t *per_file_count, uint64_t *n_out);
+/* plan + launch + fetch */
+int32_t syncr_cdc_chunk_batch_device(syncr_cdc *h, const uint8_t *d_bytes, uint64_t span,
+                                     const uint64_t *file_off, const uint64_t *file_len,
+                                     uint32_t nfiles, syncr_cut *out, uint64_t cap,
+                                     uint64_t *per_file_count, uint64_t *n_out, void *stream);
+
+/* --- device memory / stream / timing helpers (hosts without a GPU framework) -- */
+int32_t syncr_cdc_device_alloc(syncr_cdc *h, uint64_t bytes, void **d_ptr);
+int32_t syncr_cdc_device_free(syncr_cdc *h, void *d_ptr);
+int32_t syncr_cdc_host_alloc_pinned(syncr_cdc *h, uint64_t bytes, void **ptr);
+int32_t syncr_cdc_host_free_pinned(syncr_cdc *h, void *ptr);
+int32_t syncr_cdc_memcpy_h2d(syncr_cdc *h, void *d_dst, const void *src, uint64_t bytes, void *stream);
+int32_t syncr_cdc_memcpy_d2h(syncr_cdc *h, void *dst, const void *d_src, uint64_t bytes, void *stream);
+int32_t syncr_cdc_synchronize(syncr_cdc *h);
+void *syncr_cdc_stream(syncr_cdc *h);
+/* Fill [d_bytes + file_off[i], +file_len[i]) with corpus file number
+ * file_index[i] (or first_index+i when file_index is NULL) of the synthetic
+ * corpus: xorshift64 seeded 0x9E3779B97F4A7C15*(index+1), 64 outputs discarded,
+ * byte=(x>>32)&0xff.  Synchronous. */
+int32_t syncr_cdc_gen_corpus(syncr_cdc *h, uint8_t *d_bytes, const uint64_t *file_off,
+                             const uint64_t *file_len, const uint64_t *file_index,
+                             uint32_t nfiles, uint64_t first_index, void *stream);
+/* Per-kernel timing: when enabled, every launch brackets its kernels with HIP
+ * events on the launch stream; kernel_times returns the summed milliseconds of
+ * [scan, dense, resolve] since the last reset and the number of launches. */
+int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable);
+int32_t syncr_cdc_kernel_times(syncr_cdc *h, double *ms3, uint64_t *launches);
+/* Diagnostics of the last fetched launch: [candidates, dense_tiles, tiles, overflow]. */
+int32_t syncr_cdc_last_stats(syncr_cdc *h, uint64_t *stats4);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SYNCR_CDC_H */

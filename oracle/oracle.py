@@ -1,0 +1,197 @@
+"""ctypes front-end of the CPU oracle (oracle/bup_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the *checker*.  The product package
+(syncr_amd) never imports this module.
+
+Reference semantics restated (paths relative to /root/reference):
+  * production driver  src/protocol/file_operations.rs:721-788
+  * ideal driver       tests/chunking_test.rs:170-192
+  * parameters         src/chunking.rs:7-13
+  * rollsum::Bup       rollsum 0.3 (Cargo.toml:24; crate not on disk)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liborc_bup.so")
+
+CHUNK_BITS = 20                       # src/chunking.rs:7
+MAX_CHUNK_SIZE = (1 << 20) * 16       # src/chunking.rs:10-13
+TOKIO_READ_CAP = 2 * 1024 * 1024      # tokio DEFAULT_MAX_BUF_SIZE (Cargo.toml:29)
+
+MODE_PRODUCTION, MODE_IDEAL, MODE_CLOSED_FORM = 0, 1, 2
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_lib = None
+
+
+def build() -> str:
+    """Compile liborc_bup.so with the committed Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH) or (
+            os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "bup_oracle.c"))
+        ):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.orc_chunk_production.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                           ctypes.c_uint64, _u64p, ctypes.c_uint64]
+        L.orc_chunk_production.restype = ctypes.c_uint64
+        L.orc_chunk_closed_form.argtypes = L.orc_chunk_production.argtypes
+        L.orc_chunk_closed_form.restype = ctypes.c_uint64
+        L.orc_chunk_no_head_fixup.argtypes = L.orc_chunk_production.argtypes
+        L.orc_chunk_no_head_fixup.restype = ctypes.c_uint64
+        L.orc_chunk_ideal.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                      _u64p, ctypes.c_uint64]
+        L.orc_chunk_ideal.restype = ctypes.c_uint64
+        L.orc_digest_after.argtypes = [_u8p, ctypes.c_uint64]
+        L.orc_digest_after.restype = ctypes.c_uint32
+        L.orc_xorshift_fill.argtypes = [ctypes.c_uint64, ctypes.c_uint64, _u8p, ctypes.c_uint64]
+        L.orc_xorshift_fill.restype = None
+        L.orc_corpus_seed.argtypes = [ctypes.c_uint64]
+        L.orc_corpus_seed.restype = ctypes.c_uint64
+        L.orc_corpus_fill.argtypes = [_u64p, _u64p, ctypes.c_uint64, ctypes.c_uint64, _u8p]
+        L.orc_corpus_fill.restype = None
+        L.orc_fnv_ends.argtypes = [_u64p, ctypes.c_uint64]
+        L.orc_fnv_ends.restype = ctypes.c_uint64
+        L.orc_chunk_batch.argtypes = [_u8p, _u64p, _u64p, ctypes.c_uint64, ctypes.c_uint32,
+                                      ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, _u64p, _u64p,
+                                      _u64p, _u64p, ctypes.c_int]
+        L.orc_chunk_batch.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _p8(a: np.ndarray):
+    return a.ctypes.data_as(_u8p)
+
+
+def _p64(a: np.ndarray):
+    return a.ctypes.data_as(_u64p)
+
+
+def _as_u8(data) -> np.ndarray:
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(data), dtype=np.uint8)
+    return np.ascontiguousarray(data, dtype=np.uint8)
+
+
+def _run(fn, data, *args) -> np.ndarray:
+    a = _as_u8(data)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    cap = max(16, a.size // 4096 + 64)
+    while True:
+        ends = np.zeros(cap, np.uint64)
+        n = fn(_p8(buf), a.size, *args, _p64(ends), cap)
+        if n == 2**64 - 1:
+            raise MemoryError("oracle allocation failed")
+        if n <= cap:
+            return ends[:n].copy()
+        cap = int(n)
+
+
+def chunk_production(data, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE, read_cap=TOKIO_READ_CAP):
+    """Cut END offsets of compute_file_chunks (file_operations.rs:721-788)."""
+    return _run(lib().orc_chunk_production, data, bits, max_chunk, read_cap)
+
+
+def chunk_ideal(data, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE):
+    """Cut END offsets of chunk_data (tests/chunking_test.rs:170-192)."""
+    return _run(lib().orc_chunk_ideal, data, bits, max_chunk)
+
+
+def chunk_closed_form(data, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE, read_cap=TOKIO_READ_CAP):
+    """Formulation (ii): prefix-sum candidates + serial resolve (read_cap=0: ideal)."""
+    return _run(lib().orc_chunk_closed_form, data, bits, max_chunk, read_cap)
+
+
+def chunk_no_head_fixup(data, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE, read_cap=TOKIO_READ_CAP):
+    """Deliberately wrong (no chunk-head fix-up): adversarial-input search only."""
+    return _run(lib().orc_chunk_no_head_fixup, data, bits, max_chunk, read_cap)
+
+
+def ends_to_cuts(ends) -> list[tuple[int, int]]:
+    """[(offset, size)] like the reference's ChunkInfo{offset,size} (protocol/types.rs:24-29)."""
+    out, prev = [], 0
+    for e in np.asarray(ends, dtype=np.uint64).tolist():
+        out.append((prev, e - prev))
+        prev = e
+    return out
+
+
+def digest_after(data) -> int:
+    a = _as_u8(data)
+    return int(lib().orc_digest_after(_p8(a if a.size else np.zeros(1, np.uint8)), a.size))
+
+
+def xorshift_bytes(seed: int, n: int, discard: int = 0) -> np.ndarray:
+    out = np.empty(max(n, 1), np.uint8)
+    lib().orc_xorshift_fill(seed, discard, _p8(out), n)
+    return out[:n]
+
+
+def corpus_seed(i: int) -> int:
+    return int(lib().orc_corpus_seed(i))
+
+
+def corpus_fill(lens, first_index: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Back-to-back corpus of xorshift files. Returns (bytes, offsets)."""
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    offs = np.zeros_like(lens)
+    if lens.size:
+        offs[1:] = np.cumsum(lens)[:-1]
+    total = int(lens.sum())
+    buf = np.empty(max(total, 1), np.uint8)
+    lib().orc_corpus_fill(_p64(offs), _p64(lens), lens.size, first_index, _p8(buf))
+    return buf[:total], offs
+
+
+def fnv_ends(ends) -> int:
+    e = np.ascontiguousarray(ends, dtype=np.uint64)
+    return int(lib().orc_fnv_ends(_p64(e if e.size else np.zeros(1, np.uint64)), e.size))
+
+
+def chunk_batch(base, offs, lens, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE,
+                read_cap=TOKIO_READ_CAP, mode=MODE_PRODUCTION, nthreads=None):
+    """Chunk many files (threads over files, largest first). Returns list of end arrays."""
+    base = _as_u8(base)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    n = lens.size
+    caps = lens // max(1, 1 << max(0, bits - 6)) + 64
+    order = np.argsort(-lens.astype(np.int64), kind="stable")
+    ob = np.zeros(n, np.uint64)
+    if n:
+        ob[1:] = np.cumsum(caps)[:-1]
+    ends = np.zeros(max(int(caps.sum()), 1), np.uint64)
+    counts = np.zeros(max(n, 1), np.uint64)
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    # pass the permuted tables so big files start first
+    po, pl, pb, pc = (np.ascontiguousarray(a[order]) for a in (offs, lens, ob, caps))
+    pcount = np.zeros(max(n, 1), np.uint64)
+    lib().orc_chunk_batch(_p8(base if base.size else np.zeros(1, np.uint8)), _p64(po), _p64(pl), n,
+                          bits, max_chunk, read_cap, mode, _p64(pb), _p64(pc), _p64(ends),
+                          _p64(pcount), nthreads)
+    counts[order] = pcount[:n]
+    out = []
+    for i in range(n):
+        c = int(counts[i])
+        if c > int(caps[i]):  # rare: re-run this file alone with exact capacity
+            f = base[int(offs[i]): int(offs[i]) + int(lens[i])]
+            fn = {MODE_PRODUCTION: chunk_production, MODE_CLOSED_FORM: chunk_closed_form}.get(mode)
+            out.append(chunk_ideal(f, bits, max_chunk) if mode == MODE_IDEAL else fn(f, bits, max_chunk, read_cap))
+        else:
+            out.append(ends[int(ob[i]): int(ob[i]) + c].copy())
+    return out

@@ -1,0 +1,347 @@
+"""syncr_amd -- MI355X-native Bup content-defined chunker (host mirror).
+
+Python mirror of szilu/syncr's chunking interface over the C ABI in
+include/syncr_cdc.h (libsyncr_cdc.so, HIP kernels for gfx950):
+
+  * constants             src/chunking.rs:7-13           -> CHUNK_BITS, MAX_CHUNK_SIZE
+  * ChunkInfo             src/protocol/types.rs:24-29    -> ChunkInfo(offset, size, hash)
+  * compute_file_chunks   src/protocol/file_operations.rs:721-788
+                          (open/read failure -> warn + empty list, like :727-744)
+  * chunk_data            tests/chunking_test.rs:170-192 (ideal, in-memory semantics)
+
+There is no CPU fallback: if the HIP library is missing or no GPU is visible the
+calls raise (SyncrCdcError), they never silently compute on the host.
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+__all__ = [
+    "CHUNK_BITS", "MAX_CHUNK_SIZE_FACTOR", "MAX_CHUNK_SIZE", "TOKIO_READ_CAP",
+    "ChunkInfo", "Chunker", "SyncrCdcError", "compute_file_chunks", "chunk_data",
+    "library", "library_path", "EXPORTED_SYMBOLS",
+]
+
+log = logging.getLogger("syncr_amd")
+
+CHUNK_BITS = 20                                   # src/chunking.rs:7
+MAX_CHUNK_SIZE_FACTOR = 16                        # src/chunking.rs:10
+MAX_CHUNK_SIZE = (1 << CHUNK_BITS) * MAX_CHUNK_SIZE_FACTOR   # src/chunking.rs:13
+TOKIO_READ_CAP = 2 * 1024 * 1024                  # tokio File::read (file_operations.rs:738,776)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+library_path = os.path.join(_PKG, "libsyncr_cdc.so")
+
+# every symbol declared in include/syncr_cdc.h
+EXPORTED_SYMBOLS = (
+    "syncr_cdc_abi_version", "syncr_cdc_strerror", "syncr_cdc_default_params",
+    "syncr_cdc_device_count", "syncr_cdc_open", "syncr_cdc_close", "syncr_cdc_get_params",
+    "syncr_cdc_chunk_host", "syncr_cdc_chunk_batch_host", "syncr_cdc_plan", "syncr_cdc_launch",
+    "syncr_cdc_fetch", "syncr_cdc_chunk_batch_device", "syncr_cdc_device_alloc",
+    "syncr_cdc_device_free", "syncr_cdc_host_alloc_pinned", "syncr_cdc_host_free_pinned",
+    "syncr_cdc_memcpy_h2d", "syncr_cdc_memcpy_d2h", "syncr_cdc_synchronize", "syncr_cdc_stream",
+    "syncr_cdc_gen_corpus", "syncr_cdc_set_timing", "syncr_cdc_kernel_times",
+    "syncr_cdc_last_stats",
+)
+
+ABI_VERSION = 1
+E_RANGE = -34
+
+
+class SyncrCdcError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        msg = library().syncr_cdc_strerror(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{what}: {msg} ({code})")
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("chunk_bits", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("max_chunk", ctypes.c_uint64), ("read_cap", ctypes.c_uint64)]
+
+
+class Cut(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("len", ctypes.c_uint32), ("file", ctypes.c_uint32)]
+
+
+CUT_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("file", "<u4")])
+assert CUT_DTYPE.itemsize == ctypes.sizeof(Cut) == 16
+
+_lib = None
+_vp, _u64, _u32, _i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32
+_pu64 = ctypes.POINTER(ctypes.c_uint64)
+
+
+def library():
+    """Load libsyncr_cdc.so (raises if it was not built -- no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(library_path):
+            raise ImportError(f"syncr_amd: {library_path} not built; run `python -m syncr_amd.build` "
+                              "(the HIP engine has no CPU fallback)")
+        L = ctypes.CDLL(library_path)
+        sig = {
+            "syncr_cdc_abi_version": ([], _i32),
+            "syncr_cdc_strerror": ([_i32], ctypes.c_char_p),
+            "syncr_cdc_default_params": ([ctypes.POINTER(Params)], None),
+            "syncr_cdc_device_count": ([ctypes.POINTER(_i32)], _i32),
+            "syncr_cdc_open": ([_i32, ctypes.POINTER(Params), ctypes.POINTER(_vp)], _i32),
+            "syncr_cdc_close": ([_vp], None),
+            "syncr_cdc_get_params": ([_vp, ctypes.POINTER(Params)], _i32),
+            "syncr_cdc_chunk_host": ([_vp, _vp, _u64, _vp, _u64, _pu64], _i32),
+            "syncr_cdc_chunk_batch_host": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u64, _vp, _pu64], _i32),
+            "syncr_cdc_plan": ([_vp, _vp, _vp, _u32, _u64], _i32),
+            "syncr_cdc_launch": ([_vp, _vp, _vp], _i32),
+            "syncr_cdc_fetch": ([_vp, _vp, _u64, _vp, _pu64], _i32),
+            "syncr_cdc_chunk_batch_device": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u64, _vp, _pu64, _vp], _i32),
+            "syncr_cdc_device_alloc": ([_vp, _u64, ctypes.POINTER(_vp)], _i32),
+            "syncr_cdc_device_free": ([_vp, _vp], _i32),
+            "syncr_cdc_host_alloc_pinned": ([_vp, _u64, ctypes.POINTER(_vp)], _i32),
+            "syncr_cdc_host_free_pinned": ([_vp, _vp], _i32),
+            "syncr_cdc_memcpy_h2d": ([_vp, _vp, _vp, _u64, _vp], _i32),
+            "syncr_cdc_memcpy_d2h": ([_vp, _vp, _vp, _u64, _vp], _i32),
+            "syncr_cdc_synchronize": ([_vp], _i32),
+            "syncr_cdc_stream": ([_vp], _vp),
+            "syncr_cdc_gen_corpus": ([_vp, _vp, _vp, _vp, _vp, _u32, _u64, _vp], _i32),
+            "syncr_cdc_set_timing": ([_vp, _i32], _i32),
+            "syncr_cdc_kernel_times": ([_vp, ctypes.POINTER(ctypes.c_double), _pu64], _i32),
+            "syncr_cdc_last_stats": ([_vp, _pu64], _i32),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        if L.syncr_cdc_abi_version() != ABI_VERSION:
+            raise ImportError("syncr_amd: ABI version mismatch with libsyncr_cdc.so")
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise SyncrCdcError(rc, what)
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    rc = library().syncr_cdc_device_count(ctypes.byref(n))
+    return int(n.value) if rc == 0 else 0
+
+
+@dataclass(frozen=True)
+class ChunkInfo:
+    """ChunkInfo{hash, offset, size} (src/protocol/types.rs:24-29).
+
+    `hash` (BLAKE3, util::hash_binary, src/util.rs:57-59) is computed by the
+    caller per chunk, exactly as in compute_file_chunks (file_operations.rs:757);
+    it is None here until filled in."""
+    offset: int
+    size: int
+    hash: Optional[bytes] = None
+
+
+def _u8(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data.reshape(-1).view(np.uint8))
+    return np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+
+
+class Chunker:
+    """One engine handle on one device (Bup::new_with_chunk_bits, fixed params)."""
+
+    def __init__(self, chunk_bits: int = CHUNK_BITS, max_chunk: int = MAX_CHUNK_SIZE,
+                 read_cap: int = TOKIO_READ_CAP, device: int = 0):
+        L = library()
+        self.params = Params(chunk_bits, 0, max_chunk, read_cap)
+        h = _vp()
+        _check(L.syncr_cdc_open(device, ctypes.byref(self.params), ctypes.byref(h)), "syncr_cdc_open")
+        self._h = h
+        self.device = device
+        self._nfiles = 0
+
+    # -- lifetime ---------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            library().syncr_cdc_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        return library().syncr_cdc_stream(self._h) or 0
+
+    # -- host-memory paths ------------------------------------------------
+    def cut_array(self, data) -> np.ndarray:
+        """One file from host memory -> structured array (offset, len, file)."""
+        a = _u8(data)
+        return self.batch_arrays(a, [0], [a.size])[0]
+
+    def chunk_bytes(self, data) -> list[ChunkInfo]:
+        return [ChunkInfo(int(o), int(n)) for o, n, _ in self.cut_array(data).tolist()]
+
+    def batch_arrays(self, buf, offsets: Sequence[int], lengths: Sequence[int]) -> list[np.ndarray]:
+        L = library()
+        a = _u8(buf)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lengths, dtype=np.uint64)
+        nf = offs.size
+        counts = np.zeros(max(nf, 1), np.uint64)
+        n = ctypes.c_uint64(0)
+        cap = max(16, a.size // (1 << max(0, self.params.chunk_bits - 2)) + 4 * nf + 16)
+        for _ in range(3):
+            out = np.zeros(cap, CUT_DTYPE)
+            rc = L.syncr_cdc_chunk_batch_host(self._h, a.ctypes.data if a.size else None, a.size,
+                                              offs.ctypes.data, lens.ctypes.data, nf,
+                                              out.ctypes.data, cap, counts.ctypes.data, ctypes.byref(n))
+            if rc == E_RANGE:
+                cap = int(n.value)
+                continue
+            _check(rc, "syncr_cdc_chunk_batch_host")
+            break
+        return _split(out[: int(n.value)], counts[:nf])
+
+    # -- device-resident paths (what the metric times) -------------------
+    def plan(self, offsets, lengths, span: int) -> None:
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lengths, dtype=np.uint64)
+        _check(library().syncr_cdc_plan(self._h, offs.ctypes.data, lens.ctypes.data, offs.size, span),
+               "syncr_cdc_plan")
+        self._nfiles = offs.size
+
+    def launch(self, d_bytes: int, stream: int = 0) -> None:
+        _check(library().syncr_cdc_launch(self._h, d_bytes, stream or None), "syncr_cdc_launch")
+
+    def fetch(self) -> list[np.ndarray]:
+        L = library()
+        nf = self._nfiles
+        counts = np.zeros(max(nf, 1), np.uint64)
+        n = ctypes.c_uint64(0)
+        rc = L.syncr_cdc_fetch(self._h, None, 0, counts.ctypes.data, ctypes.byref(n))
+        if rc not in (0, E_RANGE):
+            _check(rc, "syncr_cdc_fetch")
+        out = np.zeros(max(int(n.value), 1), CUT_DTYPE)
+        _check(L.syncr_cdc_fetch(self._h, out.ctypes.data, out.size, counts.ctypes.data, ctypes.byref(n)),
+               "syncr_cdc_fetch")
+        return _split(out[: int(n.value)], counts[:nf])
+
+    def set_timing(self, on: bool) -> None:
+        _check(library().syncr_cdc_set_timing(self._h, 1 if on else 0), "syncr_cdc_set_timing")
+
+    def kernel_times(self) -> tuple[list[float], int]:
+        ms = (ctypes.c_double * 3)()
+        n = ctypes.c_uint64(0)
+        _check(library().syncr_cdc_kernel_times(self._h, ms, ctypes.byref(n)), "syncr_cdc_kernel_times")
+        return [ms[0], ms[1], ms[2]], int(n.value)
+
+    def last_stats(self) -> dict:
+        st = (ctypes.c_uint64 * 4)()
+        _check(library().syncr_cdc_last_stats(self._h, st), "syncr_cdc_last_stats")
+        return {"candidates": st[0], "dense_tiles": st[1], "tiles": st[2], "flags": st[3]}
+
+    def synchronize(self) -> None:
+        _check(library().syncr_cdc_synchronize(self._h), "syncr_cdc_synchronize")
+
+
+class DeviceBuffer:
+    """Device allocation owned by a Chunker's device (plumbing for tests/bench)."""
+
+    def __init__(self, chunker: Chunker, nbytes: int):
+        self._c = chunker
+        p = _vp()
+        _check(library().syncr_cdc_device_alloc(chunker.handle, nbytes, ctypes.byref(p)), "device_alloc")
+        self.ptr = int(p.value)
+        self.nbytes = nbytes
+
+    def upload(self, data, offset: int = 0) -> None:
+        a = _u8(data)
+        if a.size:
+            _check(library().syncr_cdc_memcpy_h2d(self._c.handle, self.ptr + offset, a.ctypes.data,
+                                                  a.size, None), "memcpy_h2d")
+            self._c.synchronize()
+
+    def download(self, nbytes: Optional[int] = None, offset: int = 0) -> np.ndarray:
+        n = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(max(n, 1), np.uint8)
+        if n:
+            _check(library().syncr_cdc_memcpy_d2h(self._c.handle, out.ctypes.data, self.ptr + offset, n,
+                                                  None), "memcpy_d2h")
+            self._c.synchronize()
+        return out[:n]
+
+    def gen_corpus(self, offsets, lengths, first_index: int = 0, indices=None) -> None:
+        """Synthetic corpus on the device: file i gets corpus file number
+        indices[i] (default first_index + i)."""
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lengths, dtype=np.uint64)
+        idx = None if indices is None else np.ascontiguousarray(indices, dtype=np.uint64)
+        _check(library().syncr_cdc_gen_corpus(self._c.handle, self.ptr, offs.ctypes.data, lens.ctypes.data,
+                                              None if idx is None else idx.ctypes.data, offs.size,
+                                              first_index, None), "gen_corpus")
+
+    def free(self) -> None:
+        if self.ptr:
+            library().syncr_cdc_device_free(self._c.handle, self.ptr)
+            self.ptr = 0
+
+
+def _split(cuts: np.ndarray, counts: np.ndarray) -> list[np.ndarray]:
+    out, o = [], 0
+    for c in counts.tolist():
+        out.append(cuts[o: o + int(c)])
+        o += int(c)
+    return out
+
+
+_default: Optional[Chunker] = None
+
+
+def _default_chunker() -> Chunker:
+    global _default
+    if _default is None:
+        _default = Chunker()
+    return _default
+
+
+def compute_file_chunks(path, chunker: Optional[Chunker] = None) -> list[ChunkInfo]:
+    """compute_file_chunks (src/protocol/file_operations.rs:721-788): chunk one
+    file with production semantics.  Like the reference, an unreadable file is
+    logged and yields an empty list (:727-744); GPU errors raise."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError as e:
+        log.warning("Cannot open file %s: %s", path, e)
+        return []
+    return (chunker or _default_chunker()).chunk_bytes(data)
+
+
+def chunk_data(data, chunk_bits: int = 13, max_chunk: Optional[int] = None,
+               chunker: Optional[Chunker] = None) -> list[tuple[int, int]]:
+    """tests/chunking_test.rs:170-192: in-memory ideal semantics, (offset, size)
+    pairs; defaults are that test's CHUNK_BITS=13, MAX=(1<<13)*16 (:7-8)."""
+    if chunker is None:
+        max_chunk = max_chunk or (1 << chunk_bits) * 16
+        with Chunker(chunk_bits, max_chunk, 0) as c:
+            return [(ci.offset, ci.size) for ci in c.chunk_bytes(data)]
+    return [(ci.offset, ci.size) for ci in chunker.chunk_bytes(data)]

@@ -1,0 +1,39 @@
+"""Build libsyncr_cdc.so (HIP kernels + C ABI) in-tree with hipcc for gfx950."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libsyncr_cdc.so")
+SOURCES = [os.path.join(CSRC, "cdc_kernels.hip"), os.path.join(CSRC, "cdc_api.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, "cdc_internal.h"), os.path.join(ROOT, "include", "syncr_cdc.h")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("SYNCR_CDC_ARCH", "gfx950")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(p) > t for p in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return LIB
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
+           "-o", LIB + ".tmp", *SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

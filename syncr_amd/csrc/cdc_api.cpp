@@ -1,0 +1,619 @@
+// cdc_api.cpp -- C ABI of the MI355X CDC engine (declared in include/syncr_cdc.h).
+//
+// Replaces the scan half of compute_file_chunks (reference
+// src/protocol/file_operations.rs:721-788): the caller hands over file bytes,
+// gets (offset, size) per chunk back.  No C++ exception crosses this boundary.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <numeric>
+#include <vector>
+
+#include "../../include/syncr_cdc.h"
+#include "cdc_internal.h"
+
+using namespace cdc;
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+struct PendingTiming {
+    hipEvent_t ev[4];
+};
+
+}  // namespace
+
+struct syncr_cdc {
+    int device = 0;
+    syncr_cdc_params params{};
+    KParams kp{};
+    hipStream_t stream = nullptr;
+
+    // plan
+    bool planned = false;
+    uint32_t nfiles = 0, nstarts = 0, ntiles = 0, nwords = 0;
+    uint64_t span = 0;
+    uint32_t dense_cap = 0;
+    uint64_t total_cut_cap = 0;
+    std::vector<uint64_t> h_foff, h_flen, h_cut_base;
+    std::vector<uint32_t> h_cut_cap;
+    DevBuf fstart, foff, flen, order, cut_base, cut_cap, tile_range, tile_meta, slots, zeroed,
+        dense_list, dense_bits, cuts, counts;
+
+    // launch
+    bool launched = false;
+    const uint8_t *last_bytes = nullptr;
+    hipStream_t last_stream = nullptr;
+    uint64_t stats[4] = {0, 0, 0, 0};
+
+    // host-path staging
+    DevBuf stage;
+
+    // timing
+    bool timing = false;
+    std::vector<PendingTiming> pending;
+    double ms[3] = {0, 0, 0};
+    uint64_t timed_launches = 0;
+};
+
+namespace {
+
+int32_t hip_err(hipError_t e) {
+    if (e == hipSuccess) return SYNCR_CDC_OK;
+    if (e == hipErrorOutOfMemory) return SYNCR_CDC_ENOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return SYNCR_CDC_ENODEV;
+    return SYNCR_CDC_EIO;
+}
+
+#define CHECK_HIP(x)                                  \
+    do {                                              \
+        hipError_t e_ = (x);                          \
+        if (e_ != hipSuccess) return hip_err(e_);     \
+    } while (0)
+
+int32_t validate_params(const syncr_cdc_params *p) {
+    if (!p) return SYNCR_CDC_EINVAL;
+    if (p->chunk_bits < 1 || p->chunk_bits > 31) return SYNCR_CDC_EINVAL;
+    if (p->flags != 0) return SYNCR_CDC_EINVAL;
+    if (p->max_chunk < 1 || p->max_chunk > 0xffffffffull) return SYNCR_CDC_EINVAL;
+    return SYNCR_CDC_OK;
+}
+
+KParams make_kparams(const syncr_cdc_params &p) {
+    KParams k{};
+    k.bits = p.chunk_bits;
+    k.mask = (uint32_t)((1ull << p.chunk_bits) - 1);
+    k.m1 = p.chunk_bits > 16 ? (uint32_t)((1u << (p.chunk_bits - 16)) - 1) : 0u;
+    const uint32_t kk = 1u << (16 - std::min<uint32_t>(p.chunk_bits, 16));
+    k.k = kk;
+    k.kk = (kk & 0xffffu) | ((kk & 0xffffu) << 16);
+    const uint32_t km = (0u - 64u * kk) & 0xffffu;
+    k.kmv = km | (km << 16);
+    k.max_chunk = p.max_chunk;
+    k.read_cap = p.read_cap;
+    return k;
+}
+
+// Output slots reserved per file: 16x the expected chunk count plus slack; a
+// file that needs more is re-resolved with its exact count (fetch()).
+uint32_t default_cut_cap(uint64_t len, uint32_t bits) {
+    const uint32_t sh = bits > 4 ? bits - 4 : 0;
+    uint64_t c = (len >> sh) + 8;
+    return (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
+}
+
+Tables make_tables(syncr_cdc *h) {
+    Tables t{};
+    t.span = h->span;
+    t.ntiles = h->ntiles;
+    t.nstarts = h->nstarts;
+    t.fstart = h->fstart.as<uint64_t>();
+    t.tile_range = h->tile_range.as<uint2>();
+    t.nfiles = h->nfiles;
+    t.foff = h->foff.as<uint64_t>();
+    t.flen = h->flen.as<uint64_t>();
+    t.order = h->order.as<uint32_t>();
+    t.cut_base = h->cut_base.as<uint64_t>();
+    t.cut_cap = h->cut_cap.as<uint32_t>();
+    t.tile_meta = h->tile_meta.as<uint32_t>();
+    t.slots = h->slots.as<uint2>();
+    t.ctr = h->zeroed.as<uint32_t>();
+    t.nonempty = reinterpret_cast<unsigned long long *>(h->zeroed.as<uint8_t>() + 16);
+    t.dense_list = h->dense_list.as<uint32_t>();
+    t.dense_cap = h->dense_cap;
+    t.dense_bits = h->dense_bits.as<uint32_t>();
+    t.cuts = h->cuts.as<DevCut>();
+    t.counts = h->counts.as<uint64_t>();
+    return t;
+}
+
+int32_t upload_cut_tables(syncr_cdc *h) {
+    h->h_cut_base.resize(h->nfiles);
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < h->nfiles; i++) {
+        h->h_cut_base[i] = acc;
+        acc += h->h_cut_cap[i];
+    }
+    h->total_cut_cap = acc;
+    CHECK_HIP(h->cut_base.ensure(std::max<size_t>(h->nfiles, 1) * 8));
+    CHECK_HIP(h->cut_cap.ensure(std::max<size_t>(h->nfiles, 1) * 4));
+    CHECK_HIP(h->cuts.ensure(std::max<uint64_t>(acc, 1) * sizeof(DevCut)));
+    if (h->nfiles) {
+        CHECK_HIP(hipMemcpy(h->cut_base.p, h->h_cut_base.data(), h->nfiles * 8ull, hipMemcpyHostToDevice));
+        CHECK_HIP(hipMemcpy(h->cut_cap.p, h->h_cut_cap.data(), h->nfiles * 4ull, hipMemcpyHostToDevice));
+    }
+    return SYNCR_CDC_OK;
+}
+
+int32_t ensure_dense(syncr_cdc *h, uint32_t cap) {
+    h->dense_cap = cap;
+    CHECK_HIP(h->dense_list.ensure(std::max<size_t>(cap, 1) * 4));
+    CHECK_HIP(h->dense_bits.ensure(std::max<size_t>(cap, 1) * (size_t)DENSE_WORDS * 4));
+    return SYNCR_CDC_OK;
+}
+
+void drain_timing(syncr_cdc *h) {
+    for (auto &pt : h->pending) {
+        (void)hipEventSynchronize(pt.ev[3]);
+        for (int k = 0; k < 3; k++) {
+            float f = 0.f;
+            if (hipEventElapsedTime(&f, pt.ev[k], pt.ev[k + 1]) == hipSuccess) h->ms[k] += f;
+        }
+        for (int k = 0; k < 4; k++) (void)hipEventDestroy(pt.ev[k]);
+        h->timed_launches++;
+    }
+    h->pending.clear();
+}
+
+int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
+    KParams kp = h->kp;
+    Tables t = make_tables(h);
+    const size_t zbytes = 16 + (size_t)h->nwords * 8;
+    PendingTiming pt{};
+    if (h->timing) {
+        if (h->pending.size() >= 256) drain_timing(h);
+        for (int k = 0; k < 4; k++) CHECK_HIP(hipEventCreate(&pt.ev[k]));
+    }
+    CHECK_HIP(hipMemsetAsync(h->zeroed.p, 0, (zbytes + 15) & ~size_t(15), s));
+    if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[0], s));
+    CHECK_HIP(launch_scan(d_bytes, kp, t, s));
+    if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[1], s));
+    CHECK_HIP(launch_dense(d_bytes, kp, t, s));
+    if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[2], s));
+    CHECK_HIP(launch_resolve(d_bytes, kp, t, s));
+    if (h->timing) {
+        CHECK_HIP(hipEventRecord(pt.ev[3], s));
+        h->pending.push_back(pt);
+    }
+    h->launched = true;
+    h->last_bytes = d_bytes;
+    h->last_stream = s;
+    return SYNCR_CDC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t syncr_cdc_abi_version(void) { return SYNCR_CDC_ABI_VERSION; }
+
+const char *syncr_cdc_strerror(int32_t code) {
+    switch (code) {
+        case SYNCR_CDC_OK: return "ok";
+        case SYNCR_CDC_EINVAL: return "invalid argument";
+        case SYNCR_CDC_ENOMEM: return "out of memory";
+        case SYNCR_CDC_ERANGE: return "output capacity too small";
+        case SYNCR_CDC_ENODEV: return "no HIP device";
+        case SYNCR_CDC_EIO: return "HIP runtime error";
+        case SYNCR_CDC_ESTATE: return "call out of order";
+        default: return "unknown error";
+    }
+}
+
+void syncr_cdc_default_params(syncr_cdc_params *p) {
+    if (!p) return;
+    p->chunk_bits = 20;                 // src/chunking.rs:7
+    p->flags = 0;
+    p->max_chunk = (1ull << 20) * 16;   // src/chunking.rs:10-13
+    p->read_cap = 2ull * 1024 * 1024;   // tokio File::read cap (file_operations.rs:738,776)
+}
+
+int32_t syncr_cdc_device_count(int32_t *n) {
+    if (!n) return SYNCR_CDC_EINVAL;
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) { *n = 0; return SYNCR_CDC_ENODEV; }
+    *n = c;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **out) {
+    if (!out) return SYNCR_CDC_EINVAL;
+    *out = nullptr;
+    syncr_cdc_params prm;
+    if (p) prm = *p; else syncr_cdc_default_params(&prm);
+    int32_t rc = validate_params(&prm);
+    if (rc) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SYNCR_CDC_ENODEV;
+    if (device < 0 || device >= ndev) return SYNCR_CDC_ENODEV;
+    CHECK_HIP(hipSetDevice(device));
+    syncr_cdc *h = new (std::nothrow) syncr_cdc();
+    if (!h) return SYNCR_CDC_ENOMEM;
+    h->device = device;
+    h->params = prm;
+    h->kp = make_kparams(prm);
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return SYNCR_CDC_EIO;
+    }
+    *out = h;
+    return SYNCR_CDC_OK;
+}
+
+void syncr_cdc_close(syncr_cdc *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    drain_timing(h);
+    DevBuf *bufs[] = {&h->fstart, &h->foff, &h->flen, &h->order, &h->cut_base, &h->cut_cap,
+                      &h->tile_range, &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
+                      &h->dense_bits, &h->cuts, &h->counts, &h->stage};
+    for (DevBuf *b : bufs) b->release();
+    (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int32_t syncr_cdc_get_params(const syncr_cdc *h, syncr_cdc_params *p) {
+    if (!h || !p) return SYNCR_CDC_EINVAL;
+    *p = h->params;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *file_len,
+                       uint32_t nfiles, uint64_t span) {
+    if (!h) return SYNCR_CDC_EINVAL;
+    if (nfiles && (!file_off || !file_len)) return SYNCR_CDC_EINVAL;
+    try {
+        CHECK_HIP(hipSetDevice(h->device));
+        h->planned = false;
+        h->launched = false;
+        // validate: inside span, non-empty files must not overlap
+        std::vector<uint32_t> ne;
+        ne.reserve(nfiles);
+        for (uint32_t i = 0; i < nfiles; i++) {
+            if (file_len[i] > span || file_off[i] > span - file_len[i]) return SYNCR_CDC_EINVAL;
+            if (file_len[i]) ne.push_back(i);
+        }
+        std::sort(ne.begin(), ne.end(), [&](uint32_t a, uint32_t b) { return file_off[a] < file_off[b]; });
+        std::vector<uint64_t> starts(ne.size());
+        for (size_t j = 0; j < ne.size(); j++) {
+            starts[j] = file_off[ne[j]];
+            if (j && file_off[ne[j - 1]] + file_len[ne[j - 1]] > starts[j]) return SYNCR_CDC_EINVAL;
+        }
+        const uint64_t ntiles64 = (span + TILE - 1) / TILE;
+        if (ntiles64 > 0x7fffffffull) return SYNCR_CDC_EINVAL;
+        h->nfiles = nfiles;
+        h->nstarts = (uint32_t)starts.size();
+        h->span = span;
+        h->ntiles = (uint32_t)ntiles64;
+        h->nwords = (h->ntiles + 63) / 64;
+        h->h_foff.assign(file_off, file_off + nfiles);
+        h->h_flen.assign(file_len, file_len + nfiles);
+
+        // per-tile range of relevant file starts: [t0-63, t0+TILE)
+        std::vector<uint2> tr(std::max<uint32_t>(h->ntiles, 1));
+        {
+            size_t lo = 0, hi = 0;
+            for (uint32_t t = 0; t < h->ntiles; t++) {
+                const int64_t t0 = (int64_t)t * TILE;
+                while (lo < starts.size() && (int64_t)starts[lo] < t0 - 63) lo++;
+                if (hi < lo) hi = lo;
+                while (hi < starts.size() && (int64_t)starts[hi] < t0 + TILE) hi++;
+                tr[t] = make_uint2((uint32_t)lo, (uint32_t)hi);
+            }
+        }
+        // resolve order: largest files first (longest serial chains start first)
+        std::vector<uint32_t> order(nfiles);
+        std::iota(order.begin(), order.end(), 0u);
+        std::stable_sort(order.begin(), order.end(),
+                         [&](uint32_t a, uint32_t b) { return file_len[a] > file_len[b]; });
+        h->h_cut_cap.resize(nfiles);
+        for (uint32_t i = 0; i < nfiles; i++) h->h_cut_cap[i] = default_cut_cap(file_len[i], h->params.chunk_bits);
+
+        CHECK_HIP(h->fstart.ensure(std::max<size_t>(starts.size(), 1) * 8));
+        CHECK_HIP(h->foff.ensure(std::max<size_t>(nfiles, 1) * 8));
+        CHECK_HIP(h->flen.ensure(std::max<size_t>(nfiles, 1) * 8));
+        CHECK_HIP(h->order.ensure(std::max<size_t>(nfiles, 1) * 4));
+        CHECK_HIP(h->counts.ensure(std::max<size_t>(nfiles, 1) * 8));
+        CHECK_HIP(h->tile_range.ensure(tr.size() * sizeof(uint2)));
+        CHECK_HIP(h->tile_meta.ensure(std::max<size_t>(h->ntiles, 1) * 4));
+        CHECK_HIP(h->slots.ensure(std::max<size_t>(h->ntiles, 1) * LISTCAP * sizeof(uint2)));
+        CHECK_HIP(h->zeroed.ensure((16 + (size_t)h->nwords * 8 + 15) & ~size_t(15)));
+        // dense tiles are rare (adversarial data); grow on demand in fetch()
+        uint32_t dcap = std::max<uint32_t>(64u, h->ntiles / 256u);
+        dcap = std::min<uint32_t>(dcap, std::max<uint32_t>(h->ntiles, 1u));
+        int32_t rc = ensure_dense(h, dcap);
+        if (rc) return rc;
+        if (!starts.empty())
+            CHECK_HIP(hipMemcpy(h->fstart.p, starts.data(), starts.size() * 8, hipMemcpyHostToDevice));
+        if (nfiles) {
+            CHECK_HIP(hipMemcpy(h->foff.p, file_off, nfiles * 8ull, hipMemcpyHostToDevice));
+            CHECK_HIP(hipMemcpy(h->flen.p, file_len, nfiles * 8ull, hipMemcpyHostToDevice));
+            CHECK_HIP(hipMemcpy(h->order.p, order.data(), nfiles * 4ull, hipMemcpyHostToDevice));
+        }
+        CHECK_HIP(hipMemcpy(h->tile_range.p, tr.data(), tr.size() * sizeof(uint2), hipMemcpyHostToDevice));
+        rc = upload_cut_tables(h);
+        if (rc) return rc;
+        h->planned = true;
+        return SYNCR_CDC_OK;
+    } catch (const std::bad_alloc &) {
+        return SYNCR_CDC_ENOMEM;
+    } catch (...) {
+        return SYNCR_CDC_EIO;
+    }
+}
+
+int32_t syncr_cdc_launch(syncr_cdc *h, const uint8_t *d_bytes, void *stream) {
+    if (!h) return SYNCR_CDC_EINVAL;
+    if (!h->planned) return SYNCR_CDC_ESTATE;
+    if (h->span && !d_bytes) return SYNCR_CDC_EINVAL;
+    if (((uintptr_t)d_bytes & 15u) != 0) return SYNCR_CDC_EINVAL;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    return do_launch(h, d_bytes, s);
+}
+
+int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap, uint64_t *per_file_count,
+                        uint64_t *n_out) {
+    if (!h) return SYNCR_CDC_EINVAL;
+    if (!h->launched) return SYNCR_CDC_ESTATE;
+    try {
+        CHECK_HIP(hipSetDevice(h->device));
+        for (int attempt = 0; attempt < 8; attempt++) {
+            CHECK_HIP(hipStreamSynchronize(h->last_stream));
+            uint32_t ctr[4];
+            CHECK_HIP(hipMemcpy(ctr, h->zeroed.p, 16, hipMemcpyDeviceToHost));
+            std::vector<uint64_t> counts(h->nfiles);
+            if (h->nfiles)
+                CHECK_HIP(hipMemcpy(counts.data(), h->counts.p, h->nfiles * 8ull, hipMemcpyDeviceToHost));
+            bool rerun = false;
+            if (ctr[CTR_FLAGS] & FLAG_DENSE_OVERFLOW) {
+                uint32_t want = std::min<uint32_t>(std::max<uint32_t>(h->ntiles, 1u),
+                                                   std::max<uint32_t>(ctr[CTR_DENSE] + ctr[CTR_DENSE] / 4 + 16, 2 * h->dense_cap));
+                int32_t rc = ensure_dense(h, want);
+                if (rc) return rc;
+                rerun = true;
+            }
+            if (ctr[CTR_FLAGS] & FLAG_CUT_OVERFLOW) {
+                for (uint32_t i = 0; i < h->nfiles; i++)
+                    if (counts[i] > h->h_cut_cap[i]) {
+                        if (counts[i] > 0xffffffffull) return SYNCR_CDC_ERANGE;
+                        h->h_cut_cap[i] = (uint32_t)counts[i];
+                    }
+                int32_t rc = upload_cut_tables(h);
+                if (rc) return rc;
+                rerun = true;
+            }
+            if (rerun) {
+                int32_t rc = do_launch(h, h->last_bytes, h->last_stream);
+                if (rc) return rc;
+                continue;
+            }
+            h->stats[0] = ctr[CTR_CANDS];
+            h->stats[1] = ctr[CTR_DENSE];
+            h->stats[2] = h->ntiles;
+            h->stats[3] = ctr[CTR_FLAGS];
+            uint64_t total = 0;
+            for (uint32_t i = 0; i < h->nfiles; i++) total += counts[i];
+            if (per_file_count)
+                for (uint32_t i = 0; i < h->nfiles; i++) per_file_count[i] = counts[i];
+            if (n_out) *n_out = total;
+            if (total > cap || (total && !out)) return SYNCR_CDC_ERANGE;
+            if (total) {
+                std::vector<DevCut> all(h->total_cut_cap);
+                CHECK_HIP(hipMemcpy(all.data(), h->cuts.p, h->total_cut_cap * sizeof(DevCut), hipMemcpyDeviceToHost));
+                uint64_t o = 0;
+                for (uint32_t i = 0; i < h->nfiles; i++) {
+                    const DevCut *src = all.data() + h->h_cut_base[i];
+                    for (uint64_t j = 0; j < counts[i]; j++, o++) {
+                        out[o].offset = src[j].offset;
+                        out[o].len = src[j].len;
+                        out[o].file = src[j].file;
+                    }
+                }
+            }
+            return SYNCR_CDC_OK;
+        }
+        return SYNCR_CDC_EIO;
+    } catch (const std::bad_alloc &) {
+        return SYNCR_CDC_ENOMEM;
+    } catch (...) {
+        return SYNCR_CDC_EIO;
+    }
+}
+
+int32_t syncr_cdc_chunk_batch_device(syncr_cdc *h, const uint8_t *d_bytes, uint64_t span,
+                                     const uint64_t *file_off, const uint64_t *file_len,
+                                     uint32_t nfiles, syncr_cut *out, uint64_t cap,
+                                     uint64_t *per_file_count, uint64_t *n_out, void *stream) {
+    int32_t rc = syncr_cdc_plan(h, file_off, file_len, nfiles, span);
+    if (rc) return rc;
+    rc = syncr_cdc_launch(h, d_bytes, stream);
+    if (rc) return rc;
+    return syncr_cdc_fetch(h, out, cap, per_file_count, n_out);
+}
+
+int32_t syncr_cdc_chunk_batch_host(syncr_cdc *h, const uint8_t *data, uint64_t span,
+                                   const uint64_t *file_off, const uint64_t *file_len,
+                                   uint32_t nfiles, syncr_cut *out, uint64_t cap,
+                                   uint64_t *per_file_count, uint64_t *n_out) {
+    if (!h || (span && !data)) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    CHECK_HIP(h->stage.ensure(std::max<uint64_t>(span, 16)));
+    if (span) CHECK_HIP(hipMemcpyAsync(h->stage.p, data, span, hipMemcpyHostToDevice, h->stream));
+    return syncr_cdc_chunk_batch_device(h, h->stage.as<uint8_t>(), span, file_off, file_len, nfiles,
+                                        out, cap, per_file_count, n_out, h->stream);
+}
+
+int32_t syncr_cdc_chunk_host(syncr_cdc *h, const uint8_t *data, uint64_t len, syncr_cut *out,
+                             uint64_t cap, uint64_t *n_out) {
+    const uint64_t off = 0;
+    uint64_t cnt = 0;
+    int32_t rc = syncr_cdc_chunk_batch_host(h, data, len, &off, &len, 1, out, cap, &cnt, n_out);
+    return rc;
+}
+
+int32_t syncr_cdc_device_alloc(syncr_cdc *h, uint64_t bytes, void **d_ptr) {
+    if (!h || !d_ptr) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    CHECK_HIP(hipMalloc(d_ptr, std::max<uint64_t>(bytes, 16)));
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_device_free(syncr_cdc *h, void *d_ptr) {
+    if (!h) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    CHECK_HIP(hipFree(d_ptr));
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_host_alloc_pinned(syncr_cdc *h, uint64_t bytes, void **ptr) {
+    if (!h || !ptr) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    CHECK_HIP(hipHostMalloc(ptr, std::max<uint64_t>(bytes, 16), hipHostMallocDefault));
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_host_free_pinned(syncr_cdc *h, void *ptr) {
+    if (!h) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipHostFree(ptr));
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_memcpy_h2d(syncr_cdc *h, void *d_dst, const void *src, uint64_t bytes, void *stream) {
+    if (!h || (bytes && (!d_dst || !src))) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    if (bytes) CHECK_HIP(hipMemcpyAsync(d_dst, src, bytes, hipMemcpyHostToDevice, s));
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_memcpy_d2h(syncr_cdc *h, void *dst, const void *d_src, uint64_t bytes, void *stream) {
+    if (!h || (bytes && (!dst || !d_src))) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    if (bytes) CHECK_HIP(hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost, s));
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_synchronize(syncr_cdc *h) {
+    if (!h) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    CHECK_HIP(hipDeviceSynchronize());
+    return SYNCR_CDC_OK;
+}
+
+void *syncr_cdc_stream(syncr_cdc *h) { return h ? (void *)h->stream : nullptr; }
+
+int32_t syncr_cdc_gen_corpus(syncr_cdc *h, uint8_t *d_bytes, const uint64_t *file_off,
+                             const uint64_t *file_len, const uint64_t *file_index,
+                             uint32_t nfiles, uint64_t first_index, void *stream) {
+    if (!h || (nfiles && (!file_off || !file_len || !d_bytes))) return SYNCR_CDC_EINVAL;
+    try {
+        CHECK_HIP(hipSetDevice(h->device));
+        hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+        // xorshift64 step as 64 GF(2) columns, squared GEN_JUMPS times
+        std::vector<uint64_t> jump((size_t)GEN_JUMPS * 64);
+        auto step = [](uint64_t x) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+        auto apply = [](const uint64_t *cols, uint64_t x) {
+            uint64_t y = 0;
+            for (int b = 0; b < 64; b++) if ((x >> b) & 1) y ^= cols[b];
+            return y;
+        };
+        for (int b = 0; b < 64; b++) jump[b] = step(1ull << b);
+        for (int k = 1; k < GEN_JUMPS; k++)
+            for (int b = 0; b < 64; b++)
+                jump[(size_t)k * 64 + b] = apply(&jump[(size_t)(k - 1) * 64], jump[(size_t)(k - 1) * 64 + b]);
+        std::vector<uint64_t> seg(nfiles + 1, 0);
+        for (uint32_t i = 0; i < nfiles; i++) {
+            if (file_len[i] >> GEN_JUMPS) return SYNCR_CDC_EINVAL;
+            seg[i + 1] = seg[i] + (file_len[i] + GEN_SEG - 1) / GEN_SEG;
+        }
+        const uint64_t nseg = seg[nfiles];
+        if (!nseg) return SYNCR_CDC_OK;
+        DevBuf dj, dfo, dfl, dsp, dfi;
+        int32_t rc = SYNCR_CDC_OK;
+        hipError_t e = hipSuccess;
+        do {
+            if ((e = dj.ensure(jump.size() * 8)) != hipSuccess) break;
+            if ((e = dfo.ensure(nfiles * 8ull)) != hipSuccess) break;
+            if ((e = dfl.ensure(nfiles * 8ull)) != hipSuccess) break;
+            if ((e = dsp.ensure((nfiles + 1) * 8ull)) != hipSuccess) break;
+            if (file_index) {
+                if ((e = dfi.ensure(nfiles * 8ull)) != hipSuccess) break;
+                if ((e = hipMemcpyAsync(dfi.p, file_index, nfiles * 8ull, hipMemcpyHostToDevice, s)) != hipSuccess) break;
+            }
+            if ((e = hipMemcpyAsync(dj.p, jump.data(), jump.size() * 8, hipMemcpyHostToDevice, s)) != hipSuccess) break;
+            if ((e = hipMemcpyAsync(dfo.p, file_off, nfiles * 8ull, hipMemcpyHostToDevice, s)) != hipSuccess) break;
+            if ((e = hipMemcpyAsync(dfl.p, file_len, nfiles * 8ull, hipMemcpyHostToDevice, s)) != hipSuccess) break;
+            if ((e = hipMemcpyAsync(dsp.p, seg.data(), (nfiles + 1) * 8ull, hipMemcpyHostToDevice, s)) != hipSuccess) break;
+            if ((e = launch_gen(d_bytes, dfo.as<uint64_t>(), dfl.as<uint64_t>(),
+                                file_index ? dfi.as<uint64_t>() : nullptr, dsp.as<uint64_t>(), nfiles,
+                                nseg, first_index, dj.as<uint64_t>(), s)) != hipSuccess) break;
+            e = hipStreamSynchronize(s);
+        } while (0);
+        if (e != hipSuccess) rc = hip_err(e);
+        dj.release(); dfo.release(); dfl.release(); dsp.release(); dfi.release();
+        return rc;
+    } catch (const std::bad_alloc &) {
+        return SYNCR_CDC_ENOMEM;
+    }
+}
+
+int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable) {
+    if (!h) return SYNCR_CDC_EINVAL;
+    (void)hipSetDevice(h->device);
+    drain_timing(h);
+    h->timing = enable != 0;
+    h->ms[0] = h->ms[1] = h->ms[2] = 0;
+    h->timed_launches = 0;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_kernel_times(syncr_cdc *h, double *ms3, uint64_t *launches) {
+    if (!h) return SYNCR_CDC_EINVAL;
+    (void)hipSetDevice(h->device);
+    drain_timing(h);
+    if (ms3) for (int k = 0; k < 3; k++) ms3[k] = h->ms[k];
+    if (launches) *launches = h->timed_launches;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_last_stats(syncr_cdc *h, uint64_t *stats4) {
+    if (!h || !stats4) return SYNCR_CDC_EINVAL;
+    for (int k = 0; k < 4; k++) stats4[k] = h->stats[k];
+    return SYNCR_CDC_OK;
+}
+
+}  // extern "C"

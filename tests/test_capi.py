@@ -1,0 +1,99 @@
+"""C-ABI library (libsyncr_cdc.so) checks that need no GPU: it builds, loads,
+exports every symbol include/syncr_cdc.h declares, and the host-side mirror
+behaves like the reference where no device is involved."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "syncr_cdc.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from syncr_amd import build as B
+    B.build()
+    import syncr_amd
+    return syncr_amd.library()
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(syncr_cdc_\w+)\s*\(", src)))
+
+
+def test_header_matches_python_binding():
+    import syncr_amd
+    assert sorted(syncr_amd.EXPORTED_SYMBOLS) == declared_functions()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    import syncr_amd
+    out = subprocess.run(["nm", "-D", "--defined-only", syncr_amd.library_path],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (syncr_cdc_\w+)", out))
+    missing = [s for s in declared_functions() if s not in exported]
+    assert not missing, missing
+    for s in declared_functions():
+        assert getattr(lib, s) is not None
+
+
+def test_gfx950_code_object(lib):
+    import syncr_amd
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list", "--type=o",
+                          f"--input={syncr_amd.library_path}"], capture_output=True, text=True)
+    blob = open(syncr_amd.library_path, "rb").read()
+    assert b"gfx950" in blob or "gfx950" in out.stdout
+
+
+def test_abi_and_defaults(lib):
+    import syncr_amd
+    assert lib.syncr_cdc_abi_version() == 1
+    p = syncr_amd.Params()
+    lib.syncr_cdc_default_params(ctypes.byref(p))
+    # src/chunking.rs:7-13 and the 2 MiB tokio read of file_operations.rs:738,776
+    assert (p.chunk_bits, p.flags, p.max_chunk, p.read_cap) == (20, 0, 16 << 20, 2 << 20)
+    assert syncr_amd.CHUNK_BITS == 20 and syncr_amd.MAX_CHUNK_SIZE == 16 * (1 << 20)
+    for code, text in ((0, b"ok"), (-22, b"invalid argument"), (-34, b"output capacity too small"),
+                       (-19, b"no HIP device"), (-5, b"HIP runtime error"), (-71, b"call out of order")):
+        assert lib.syncr_cdc_strerror(code) == text
+
+
+def test_no_device_is_loud(lib):
+    """Without a GPU the engine refuses (ENODEV) -- it never computes on the CPU."""
+    import syncr_amd
+    if syncr_amd.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    h = ctypes.c_void_p()
+    assert lib.syncr_cdc_open(0, None, ctypes.byref(h)) == -19
+    with pytest.raises(syncr_amd.SyncrCdcError):
+        syncr_amd.Chunker()
+
+
+def test_invalid_params_rejected(lib):
+    import syncr_amd
+    h = ctypes.c_void_p()
+    for bits, mx in ((0, 1 << 20), (32, 1 << 20), (20, 0), (20, 1 << 32)):
+        p = syncr_amd.Params(bits, 0, mx, 0)
+        assert lib.syncr_cdc_open(0, ctypes.byref(p), ctypes.byref(h)) in (-22, -19)
+    assert lib.syncr_cdc_open(0, None, None) == -22
+
+
+def test_compute_file_chunks_missing_file_is_empty(tmp_path):
+    """file_operations.rs:727-733: an unopenable file yields an empty list."""
+    import syncr_amd
+    assert syncr_amd.compute_file_chunks(str(tmp_path / "does-not-exist")) == []
+
+
+def test_product_never_touches_oracle():
+    """The product package must not import/load the test oracle."""
+    pkg = os.path.join(ROOT, "syncr_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith((".py", ".cpp", ".hip", ".h")):
+                src = open(os.path.join(dirpath, fn)).read()
+                assert "oracle" not in src.replace("oracle/", ""), fn

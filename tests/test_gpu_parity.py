@@ -1,0 +1,274 @@
+"""Parity of the HIP engine (libsyncr_cdc.so via the C ABI) with the CPU oracle.
+
+Bar: bit-exact cut offsets and counts (integer work).  Every test here runs the
+HIP kernels on the GPU; the oracle is only the checker."""
+import numpy as np
+import pytest
+
+import syncr_amd
+from golden_inputs import make_input
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+M = 1 << 20
+
+
+def ends_of(cuts: np.ndarray) -> list:
+    return (cuts["offset"].astype(np.uint64) + cuts["len"].astype(np.uint64)).tolist()
+
+
+def check_contiguous(cuts, n, mx):
+    off = 0
+    for o, ln, _ in cuts.tolist():
+        assert o == off and 1 <= ln <= mx
+        off += ln
+    assert off == n
+
+
+def oracle_ends(data, bits, mx, cap):
+    return (O.chunk_production(data, bits, mx, cap) if cap else O.chunk_ideal(data, bits, mx)).tolist()
+
+
+# --------------------------------------------------------------------------
+def test_golden_kats(kat_cases, chunkers):
+    for c in kat_cases:
+        data = make_input(c["recipe"])
+        ch = chunkers(c["chunk_bits"], c["max_chunk"], c["read_cap"])
+        cuts = ch.cut_array(data)
+        assert ends_of(cuts) == c["ends"], c["name"]
+        check_contiguous(cuts, data.size, c["max_chunk"])
+
+
+def test_reference_small_and_empty(chunkers):
+    ch = chunkers()
+    assert [(c.offset, c.size) for c in ch.chunk_bytes(b"small")] == [(0, 5)]   # protocol_list_test.rs:305-322
+    assert ch.chunk_bytes(b"") == []                                           # chunking_test.rs:37-43
+    assert syncr_amd.chunk_data(b"Small file") == [(0, 10)]                    # chunking_test.rs:26-34
+
+
+def test_compute_file_chunks_file(tmp_path, chunkers):
+    data = O.xorshift_bytes(99, 5 * M + 17)
+    p = tmp_path / "f.bin"
+    p.write_bytes(data.tobytes())
+    got = syncr_amd.compute_file_chunks(str(p), chunkers())
+    assert [c.offset + c.size for c in got] == O.chunk_production(data).tolist()
+
+
+def test_device_generator_matches_cpu(chunkers):
+    ch = chunkers()
+    lens = np.array([1, 4095, 4096, 4097, 0, 65536 + 3, 3 * M + 5, 77], np.uint64)
+    offs = np.zeros_like(lens)
+    offs[1:] = np.cumsum(lens)[:-1]
+    total = int(lens.sum())
+    buf = syncr_amd.DeviceBuffer(ch, total + 64)
+    try:
+        idx = np.array([5, 9, 2, 100000, 3, 17, 8, 12345], np.uint64)
+        buf.gen_corpus(offs, lens, indices=idx)
+        dev = buf.download(total)
+        for i in range(lens.size):
+            ref = O.xorshift_bytes(O.corpus_seed(int(idx[i])), int(lens[i]), discard=64)
+            assert np.array_equal(dev[int(offs[i]): int(offs[i] + lens[i])], ref), i
+    finally:
+        buf.free()
+
+
+def _batch_vs_oracle(ch, buf, offs, lens, bits, mx, cap):
+    res = ch.batch_arrays(buf, offs, lens)
+    for i, (o, n) in enumerate(zip(np.asarray(offs).tolist(), np.asarray(lens).tolist())):
+        f = buf[o: o + n]
+        assert ends_of(res[i]) == oracle_ends(f, bits, mx, cap), (i, o, n, bits, mx, cap)
+        assert (res[i]["file"] == i).all()
+
+
+@pytest.mark.parametrize("bits,mx,cap", [(20, 16 << 20, 2 << 20), (20, 16 << 20, 0), (13, 1 << 17, 0),
+                                         (13, 1 << 17, 65536), (8, 4096, 0), (16, 1 << 18, 5000),
+                                         (17, 1 << 19, 0), (31, 1 << 20, 0), (1, 100, 0), (4, 50, 7)])
+def test_many_small_files(chunkers, bits, mx, cap):
+    """Edge sizes: 0, 1, 62..66 bytes, run/tile boundaries (144 / 18432), odd offsets."""
+    rng = np.random.default_rng(bits * 1000 + cap)
+    sizes = [0, 1, 2, 62, 63, 64, 65, 66, 143, 144, 145, 18431, 18432, 18433, 36863, 100000, 0, 7]
+    sizes += rng.integers(0, 60000, 120).tolist()
+    lens = np.array(sizes, np.uint64)
+    offs = np.zeros_like(lens)
+    offs[1:] = np.cumsum(lens)[:-1]
+    data = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    data[: data.size // 3] &= 7                         # some low-entropy regions
+    _batch_vs_oracle(chunkers(bits, mx, cap), data, offs, lens, bits, mx, cap)
+
+
+def test_gaps_and_unsorted_table(chunkers):
+    """Files with holes between them and a table not sorted by offset."""
+    rng = np.random.default_rng(7)
+    n = 60
+    lens = rng.integers(0, 300000, n).astype(np.uint64)
+    gaps = rng.integers(0, 5000, n).astype(np.uint64)
+    offs = np.zeros(n, np.uint64)
+    acc = 0
+    for i in range(n):
+        acc += int(gaps[i])
+        offs[i] = acc
+        acc += int(lens[i])
+    data = rng.integers(0, 256, acc + 100, dtype=np.uint8)
+    perm = rng.permutation(n)
+    for bits, mx, cap in ((20, 16 << 20, 2 << 20), (12, 1 << 15, 0)):
+        _batch_vs_oracle(chunkers(bits, mx, cap), data, offs[perm], lens[perm], bits, mx, cap)
+
+
+def test_dense_tiles_low_entropy(chunkers):
+    """Data with >64 candidates per 18 KiB tile goes through the dense-bitmap path."""
+    data = O.xorshift_bytes(4242, 2 * M)
+    data = (data & 1).astype(np.uint8)
+    for bits, mx, cap in ((6, 4096, 0), (8, 1 << 12, 3000), (10, 1 << 14, 0)):
+        ch = chunkers(bits, mx, cap)
+        cuts = ch.cut_array(data)
+        assert ends_of(cuts) == oracle_ends(data, bits, mx, cap)
+
+
+def test_periodic_pattern_every_64(chunkers):
+    """A 64-byte period whose window hits: one G-candidate every 64 bytes."""
+    bits = 12
+    rng = np.random.default_rng(3)
+    for _ in range(2000):
+        pat = rng.integers(0, 256, 64, dtype=np.uint8)
+        rep = np.tile(pat, 2)
+        if O.chunk_ideal(rep, bits, 1 << 20).tolist() != [128]:
+            break
+    data = np.tile(pat, 40000)
+    for cap in (0, 1 << 16):
+        ch = chunkers(bits, 1 << 16, cap)
+        assert ends_of(ch.cut_array(data)) == oracle_ends(data, bits, 1 << 16, cap)
+
+
+def test_error_contract(chunkers):
+    import ctypes
+    L = syncr_amd.library()
+    ch = chunkers()
+    h = ch.handle
+    # launch before plan -> ESTATE on a fresh handle
+    fresh = syncr_amd.Chunker()
+    assert L.syncr_cdc_launch(fresh.handle, None, None) == -71
+    fresh.close()
+    # overlapping files -> EINVAL
+    offs = np.array([0, 10], np.uint64)
+    lens = np.array([20, 20], np.uint64)
+    assert L.syncr_cdc_plan(h, offs.ctypes.data, lens.ctypes.data, 2, 100) == -22
+    # file beyond span -> EINVAL
+    assert L.syncr_cdc_plan(h, offs.ctypes.data, lens.ctypes.data, 1, 10) == -22
+    # capacity too small -> ERANGE with the needed count
+    data = O.xorshift_bytes(5, 8 * M)
+    out = np.zeros(2, syncr_amd.CUT_DTYPE)
+    n = ctypes.c_uint64(0)
+    rc = L.syncr_cdc_chunk_host(h, data.ctypes.data, data.size, out.ctypes.data, 2, ctypes.byref(n))
+    assert rc == -34 and n.value == len(O.chunk_production(data))
+    # unaligned device pointer -> EINVAL
+    buf = syncr_amd.DeviceBuffer(ch, 4096)
+    ch.plan([0], [100], 100)
+    assert L.syncr_cdc_launch(h, buf.ptr + 1, None) == -22
+    buf.free()
+
+
+def test_uniform_corpus_device_resident(chunkers, uniform_corpus_golden):
+    """SURVEY §8d config 2 at full size (1 GiB), generated and chunked on the device."""
+    g = uniform_corpus_golden
+    ch = chunkers()
+    lens = np.full(g["files"], g["file_len"], np.uint64)
+    offs = np.arange(g["files"], dtype=np.uint64) * np.uint64(g["file_len"])
+    buf = syncr_amd.DeviceBuffer(ch, int(lens.sum()))
+    try:
+        buf.gen_corpus(offs, lens)
+        ch.plan(offs, lens, int(lens.sum()))
+        for _ in range(2):                      # repeated launches give identical results
+            ch.launch(buf.ptr)
+            res = ch.fetch()
+            assert [ends_of(r) for r in res] == g["ends"]
+    finally:
+        buf.free()
+
+
+def zipf_sizes(n=10000, seed=20251212):
+    z = np.random.default_rng(seed).zipf(1.5, n).astype(np.float64)
+    return np.minimum(4096.0 * z, float(128 * M)).astype(np.uint64)
+
+
+@pytest.mark.slow
+def test_zipf_corpus_full_size(chunkers):
+    """SURVEY §8d config 3 (10 000 Zipf files, 9.73 GiB) at full size: every
+    file's cuts vs the oracle in both modes."""
+    lens = zipf_sizes()
+    offs = np.zeros_like(lens)
+    offs[1:] = np.cumsum(lens)[:-1]
+    span = int(lens.sum())
+    assert abs(span / 2**30 - 9.73) < 0.02
+    for cap in (2 << 20, 0):
+        ch = chunkers(20, 16 << 20, cap)
+        buf = syncr_amd.DeviceBuffer(ch, span)
+        try:
+            buf.gen_corpus(offs, lens)
+            ch.plan(offs, lens, span)
+            ch.launch(buf.ptr)
+            res = ch.fetch()
+            host = buf.download(span)
+        finally:
+            buf.free()
+        ref = O.chunk_batch(host, offs, lens, read_cap=cap,
+                            mode=O.MODE_PRODUCTION if cap else O.MODE_IDEAL)
+        bad = [i for i in range(lens.size) if ends_of(res[i]) != ref[i].tolist()]
+        assert not bad, bad[:10]
+        del host
+
+
+@pytest.mark.slow
+def test_dedup_corpus(chunkers):
+    """SURVEY §8d config 5 (scaled to 200 variants of a 32 MiB base): bit-exact
+    and boundary-stable (most base cuts survive a small edit, shift-adjusted)."""
+    rng = np.random.default_rng(55)
+    base = O.xorshift_bytes(31337, 32 * M)
+    files, edits = [], []
+    for _ in range(200):
+        pos = int(rng.integers(0, base.size))
+        ln = int(rng.integers(1, 257))
+        kind = rng.choice(["overwrite", "overwrite", "insert", "delete"])
+        ins = rng.integers(0, 256, ln, dtype=np.uint8)
+        if kind == "overwrite":
+            f = base.copy(); f[pos:pos + ln] = ins[: max(0, min(ln, base.size - pos))]
+            delta = 0
+        elif kind == "insert":
+            f = np.concatenate([base[:pos], ins, base[pos:]]); delta = ln
+        else:
+            f = np.concatenate([base[:pos], base[pos + ln:]]); delta = -min(ln, base.size - pos)
+        files.append(f); edits.append((pos, delta))
+    lens = np.array([f.size for f in files], np.uint64)
+    offs = np.zeros_like(lens)
+    offs[1:] = np.cumsum(lens)[:-1]
+    buf = np.concatenate(files)
+    ch = chunkers()
+    res = ch.batch_arrays(buf, offs, lens)
+    ref = O.chunk_batch(buf, offs, lens)
+    base_cuts = set(O.chunk_production(base).tolist())
+    kept = []
+    for i in range(len(files)):
+        assert ends_of(res[i]) == ref[i].tolist(), i
+        pos, delta = edits[i]
+        adj = {e - delta if e > pos else e for e in ends_of(res[i])}
+        kept.append(len(adj & base_cuts) / len(base_cuts))
+    assert np.median(kept) >= 0.9
+
+
+def test_kernel_timing_api(chunkers):
+    ch = chunkers()
+    data_len = 64 * M
+    buf = syncr_amd.DeviceBuffer(ch, data_len)
+    try:
+        buf.gen_corpus([0], [data_len])
+        ch.plan([0], [data_len], data_len)
+        ch.set_timing(True)
+        for _ in range(3):
+            ch.launch(buf.ptr)
+        ms, n = ch.kernel_times()
+        ch.set_timing(False)
+        assert n == 3 and ms[0] > 0 and ms[2] > 0
+        ch.fetch()
+        st = ch.last_stats()
+        assert st["tiles"] == (data_len + 18431) // 18432 and st["flags"] == 0
+    finally:
+        buf.free()
