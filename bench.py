@@ -202,6 +202,7 @@ def main(argv=None):
 
     cuts = ch.fetch()
     stats = ch.last_stats()
+    engine_info = ch.info()
     ncuts = int(sum(c.size for c in cuts))
     covered = all(int(c["len"].sum()) == int(n) for c, n in zip(cuts, lens.tolist()))
 
@@ -236,6 +237,7 @@ def main(argv=None):
                 "parallelism": f"file-sharded x{world} (LPT), one HIP stream per GPU, no collective",
                 "cuts_rank0": ncuts, "coverage_ok_rank0": covered,
                 "candidates_rank0": int(stats["candidates"]), "dense_tiles_rank0": int(stats["dense_tiles"]),
+                "engine": engine_info,
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

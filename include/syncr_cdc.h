@@ -121,6 +121,9 @@ int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable);
 int32_t syncr_cdc_kernel_times(syncr_cdc *h, double *ms3, uint64_t *launches);
 /* Diagnostics of the last fetched launch: [candidates, dense_tiles, tiles, overflow]. */
 int32_t syncr_cdc_last_stats(syncr_cdc *h, uint64_t *stats4);
+/* Engine geometry: [run_bytes, tile_bytes, scan_grid, compute_units,
+ * scan_blocks_per_cu, lds_bytes_per_scan_block, device, abi_version]. */
+int32_t syncr_cdc_get_info(const syncr_cdc *h, uint64_t *info8);
 
 #ifdef __cplusplus
 }

@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "syncr_cdc_device_free", "syncr_cdc_host_alloc_pinned", "syncr_cdc_host_free_pinned",
     "syncr_cdc_memcpy_h2d", "syncr_cdc_memcpy_d2h", "syncr_cdc_synchronize", "syncr_cdc_stream",
     "syncr_cdc_gen_corpus", "syncr_cdc_set_timing", "syncr_cdc_kernel_times",
-    "syncr_cdc_last_stats",
+    "syncr_cdc_last_stats", "syncr_cdc_get_info",
 )
 
 ABI_VERSION = 1
@@ -112,6 +112,7 @@ def library():
             "syncr_cdc_set_timing": ([_vp, _i32], _i32),
             "syncr_cdc_kernel_times": ([_vp, ctypes.POINTER(ctypes.c_double), _pu64], _i32),
             "syncr_cdc_last_stats": ([_vp, _pu64], _i32),
+            "syncr_cdc_get_info": ([_vp, _pu64], _i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -258,6 +259,13 @@ class Chunker:
         st = (ctypes.c_uint64 * 4)()
         _check(library().syncr_cdc_last_stats(self._h, st), "syncr_cdc_last_stats")
         return {"candidates": st[0], "dense_tiles": st[1], "tiles": st[2], "flags": st[3]}
+
+    def info(self) -> dict:
+        v = (ctypes.c_uint64 * 8)()
+        _check(library().syncr_cdc_get_info(self._h, v), "syncr_cdc_get_info")
+        keys = ("run_bytes", "tile_bytes", "scan_grid", "compute_units", "scan_blocks_per_cu",
+                "lds_bytes_per_scan_block", "device", "abi_version")
+        return {k: int(x) for k, x in zip(keys, v)}
 
     def synchronize(self) -> None:
         _check(library().syncr_cdc_synchronize(self._h), "syncr_cdc_synchronize")

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <numeric>
@@ -49,17 +50,20 @@ struct syncr_cdc {
     syncr_cdc_params params{};
     KParams kp{};
     hipStream_t stream = nullptr;
+    int run = DEFAULT_RUN;          // scan geometry (bytes per lane-run)
+    uint32_t scan_grid = 0;         // persistent scan grid (CUs x resident blocks)
 
     // plan
     bool planned = false;
     uint32_t nfiles = 0, nstarts = 0, ntiles = 0, nwords = 0;
     uint64_t span = 0;
     uint32_t dense_cap = 0;
+    uint64_t cand_cap = 0;
     uint64_t total_cut_cap = 0;
     std::vector<uint64_t> h_foff, h_flen, h_cut_base;
     std::vector<uint32_t> h_cut_cap;
     DevBuf fstart, foff, flen, order, cut_base, cut_cap, tile_range, tile_meta, slots, zeroed,
-        dense_list, dense_bits, cuts, counts;
+        dense_list, dense_cnt, dense_bits, super_off, cand, cuts, counts;
 
     // launch
     bool launched = false;
@@ -127,6 +131,8 @@ Tables make_tables(syncr_cdc *h) {
     Tables t{};
     t.span = h->span;
     t.ntiles = h->ntiles;
+    t.tile = (uint32_t)tile_bytes(h->run);
+    t.nwords = h->nwords;
     t.nstarts = h->nstarts;
     t.fstart = h->fstart.as<uint64_t>();
     t.tile_range = h->tile_range.as<uint2>();
@@ -140,9 +146,14 @@ Tables make_tables(syncr_cdc *h) {
     t.slots = h->slots.as<uint2>();
     t.ctr = h->zeroed.as<uint32_t>();
     t.nonempty = reinterpret_cast<unsigned long long *>(h->zeroed.as<uint8_t>() + 16);
+    t.super_cnt = reinterpret_cast<uint32_t *>(h->zeroed.as<uint8_t>() + 16 + (size_t)h->nwords * 8);
+    t.super_off = h->super_off.as<uint64_t>();
     t.dense_list = h->dense_list.as<uint32_t>();
+    t.dense_cnt = h->dense_cnt.as<uint32_t>();
     t.dense_cap = h->dense_cap;
     t.dense_bits = h->dense_bits.as<uint32_t>();
+    t.cand = h->cand.as<uint64_t>();
+    t.cand_cap = h->cand_cap;
     t.cuts = h->cuts.as<DevCut>();
     t.counts = h->counts.as<uint64_t>();
     return t;
@@ -169,8 +180,19 @@ int32_t upload_cut_tables(syncr_cdc *h) {
 int32_t ensure_dense(syncr_cdc *h, uint32_t cap) {
     h->dense_cap = cap;
     CHECK_HIP(h->dense_list.ensure(std::max<size_t>(cap, 1) * 4));
-    CHECK_HIP(h->dense_bits.ensure(std::max<size_t>(cap, 1) * (size_t)DENSE_WORDS * 4));
+    CHECK_HIP(h->dense_cnt.ensure(std::max<size_t>(cap, 1) * 4));
+    CHECK_HIP(h->dense_bits.ensure(std::max<size_t>(cap, 1) * (size_t)(tile_bytes(h->run) / 32) * 4));
     return SYNCR_CDC_OK;
+}
+
+int32_t ensure_cand(syncr_cdc *h, uint64_t cap) {
+    h->cand_cap = cap;
+    CHECK_HIP(h->cand.ensure(std::max<uint64_t>(cap, 1) * 8));
+    return SYNCR_CDC_OK;
+}
+
+size_t zeroed_bytes(const syncr_cdc *h) {
+    return (16 + (size_t)h->nwords * 12 + 15) & ~size_t(15);
 }
 
 void drain_timing(syncr_cdc *h) {
@@ -189,17 +211,16 @@ void drain_timing(syncr_cdc *h) {
 int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     KParams kp = h->kp;
     Tables t = make_tables(h);
-    const size_t zbytes = 16 + (size_t)h->nwords * 8;
     PendingTiming pt{};
     if (h->timing) {
         if (h->pending.size() >= 256) drain_timing(h);
         for (int k = 0; k < 4; k++) CHECK_HIP(hipEventCreate(&pt.ev[k]));
     }
-    CHECK_HIP(hipMemsetAsync(h->zeroed.p, 0, (zbytes + 15) & ~size_t(15), s));
+    CHECK_HIP(hipMemsetAsync(h->zeroed.p, 0, zeroed_bytes(h), s));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[0], s));
-    CHECK_HIP(launch_scan(d_bytes, kp, t, s));
+    CHECK_HIP(launch_scan(h->run, h->scan_grid, d_bytes, kp, t, s));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[1], s));
-    CHECK_HIP(launch_dense(d_bytes, kp, t, s));
+    CHECK_HIP(launch_post(d_bytes, kp, t, s, nullptr));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[2], s));
     CHECK_HIP(launch_resolve(d_bytes, kp, t, s));
     if (h->timing) {
@@ -264,6 +285,18 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     h->device = device;
     h->params = prm;
     h->kp = make_kparams(prm);
+    if (const char *r = getenv("SYNCR_CDC_RUN")) {
+        const int v = atoi(r);
+        if (run_supported(v)) h->run = v;
+    }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+        cus = 256;
+    h->scan_grid = (uint32_t)(cus * scan_blocks_per_cu(h->run));
+    if (const char *g = getenv("SYNCR_CDC_SCAN_GRID")) {
+        const int v = atoi(g);
+        if (v > 0) h->scan_grid = (uint32_t)v;
+    }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return SYNCR_CDC_EIO;
@@ -279,7 +312,8 @@ void syncr_cdc_close(syncr_cdc *h) {
     drain_timing(h);
     DevBuf *bufs[] = {&h->fstart, &h->foff, &h->flen, &h->order, &h->cut_base, &h->cut_cap,
                       &h->tile_range, &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
-                      &h->dense_bits, &h->cuts, &h->counts, &h->stage};
+                      &h->dense_cnt, &h->dense_bits, &h->super_off, &h->cand, &h->cuts,
+                      &h->counts, &h->stage};
     for (DevBuf *b : bufs) b->release();
     (void)hipStreamDestroy(h->stream);
     delete h;
@@ -312,6 +346,7 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
             starts[j] = file_off[ne[j]];
             if (j && file_off[ne[j - 1]] + file_len[ne[j - 1]] > starts[j]) return SYNCR_CDC_EINVAL;
         }
+        const int TILE = tile_bytes(h->run);
         const uint64_t ntiles64 = (span + TILE - 1) / TILE;
         if (ntiles64 > 0x7fffffffull) return SYNCR_CDC_EINVAL;
         h->nfiles = nfiles;
@@ -350,11 +385,14 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         CHECK_HIP(h->tile_range.ensure(tr.size() * sizeof(uint2)));
         CHECK_HIP(h->tile_meta.ensure(std::max<size_t>(h->ntiles, 1) * 4));
         CHECK_HIP(h->slots.ensure(std::max<size_t>(h->ntiles, 1) * LISTCAP * sizeof(uint2)));
-        CHECK_HIP(h->zeroed.ensure((16 + (size_t)h->nwords * 8 + 15) & ~size_t(15)));
+        CHECK_HIP(h->zeroed.ensure(zeroed_bytes(h)));
+        CHECK_HIP(h->super_off.ensure(((size_t)h->nwords + 1) * 8));
         // dense tiles are rare (adversarial data); grow on demand in fetch()
         uint32_t dcap = std::max<uint32_t>(64u, h->ntiles / 256u);
         dcap = std::min<uint32_t>(dcap, std::max<uint32_t>(h->ntiles, 1u));
         int32_t rc = ensure_dense(h, dcap);
+        if (rc) return rc;
+        rc = ensure_cand(h, std::max<uint64_t>(4096, 2ull * h->ntiles));
         if (rc) return rc;
         if (!starts.empty())
             CHECK_HIP(hipMemcpy(h->fstart.p, starts.data(), starts.size() * 8, hipMemcpyHostToDevice));
@@ -394,6 +432,7 @@ int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap, uint64_t *pe
             CHECK_HIP(hipStreamSynchronize(h->last_stream));
             uint32_t ctr[4];
             CHECK_HIP(hipMemcpy(ctr, h->zeroed.p, 16, hipMemcpyDeviceToHost));
+            const uint64_t ncand = (uint64_t)ctr[CTR_CANDS_LO] | ((uint64_t)ctr[CTR_CANDS_HI] << 32);
             std::vector<uint64_t> counts(h->nfiles);
             if (h->nfiles)
                 CHECK_HIP(hipMemcpy(counts.data(), h->counts.p, h->nfiles * 8ull, hipMemcpyDeviceToHost));
@@ -405,7 +444,12 @@ int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap, uint64_t *pe
                 if (rc) return rc;
                 rerun = true;
             }
-            if (ctr[CTR_FLAGS] & FLAG_CUT_OVERFLOW) {
+            if (ctr[CTR_FLAGS] & FLAG_CAND_OVERFLOW) {
+                int32_t rc = ensure_cand(h, ncand + ncand / 8 + 1024);
+                if (rc) return rc;
+                rerun = true;
+            }
+            if (!rerun && (ctr[CTR_FLAGS] & FLAG_CUT_OVERFLOW)) {
                 for (uint32_t i = 0; i < h->nfiles; i++)
                     if (counts[i] > h->h_cut_cap[i]) {
                         if (counts[i] > 0xffffffffull) return SYNCR_CDC_ERANGE;
@@ -420,7 +464,7 @@ int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap, uint64_t *pe
                 if (rc) return rc;
                 continue;
             }
-            h->stats[0] = ctr[CTR_CANDS];
+            h->stats[0] = ncand;
             h->stats[1] = ctr[CTR_DENSE];
             h->stats[2] = h->ntiles;
             h->stats[3] = ctr[CTR_FLAGS];
@@ -617,3 +661,18 @@ int32_t syncr_cdc_last_stats(syncr_cdc *h, uint64_t *stats4) {
 }
 
 }  // extern "C"
+
+extern "C" int32_t syncr_cdc_get_info(const syncr_cdc *h, uint64_t *info8) {
+    if (!h || !info8) return SYNCR_CDC_EINVAL;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) cus = 0;
+    info8[0] = (uint64_t)h->run;
+    info8[1] = (uint64_t)tile_bytes(h->run);
+    info8[2] = h->scan_grid;
+    info8[3] = (uint64_t)cus;
+    info8[4] = (uint64_t)scan_blocks_per_cu(h->run);
+    info8[5] = (uint64_t)lds_wave_bytes(h->run);
+    info8[6] = (uint64_t)h->device;
+    info8[7] = SYNCR_CDC_ABI_VERSION;
+    return SYNCR_CDC_OK;
+}

@@ -7,25 +7,31 @@
 namespace cdc {
 
 // ---- scan geometry (see DESIGN.md "Scan kernel") -------------------------
-// A wave owns one tile of RUNS runs x RUN bytes; lane l rolls runs l and l+64
-// as the two 16-bit halves of packed registers.  RUN/16 is odd so the
-// per-lane ds_read_b128 of a run is bank-conflict free.
-constexpr int RUN = 144;                 // bytes rolled per (lane, half)
+// A wave owns a tile of RUNS runs x RUN bytes; lane l rolls runs l and l+64 as
+// the two 16-bit halves of packed registers.  RUN/16 is odd so that the
+// per-lane ds_read_b128 of a run is bank-conflict free.  RUN is a template
+// parameter of the scan kernel (tuned on MI355X).
 constexpr int RUNS = 128;                // runs per wave tile
-constexpr int TILE = RUN * RUNS;         // 18432 bytes per wave tile
 constexpr int HALO = 64;                 // window warm-up bytes before the tile
-constexpr int WAVES = 4;                 // waves (tiles) per 256-thread block
 constexpr int LISTCAP = 64;              // candidate slots per tile
-constexpr int LDS_WAVE = HALO + TILE + LISTCAP * 4 + 16;   // 18768 B, 16-aligned
-constexpr int LDS_BLOCK = LDS_WAVE * WAVES;                // 75072 B -> 2 blocks/CU
 constexpr uint32_t DENSE_BIT = 0x80000000u;
-constexpr int DENSE_WORDS = TILE / 32;   // bitmap words per dense tile (576)
-constexpr int DENSE_LANE_BYTES = TILE / 64;  // 288 positions per lane in the dense pass
 constexpr uint64_t NONE = ~0ull;
+constexpr int DEFAULT_RUN = 80;
+
+__host__ __device__ constexpr int tile_bytes(int run) { return run * RUNS; }
+__host__ __device__ constexpr int buf_bytes(int run) { return HALO + run * RUNS; }
+// LDS per wave: one tile landing buffer + 16 dirty-group slots (80 B) +
+// candidate list + counters
+__host__ __device__ constexpr int lds_wave_bytes(int run) { return buf_bytes(run) + 16 * 80 + LISTCAP * 4 + 16; }
 
 // ctr[] words (zeroed by the per-launch memset)
-enum { CTR_DENSE = 0, CTR_FLAGS = 1, CTR_CANDS = 2, CTR_PAD = 3 };
-enum { FLAG_DENSE_OVERFLOW = 1u, FLAG_CUT_OVERFLOW = 2u };
+enum { CTR_DENSE = 0, CTR_FLAGS = 1, CTR_CANDS_LO = 2, CTR_CANDS_HI = 3 };
+enum { FLAG_DENSE_OVERFLOW = 1u, FLAG_CUT_OVERFLOW = 2u, FLAG_CAND_OVERFLOW = 4u };
+
+// compacted candidate: bits 0..47 global position, 48..55 head fix-up (0..63),
+// bit 63 = fix-up known
+constexpr uint64_t CAND_POS_MASK = (1ull << 48) - 1;
+constexpr uint64_t CAND_KNOWN = 1ull << 63;
 
 struct KParams {
     uint32_t bits;     // chunk_bits
@@ -47,6 +53,8 @@ struct DevCut {        // == syncr_cut
 struct Tables {
     uint64_t span;                 // bytes [0, span) of d_bytes are addressable
     uint32_t ntiles;
+    uint32_t tile;                 // bytes per tile (= RUN * RUNS)
+    uint32_t nwords;               // ceil(ntiles / 64)
     uint32_t nstarts;              // non-empty files (sorted starts)
     const uint64_t *fstart;        // [nstarts] sorted file starts
     const uint2 *tile_range;       // [ntiles] {lo, hi} into fstart: starts in [t0-63, t0+TILE)
@@ -57,18 +65,27 @@ struct Tables {
     const uint32_t *cut_cap;       // [nfiles] output slots per file
     uint32_t *tile_meta;           // [ntiles] count or DENSE_BIT|pool index (valid iff nonempty bit)
     uint2 *slots;                  // [ntiles*LISTCAP] {tile-relative pos, head fix-up}
-    unsigned long long *nonempty;  // [ceil(ntiles/64)] tile has >=1 candidate
-    uint32_t *ctr;                 // [4]
+    unsigned long long *nonempty;  // [nwords] tile has >=1 candidate        (zeroed per launch)
+    uint32_t *super_cnt;           // [nwords] candidates per 64-tile group   (zeroed per launch)
+    uint64_t *super_off;           // [nwords+1] exclusive prefix of super_cnt
+    uint32_t *ctr;                 // [4]                                      (zeroed per launch)
     uint32_t *dense_list;          // [dense_cap] tile ids
+    uint32_t *dense_cnt;           // [dense_cap] candidates per dense tile
     uint32_t dense_cap;
-    uint32_t *dense_bits;          // [dense_cap*DENSE_WORDS] candidate bitmaps
+    uint32_t *dense_bits;          // [dense_cap * tile/32] candidate bitmaps
+    uint64_t *cand;                // [cand_cap] compacted sorted candidates
+    uint64_t cand_cap;
     DevCut *cuts;                  // [sum cut_cap]
     uint64_t *counts;              // [nfiles]
 };
 
 // launchers (cdc_kernels.hip)
-hipError_t launch_scan(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s);
-hipError_t launch_dense(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s);
+bool run_supported(int run);
+int scan_blocks_per_cu(int run);
+hipError_t launch_scan(int run, uint32_t grid, const uint8_t *d_bytes, const KParams &p, const Tables &t,
+                       hipStream_t s);
+hipError_t launch_post(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s,
+                       hipEvent_t after_dense);
 hipError_t launch_resolve(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s);
 hipError_t launch_gen(uint8_t *d_base, const uint64_t *d_foff, const uint64_t *d_flen,
                       const uint64_t *d_findex, const uint64_t *d_seg_prefix, uint32_t nfiles,

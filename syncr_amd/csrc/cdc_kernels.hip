@@ -11,8 +11,9 @@
 //   A chunk starting at s sees G exactly for p >= s+63; the 63 head positions
 //   need the window zeroed before s: a "head fix-up", precomputed per
 //   candidate (first chunk-local hit in [e+1, e+63]) or rolled on demand.
-//   cdc_resolve_kernel then walks the cuts of each file serially (one lane per
-//   file) applying MAX_CHUNK_SIZE and the tokio read-cap lookahead.
+//   Candidates are compacted into one sorted array (dense -> prefix ->
+//   gather), then cdc_resolve_kernel walks compute_file_chunks' loop for each
+//   file (one lane per file) applying MAX_CHUNK_SIZE and the tokio read cap.
 #include "cdc_internal.h"
 
 namespace cdc {
@@ -38,10 +39,49 @@ __device__ __forceinline__ uint32_t lower_bound_serial(const uint64_t *a, uint32
     return lo;
 }
 
+// LDS byte address of a generic pointer into dynamic shared memory.
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// Scalar (s_load) read of wave-uniform, kernel-invariant metadata.  A vector
+// load here would be waited with vmcnt(0), draining the in-flight tile DMA.
+__device__ __forceinline__ uint64_t sload_u64(const void *p) {
+    const uint64_t a = (uint64_t)p;
+    // readfirstlane returns int: go through uint32_t so the low half is not sign-extended
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const uint64_t u = ((uint64_t)hi << 32) | (uint64_t)lo;
+    uint64_t v;
+    asm volatile("s_nop 4\n\ts_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(u) : "memory");
+    return v;
+}
+
+template <int N> __device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// 16 B per lane, HBM -> LDS (M0 = wave-uniform LDS base; lane l lands at +16*l).
+// Written as inline asm so hipcc does not drain it with vmcnt(0) before the
+// ds_reads of the OTHER buffer; completion is tracked by hand (wait_vmcnt).
+__device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds)
+        : "memory");
+}
+
 // ---------------------------------------------------------------------------
 // Slow path: one run rolled byte by byte with file-start resets.  Used for the
 // (rare) runs whose windows straddle a file start.  `byte(q)` reads global
-// position q; positions before `q0` are treated as outside the window.
+// position q; positions before q0 = rs-64 are treated as outside the window.
 // ---------------------------------------------------------------------------
 template <class ByteFn, class HitFn>
 __device__ __forceinline__ void roll_with_resets(ByteFn byte, int64_t rs, int len,
@@ -66,19 +106,19 @@ __device__ __forceinline__ void roll_with_resets(ByteFn byte, int64_t rs, int le
     }
 }
 
-// First chunk-local hit in [e+1, e+63] for a chunk starting at e+1, as e+k -> k
-// (0 = none).  Bytes before e+1 are outside the fresh window, so no drops.
-__device__ __forceinline__ uint32_t head_fix(const uint8_t *data, uint64_t span, uint64_t e,
-                                             uint32_t mask) {
-    uint32_t S = 0, W = 0;
+// First chunk-local hit in [e+1, e+63] for a chunk starting at e+1, as k = hit-e
+// (0 = none).  `byte(k)` returns the byte at e+k.  No drops: the window is fresh.
+template <class ByteFn>
+__device__ __forceinline__ uint32_t head_fix(ByteFn byte, uint32_t kmax, uint32_t mask) {
+    uint32_t S = 0, W = 0, found = 0;
+#pragma unroll 9
     for (uint32_t k = 1; k <= 63; ++k) {
-        const uint64_t q = e + k;
-        if (q >= span) break;
-        S += data[q];
+        const uint32_t x = k <= kmax ? byte(k) : 0u;
+        S += x;
         W += S;
-        if (hit_exact(S, W, mask)) return k;
+        if (!found && k <= kmax && hit_exact(S, W, mask)) found = k;
     }
-    return 0;
+    return found;
 }
 
 __device__ __forceinline__ void record(uint32_t *wcount, uint32_t *wlist, uint32_t rel) {
@@ -87,174 +127,150 @@ __device__ __forceinline__ void record(uint32_t *wcount, uint32_t *wlist, uint32
 }
 
 // ---------------------------------------------------------------------------
-// Scan kernel.  One wave = one tile of 18 KiB.  Staging: coalesced 16-B loads
-// of [t0-64, t0+TILE) into the wave's LDS region.  Rolling: lane l holds the
-// 208-byte windows of runs l and l+64 in 104 VGPRs and rolls both as packed
-// u16 pairs: per byte pair 2 v_perm_b32 + 4 packed integer ops + 1 v_pk_min.
+// One tile of RUNS x RUN bytes.  The wave copies its two runs' bytes (plus the
+// 64-byte warm-up before each) from the LDS landing buffer into registers, so
+// the buffer can take the next tile's DMA while this tile is rolled.
+// Lane l rolls runs l and l+64 as the two 16-bit halves of packed registers.
+// Per byte pair: 1 v_perm_b32 builds the pair (A_j, B_j) once -- it is the new
+// byte at j and the dropped byte at j+64 -- then
+//   S += x - d      two VOP2 32-bit ops (carry-free: each half < 2^15, S >= d)
+//   tv = S*k + tv; tv = d*(-64k) + tv   two v_pk_mad_u16
+//   acc = min(acc, tv)                  one v_pk_min_u16
 // tv = ((s2+1)*k) mod 2^16 is zero exactly when the s2 half of the mask test
-// passes; the group minimum of tv flags the rare 16-byte groups that are
-// re-walked exactly (s1 half of the test included).
+// passes; a zero in a 16-byte group's minimum triggers an exact re-walk of
+// that group (s1 half of the test included).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void cdc_scan_kernel(const uint8_t *__restrict__ data,
-                                                          KParams P, Tables T) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const uint32_t tile = blockIdx.x * WAVES + wave;
-    if (tile >= T.ntiles) return;                         // whole wave
-    uint8_t *wl = smem + wave * LDS_WAVE;                 // [0,64) halo, [64, 64+TILE) tile
-    uint32_t *wlist = (uint32_t *)(wl + HALO + TILE);
-    uint32_t *wcount = wlist + LISTCAP;
-    const int64_t t0 = (int64_t)tile * TILE;
-    const int64_t span = (int64_t)T.span;
-    const uint2 trange = T.tile_range[tile];
+template <int RUN>
+__device__ __forceinline__ uint32_t pair_at(const uint32_t (&A)[(HALO + RUN) / 4],
+                                            const uint32_t (&B)[(HALO + RUN) / 4], int j) {
+    return __builtin_amdgcn_perm(B[j >> 2], A[j >> 2], 0x0C040C00u + (uint32_t)(j & 3) * 0x00010001u);
+}
 
-    // ---- stage [t0-64, t0+TILE) -> LDS (1156 x 16 B) ----
-    constexpr int NV = (HALO + TILE) / 16;
-    constexpr int NIT = (NV + 63) / 64;
-    {
-        uint4 v[NIT];
-        const bool interior = (t0 >= HALO) && (t0 + TILE <= span);
-        if (interior) {
-            const uint4 *src = (const uint4 *)(data + t0 - HALO);
+// Dirty-group side slots (LDS, per wave): a lane whose 16-byte group minimum
+// hits zero stores that group's bytes and entry state here; they are re-walked
+// exactly after the roll.  Overflow hands the tile to the exact dense pass.
+constexpr int DIRTYCAP = 16;
+struct DirtySlot {             // 80 bytes
+    uint4 xa, da, xb, db;      // new / dropped bytes of the group, runs A and B
+    uint32_t S0, T0;           // packed state before the group
+    uint32_t rel;              // tile-relative position of the group's first byte (run A)
+    uint32_t flags;            // bit0: check A, bit1: check B
+};
+
+template <int RUN>
+__device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
+                                          const uint32_t (&B)[(HALO + RUN) / 4], const KParams &P,
+                                          int lane, bool recA, bool recB, uint32_t *dcount,
+                                          DirtySlot *dslots) {
+    // closed-form window sums at run start - 1 (weights 64..1, oldest first)
+    uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
 #pragma unroll
-            for (int it = 0; it < NIT; ++it) {
-                const int vi = it * 64 + lane;
-                v[it] = (it < NIT - 1 || vi < NV) ? src[vi] : make_uint4(0, 0, 0, 0);
-            }
-        } else {
-#pragma unroll
-            for (int it = 0; it < NIT; ++it) {
-                const int vi = it * 64 + lane;
-                const int64_t g = t0 - HALO + (int64_t)vi * 16;
-                uint4 r = make_uint4(0, 0, 0, 0);
-                if (vi < NV && g >= 0 && g < span) {
-                    if (g + 16 <= span) {
-                        r = *(const uint4 *)(data + g);
-                    } else {
-                        uint32_t w[4] = {0, 0, 0, 0};
-                        for (int b = 0; b < 16 && g + b < span; ++b)
-                            w[b >> 2] |= (uint32_t)data[g + b] << (8 * (b & 3));
-                        r = make_uint4(w[0], w[1], w[2], w[3]);
-                    }
-                }
-                v[it] = r;
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int vi = it * 64 + lane;
-            if (it < NIT - 1 || vi < NV) *(uint4 *)(wl + vi * 16) = v[it];
-        }
+    for (int m = 0; m < 16; ++m) {
+        const uint32_t w = 0x3D3E3F40u - 0x04040404u * (uint32_t)m;
+        SA = __builtin_amdgcn_udot4(A[m], 0x01010101u, SA, false);
+        WA = __builtin_amdgcn_udot4(A[m], w, WA, false);
+        SB = __builtin_amdgcn_udot4(B[m], 0x01010101u, SB, false);
+        WB = __builtin_amdgcn_udot4(B[m], w, WB, false);
     }
-    if (lane == 0) *wcount = 0u;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-
-    // ---- which of my runs straddle a file start (rare) ----
-    const int64_t rsA = t0 + (int64_t)lane * RUN;
-    const int64_t rsB = t0 + (int64_t)(lane + 64) * RUN;
-    bool slowA = false, slowB = false;
-    if (trange.y > trange.x) {                            // wave-uniform
-        uint32_t j = lower_bound_serial(T.fstart, trange.x, trange.y, rsA - 62);
-        slowA = j < trange.y && (int64_t)T.fstart[j] <= rsA + RUN - 1;
-        j = lower_bound_serial(T.fstart, trange.x, trange.y, rsB - 62);
-        slowB = j < trange.y && (int64_t)T.fstart[j] <= rsB + RUN - 1;
-    }
-    const int64_t lim_rel = span - t0;                    // positions >= span are not bytes
-    const bool recA = !slowA, recB = !slowB;
-
-    // ---- fast path: both runs packed ----
-    {
-        uint32_t A[52], B[52];
-        const uint4 *la = (const uint4 *)(wl + lane * RUN);          // = run start - 64
-        const uint4 *lb = (const uint4 *)(wl + (lane + 64) * RUN);
+    uint32_t S = SA | (SB << 16);
+    const uint32_t tA = ((124993u + WA) * P.k) & 0xffffu;
+    const uint32_t tB = ((124993u + WB) * P.k) & 0xffffu;
+    u16x2 Tv = as_u16x2(tA | (tB << 16));
+    const u16x2 kk = as_u16x2(P.kk), km = as_u16x2(P.kmv);
+    const uint32_t want = (recA ? 1u : 0u) | (recB ? 2u : 0u);
 #pragma unroll
-        for (int q = 0; q < 13; ++q) {
-            const uint4 a = la[q], b = lb[q];
-            A[4 * q + 0] = a.x; A[4 * q + 1] = a.y; A[4 * q + 2] = a.z; A[4 * q + 3] = a.w;
-            B[4 * q + 0] = b.x; B[4 * q + 1] = b.y; B[4 * q + 2] = b.z; B[4 * q + 3] = b.w;
+    for (int g = 0; g < RUN / 16; ++g) {
+        const uint32_t S0 = S;
+        const u16x2 T0 = Tv;
+        u16x2 acc = as_u16x2(0xffffffffu);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const int i = g * 16 + jj;
+            const uint32_t x = pair_at<RUN>(A, B, HALO + i), d = pair_at<RUN>(A, B, i);
+            S = S + x - d;
+            Tv = as_u16x2(S) * kk + Tv;
+            Tv = as_u16x2(d) * km + Tv;
+            acc = __builtin_elementwise_min(acc, Tv);
         }
-        // closed-form window sums at run start - 1 (weights 64..1, oldest first)
-        uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            const uint32_t w = 0x3D3E3F40u - 0x04040404u * (uint32_t)m;
-            SA = __builtin_amdgcn_udot4(A[m], 0x01010101u, SA, false);
-            WA = __builtin_amdgcn_udot4(A[m], w, WA, false);
-            SB = __builtin_amdgcn_udot4(B[m], 0x01010101u, SB, false);
-            WB = __builtin_amdgcn_udot4(B[m], w, WB, false);
-        }
-        u16x2 S = as_u16x2(SA | (SB << 16));
-        const uint32_t tA = ((124993u + WA) * P.k) & 0xffffu;
-        const uint32_t tB = ((124993u + WB) * P.k) & 0xffffu;
-        u16x2 Tv = as_u16x2(tA | (tB << 16));
-        const u16x2 kk = as_u16x2(P.kk), km = as_u16x2(P.kmv);
-        const uint8_t *ba = wl + lane * RUN, *bb = wl + (lane + 64) * RUN;
-
-#pragma unroll
-        for (int g = 0; g < RUN / 16; ++g) {
-            const u16x2 S0 = S, T0 = Tv;
-            u16x2 acc = as_u16x2(0xffffffffu);
-#pragma unroll
-            for (int jj = 0; jj < 16; ++jj) {
-                const int i = g * 16 + jj;
-                const uint32_t sel = 0x0C040C00u + (uint32_t)(i & 3) * 0x00010001u;
-                const u16x2 x = as_u16x2(__builtin_amdgcn_perm(B[16 + (i >> 2)], A[16 + (i >> 2)], sel));
-                const u16x2 d = as_u16x2(__builtin_amdgcn_perm(B[i >> 2], A[i >> 2], sel));
-                S = S + x - d;
-                Tv = S * kk + Tv;
-                Tv = d * km + Tv;
-                acc = __builtin_elementwise_min(acc, Tv);
-            }
-            const uint32_t a = as_u32(acc);
-            const bool z = ((a & 0xffffu) == 0u) | ((a >> 16) == 0u);
-            if (__builtin_expect(__ballot(z) != 0ull, 0)) {
-                if (z) {
-                    // exact re-walk of this 16-byte group (bytes re-read from LDS)
-                    u16x2 s = S0, t = T0;
-                    for (int jj = 0; jj < 16; ++jj) {
-                        const int i = g * 16 + jj;
-                        const u16x2 x = {ba[64 + i], bb[64 + i]};
-                        const u16x2 d = {ba[i], bb[i]};
-                        s = s + x - d;
-                        t = s * kk + t;
-                        t = d * km + t;
-                        const int rA = lane * RUN + i, rB = (lane + 64) * RUN + i;
-                        if (recA && t.x == 0 && ((1984u + s.x) & P.m1) == P.m1 && rA < lim_rel)
-                            record(wcount, wlist, (uint32_t)rA);
-                        if (recB && t.y == 0 && ((1984u + s.y) & P.m1) == P.m1 && rB < lim_rel)
-                            record(wcount, wlist, (uint32_t)rB);
-                    }
+        const uint32_t a = as_u32(acc);
+        const uint32_t zf = (((a & 0xffffu) == 0u) ? 1u : 0u) | (((a >> 16) == 0u) ? 2u : 0u);
+        const bool z = (zf & want) != 0u;
+        if (__builtin_expect(__ballot(z) != 0ull, 0)) {
+            if (z) {
+                const uint32_t idx = atomicAdd(dcount, 1u);
+                if (idx < (uint32_t)DIRTYCAP) {
+                    DirtySlot &ds = dslots[idx];
+                    ds.xa = make_uint4(A[16 + 4 * g], A[17 + 4 * g], A[18 + 4 * g], A[19 + 4 * g]);
+                    ds.da = make_uint4(A[4 * g], A[1 + 4 * g], A[2 + 4 * g], A[3 + 4 * g]);
+                    ds.xb = make_uint4(B[16 + 4 * g], B[17 + 4 * g], B[18 + 4 * g], B[19 + 4 * g]);
+                    ds.db = make_uint4(B[4 * g], B[1 + 4 * g], B[2 + 4 * g], B[3 + 4 * g]);
+                    ds.S0 = S0;
+                    ds.T0 = as_u32(T0);
+                    ds.rel = (uint32_t)(lane * RUN + g * 16);
+                    ds.flags = zf & want;
                 }
             }
         }
     }
+}
 
-    // ---- slow path for runs straddling a file start ----
-    if (slowA || slowB) {
-        const uint8_t *wlc = wl;
-        auto byte = [&](int64_t q) -> uint32_t { return wlc[q - t0 + HALO]; };
-        if (slowA)
-            roll_with_resets(byte, rsA, RUN, T.fstart, trange.x, trange.y, P.mask, [&](int64_t q) {
-                if (q - t0 < lim_rel) record(wcount, wlist, (uint32_t)(q - t0));
-            });
-        if (slowB)
-            roll_with_resets(byte, rsB, RUN, T.fstart, trange.x, trange.y, P.mask, [&](int64_t q) {
-                if (q - t0 < lim_rel) record(wcount, wlist, (uint32_t)(q - t0));
-            });
+// Exact re-walk of the dirty groups (one lane per slot, bytes from LDS).
+template <int RUN>
+__device__ __forceinline__ void rewalk_dirty(const KParams &P, int lane, uint32_t nd,
+                                             const DirtySlot *dslots, int64_t lim_rel,
+                                             uint32_t *wcount, uint32_t *wlist) {
+    if ((uint32_t)lane >= nd) return;
+    const DirtySlot &ds = dslots[lane];
+    const uint8_t *xa = (const uint8_t *)&ds.xa, *da = (const uint8_t *)&ds.da;
+    const uint8_t *xb = (const uint8_t *)&ds.xb, *db = (const uint8_t *)&ds.db;
+    const u16x2 kk = as_u16x2(P.kk), km = as_u16x2(P.kmv);
+    uint32_t s = ds.S0;
+    u16x2 t = as_u16x2(ds.T0);
+    const uint32_t fl = ds.flags;
+    const uint32_t relA = ds.rel, relB = ds.rel + 64u * RUN;
+    for (int jj = 0; jj < 16; ++jj) {
+        const uint32_t x = (uint32_t)xa[jj] | ((uint32_t)xb[jj] << 16);
+        const uint32_t d = (uint32_t)da[jj] | ((uint32_t)db[jj] << 16);
+        s = s + x - d;
+        t = as_u16x2(s) * kk + t;
+        t = as_u16x2(d) * km + t;
+        if ((fl & 1u) && t.x == 0 && ((1984u + (s & 0xffffu)) & P.m1) == P.m1 && (int64_t)(relA + jj) < lim_rel)
+            record(wcount, wlist, relA + jj);
+        if ((fl & 2u) && t.y == 0 && ((1984u + (s >> 16)) & P.m1) == P.m1 && (int64_t)(relB + jj) < lim_rel)
+            record(wcount, wlist, relB + jj);
     }
+}
 
-    // ---- publish this tile's candidates (sorted) ----
+// First chunk-local hit in [e+1, e+63] from global memory (all loads issued up front).
+__device__ __forceinline__ uint32_t head_fix_global(const uint8_t *data, uint64_t span, uint64_t e,
+                                                    uint32_t mask) {
+    uint32_t x[63];
+#pragma unroll
+    for (int k = 0; k < 63; ++k) x[k] = (e + 1 + k < span) ? data[e + 1 + k] : 0u;
+    uint32_t S = 0, W = 0, found = 0;
+#pragma unroll
+    for (int k = 0; k < 63; ++k) {
+        S += x[k];
+        W += S;
+        if (!found && e + 1 + k < span && hit_exact(S, W, mask)) found = (uint32_t)k + 1;
+    }
+    return found;
+}
+
+// Publish this tile's candidates (sorted, with head fix-ups) or mark it dense.
+__device__ __forceinline__ void publish_tile(const uint8_t *__restrict__ data, const KParams &P,
+                                             const Tables &T, uint32_t tile, int64_t t0,
+                                             uint32_t *wlist, uint32_t *wcount, int lane,
+                                             bool force_dense) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    const uint32_t n = __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)wcount);
-    if (n == 0u) return;
-    if (lane == 0) {
-        atomicOr(&T.nonempty[tile >> 6], 1ull << (tile & 63));
-        atomicAdd(&T.ctr[CTR_CANDS], n);
-    }
-    if (n > (uint32_t)LISTCAP) {
+    // LDS-typed read: a generic (flat) read would wait vmcnt(0) on the tile DMA.
+    const uint32_t n = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)wcount, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WAVEFRONT));
+    if (n == 0u && !force_dense) return;
+    if (lane == 0) atomicOr(&T.nonempty[tile >> 6], 1ull << (tile & 63));
+    if (n > (uint32_t)LISTCAP || force_dense) {
         if (lane == 0) {
             const uint32_t idx = atomicAdd(&T.ctr[CTR_DENSE], 1u);
             if (idx < T.dense_cap) {
@@ -271,129 +287,304 @@ __global__ __launch_bounds__(256, 2) void cdc_scan_kernel(const uint8_t *__restr
     uint32_t rank = 0;
     for (uint32_t m = 0; m < n; ++m) rank += wlist[m] < e;
     if ((uint32_t)lane < n) {
-        const uint32_t fix = head_fix(data, T.span, (uint64_t)t0 + e, P.mask);
+        const uint32_t fix = head_fix_global(data, T.span, (uint64_t)t0 + e, P.mask);
         T.slots[(size_t)tile * LISTCAP + rank] = make_uint2(e, fix);
     }
-    if (lane == 0) T.tile_meta[tile] = n;
+    if (lane == 0) {
+        T.tile_meta[tile] = n;
+        atomicAdd(&T.super_cnt[tile >> 6], n);
+    }
+}
+
+// 16 B per lane from a wave-uniform SGPR base + per-lane VGPR offset into LDS.
+__device__ __forceinline__ void dma16_s(uint32_t voff, uint64_t sbase, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 4\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(lds)
+        : "memory");
+}
+
+template <int RUN>
+__device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, uint32_t tile,
+                                           uint32_t lds_buf, int lane) {
+    constexpr int BUF = buf_bytes(RUN);
+    constexpr int NDMA = (BUF + 1023) / 1024;
+    const int64_t base = (int64_t)tile * tile_bytes(RUN) - HALO;
+    if (base >= 0 && (uint64_t)base + BUF <= span) {      // interior tile: SGPR base + lane*16
+        const uint64_t b = (uint64_t)(data + base);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+        const uint64_t ub = ((uint64_t)hi << 32) | lo;
+#pragma unroll
+        for (int i = 0; i < NDMA; ++i) {
+            if (i < NDMA - 1 || i * 1024 + lane * 16 < BUF)
+                dma16_s((uint32_t)lane * 16u, ub + (uint64_t)i * 1024u, lds_buf + (uint32_t)(i * 1024));
+        }
+        return;
+    }
+    // Edge tiles: out-of-range vectors are clamped to a valid one; their bytes
+    // only feed positions outside [0, span) or before a file start (never recorded).
+    const int64_t last = (int64_t)((span - 1) & ~15ull);
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) {
+        const int off = i * 1024 + lane * 16;
+        int64_t g = base + off;
+        g = g < 0 ? 0 : (g > last ? last : g);
+        if (i < NDMA - 1 || off < BUF) dma16(data + g, lds_buf + (uint32_t)(i * 1024));
+    }
 }
 
 // ---------------------------------------------------------------------------
-// Dense tiles (more than LISTCAP candidates, i.e. adversarial / low-entropy
-// data at small chunk_bits): recompute G for the whole tile into a bitmap.
-// Lane l covers 288 positions = 9 bitmap words.  Grid-stride over the list.
+// Scan kernel: persistent, one wave per block, one LDS landing buffer.  Per
+// tile: wait for its DMA, copy the runs into registers, hand the buffer to the
+// next tile's DMA (unless a file start needs the bytes in LDS for the slow
+// path), then roll.  The DMA latency hides under the rolling of this tile and
+// under the other resident waves.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict__ data,
-                                                       KParams P, Tables T) {
+template <int RUN>
+__global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P,
+                                                      Tables T) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int BUF = buf_bytes(RUN);
+    constexpr int TILE = tile_bytes(RUN);
+    constexpr int NQ = (HALO + RUN) / 16;
+    const int lane = threadIdx.x;
+    uint8_t *wl = smem;
+    DirtySlot *dslots = (DirtySlot *)(smem + BUF);
+    uint32_t *wlist = (uint32_t *)(smem + BUF + DIRTYCAP * sizeof(DirtySlot));
+    uint32_t *wcount = wlist + LISTCAP;
+    uint32_t *dcount = wcount + 1;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
+    const uint32_t stride = gridDim.x;
+    uint32_t tile = blockIdx.x;
+    if (tile >= T.ntiles) return;
+    const int64_t span = (int64_t)T.span;
+    issue_tile<RUN>(data, T.span, tile, lds0, lane);
+    for (; tile < T.ntiles; tile += stride) {
+        const uint32_t next = tile + stride;
+        const uint64_t tr64 = sload_u64(T.tile_range + tile);       // scalar: no vmcnt
+        const uint2 trange = make_uint2((uint32_t)tr64, (uint32_t)(tr64 >> 32));
+        const int64_t t0 = (int64_t)tile * TILE;
+        if (lane == 0) { *wcount = 0u; *dcount = 0u; }
+        wait_vmcnt<0>();                                             // this tile has landed
+        uint32_t A[NQ * 4], B[NQ * 4];
+        {
+            const uint4 *la = (const uint4 *)(wl + lane * RUN);          // = run start - 64
+            const uint4 *lb = (const uint4 *)(wl + (lane + 64) * RUN);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const uint4 a = la[q], b = lb[q];
+                A[4 * q + 0] = a.x; A[4 * q + 1] = a.y; A[4 * q + 2] = a.z; A[4 * q + 3] = a.w;
+                B[4 * q + 0] = b.x; B[4 * q + 1] = b.y; B[4 * q + 2] = b.z; B[4 * q + 3] = b.w;
+            }
+        }
+        const bool starts = trange.y > trange.x;                     // wave-uniform
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");           // runs are in registers
+        if (!starts && next < T.ntiles) issue_tile<RUN>(data, T.span, next, lds0, lane);
+
+        // which of my runs straddle a file start (rare; bytes stay in LDS)
+        const int64_t rsA = t0 + (int64_t)lane * RUN;
+        const int64_t rsB = t0 + (int64_t)(lane + 64) * RUN;
+        bool slowA = false, slowB = false;
+        if (starts) {
+            uint32_t j = lower_bound_serial(T.fstart, trange.x, trange.y, rsA - 62);
+            slowA = j < trange.y && (int64_t)T.fstart[j] <= rsA + RUN - 1;
+            j = lower_bound_serial(T.fstart, trange.x, trange.y, rsB - 62);
+            slowB = j < trange.y && (int64_t)T.fstart[j] <= rsB + RUN - 1;
+        }
+        const int64_t lim_rel = span - t0;                           // positions >= span are not bytes
+        roll_fast<RUN>(A, B, P, lane, !slowA, !slowB, dcount, dslots);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const uint32_t nd = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)dcount, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WAVEFRONT));
+        if (nd) rewalk_dirty<RUN>(P, lane, nd < (uint32_t)DIRTYCAP ? nd : (uint32_t)DIRTYCAP, dslots,
+                                  lim_rel, wcount, wlist);
+        if (slowA || slowB) {
+            auto byte = [&](int64_t q) -> uint32_t { return wl[q - t0 + HALO]; };
+            auto rec = [&](int64_t q) {
+                if (q - t0 < lim_rel) record(wcount, wlist, (uint32_t)(q - t0));
+            };
+            if (slowA) roll_with_resets(byte, rsA, RUN, T.fstart, trange.x, trange.y, P.mask, rec);
+            if (slowB) roll_with_resets(byte, rsB, RUN, T.fstart, trange.x, trange.y, P.mask, rec);
+        }
+        if (starts && next < T.ntiles) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // slow-path LDS reads done
+            issue_tile<RUN>(data, T.span, next, lds0, lane);
+        }
+        publish_tile(data, P, T, tile, t0, wlist, wcount, lane, nd > (uint32_t)DIRTYCAP);
+    }
+}
+// ---------------------------------------------------------------------------
+// Dense tiles (more than LISTCAP candidates: low-entropy / adversarial data at
+// small chunk_bits): recompute G for the whole tile into a bitmap, count it.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict__ data, KParams P,
+                                                       Tables T) {
     const uint32_t nd = min(T.ctr[CTR_DENSE], T.dense_cap);
     const int lane = threadIdx.x;
+    const int per_lane = (int)T.tile / 64;             // positions per lane (multiple of 32)
+    const int words_lane = per_lane / 32;
     for (uint32_t idx = blockIdx.x; idx < nd; idx += gridDim.x) {
         const uint32_t tile = T.dense_list[idx];
-        const int64_t t0 = (int64_t)tile * TILE;
-        const int64_t rs = t0 + (int64_t)lane * DENSE_LANE_BYTES;
+        const int64_t t0 = (int64_t)tile * T.tile;
+        const int64_t rs = t0 + (int64_t)lane * per_lane;
         const int64_t span = (int64_t)T.span;
-        uint32_t words[DENSE_LANE_BYTES / 32];
-#pragma unroll
-        for (int w = 0; w < DENSE_LANE_BYTES / 32; ++w) words[w] = 0u;
+        uint32_t *out = T.dense_bits + (size_t)idx * (T.tile / 32) + lane * words_lane;
+        for (int w = 0; w < words_lane; ++w) out[w] = 0u;
         auto byte = [&](int64_t q) -> uint32_t { return (q >= 0 && q < span) ? data[q] : 0u; };
         const uint32_t lo = lower_bound_serial(T.fstart, 0, T.nstarts, rs - 64);
-        const uint32_t hi = lower_bound_serial(T.fstart, lo, T.nstarts, rs + DENSE_LANE_BYTES);
-        roll_with_resets(byte, rs, DENSE_LANE_BYTES, T.fstart, lo, hi, P.mask, [&](int64_t q) {
+        const uint32_t hi = lower_bound_serial(T.fstart, lo, T.nstarts, rs + per_lane);
+        uint32_t word = 0, cnt = 0;
+        int cur = 0;
+        roll_with_resets(byte, rs, per_lane, T.fstart, lo, hi, P.mask, [&](int64_t q) {
             if (q < span) {
                 const int r = (int)(q - rs);
-                words[r >> 5] |= 1u << (r & 31);
+                if ((r >> 5) != cur) { out[cur] = word; word = 0; cur = r >> 5; }
+                word |= 1u << (r & 31);
+                ++cnt;
             }
         });
-        uint32_t *out = T.dense_bits + (size_t)idx * DENSE_WORDS + lane * (DENSE_LANE_BYTES / 32);
-#pragma unroll
-        for (int w = 0; w < DENSE_LANE_BYTES / 32; ++w) out[w] = words[w];
+        out[cur] |= word;
+        for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if (lane == 0) {
+            T.dense_cnt[idx] = cnt;
+            atomicAdd(&T.super_cnt[tile >> 6], cnt);
+        }
     }
 }
 
-// ---------------------------------------------------------------------------
-// Resolve: one lane per file walks compute_file_chunks' loop over candidates.
-// ---------------------------------------------------------------------------
-struct Cand {
-    uint64_t pos;
-    uint32_t fix;
-    bool fix_known;
-};
+// Exclusive prefix of the per-64-tile candidate counts (one block).
+__global__ __launch_bounds__(1024) void cdc_prefix_kernel(Tables T) {
+    __shared__ uint64_t part[1024];
+    const uint32_t n = T.nwords, t = threadIdx.x;
+    const uint32_t per = (n + 1023) / 1024;
+    const uint32_t a = min(n, t * per), b = min(n, a + per);
+    uint64_t s = 0;
+    for (uint32_t i = a; i < b; ++i) s += T.super_cnt[i];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint64_t v = t >= off ? part[t - off] : 0ull;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - s;                         // exclusive
+    for (uint32_t i = a; i < b; ++i) {
+        T.super_off[i] = run;
+        run += T.super_cnt[i];
+    }
+    if (t == 1023) {
+        T.super_off[n] = part[1023];
+        T.ctr[CTR_CANDS_LO] = (uint32_t)part[1023];
+        T.ctr[CTR_CANDS_HI] = (uint32_t)(part[1023] >> 32);
+        if (part[1023] > T.cand_cap) T.ctr[CTR_FLAGS] |= FLAG_CAND_OVERFLOW;
+    }
+}
 
-// First G-candidate with global position in [a, b).
-__device__ bool find_cand(const Tables &T, uint64_t a, uint64_t b, Cand *c) {
-    if (a >= b) return false;
-    uint32_t t = (uint32_t)(a / TILE);
-    const uint32_t tl = (uint32_t)((b - 1) / TILE);
-    while (t <= tl) {
-        uint32_t w = t >> 6;
-        unsigned long long bits = T.nonempty[w] & (~0ull << (t & 63));
-        while (!bits) {
-            ++w;
-            if ((w << 6) > tl) return false;
-            bits = T.nonempty[w];
-        }
-        t = (w << 6) + (uint32_t)__builtin_ctzll(bits);
-        if (t > tl) return false;
-        const uint32_t meta = T.tile_meta[t];
-        const uint64_t tb = (uint64_t)t * TILE;
+// Compact every tile's candidates into T.cand in position order (one wave per
+// 64-tile group; empty groups exit on their bitset word).
+__global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
+    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (w >= T.nwords) return;
+    const unsigned long long bits = T.nonempty[w];
+    if (!bits) return;
+    const uint32_t tile = w * 64 + lane;
+    const bool has = (bits >> lane) & 1ull;
+    uint32_t meta = 0, c = 0;
+    if (has) {
+        meta = T.tile_meta[tile];
         if (meta & DENSE_BIT) {
             const uint32_t idx = meta & ~DENSE_BIT;
-            if (idx < T.dense_cap) {              // else: overflowed, host re-runs
-                const uint32_t *bm = T.dense_bits + (size_t)idx * DENSE_WORDS;
-                const uint32_t r0 = a > tb ? (uint32_t)(a - tb) : 0u;
-                const uint32_t r1 = (uint32_t)min<uint64_t>(b - tb, (uint64_t)TILE);
-                for (uint32_t wi = r0 >> 5; (wi << 5) < r1; ++wi) {
-                    uint32_t m = bm[wi];
-                    if ((wi << 5) < r0) m &= ~0u << (r0 & 31);
-                    if (m) {
-                        const uint32_t r = (wi << 5) + (uint32_t)__builtin_ctz(m);
-                        if (r >= r1) return false;
-                        c->pos = tb + r;
-                        c->fix = 0;
-                        c->fix_known = false;
-                        return true;
-                    }
-                }
-            }
+            c = idx < T.dense_cap ? T.dense_cnt[idx] : 0u;
         } else {
-            const uint2 *sl = T.slots + (size_t)t * LISTCAP;
-            for (uint32_t j = 0; j < meta; ++j) {
-                const uint2 v = sl[j];
-                const uint64_t p = tb + v.x;
-                if (p >= a) {
-                    if (p >= b) return false;
-                    c->pos = p;
-                    c->fix = v.y;
-                    c->fix_known = true;
-                    return true;
-                }
+            c = meta;
+        }
+    }
+    uint32_t incl = c;                                  // wave inclusive scan
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+    }
+    const uint64_t base = T.super_off[w] + (incl - c);
+    if (!has || !c) return;
+    if (base + c > T.cand_cap) return;                  // overflow flagged by prefix; host re-runs
+    const uint64_t t0 = (uint64_t)tile * T.tile;
+    if (!(meta & DENSE_BIT)) {
+        const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
+        for (uint32_t j = 0; j < c; ++j) {
+            const uint2 v = sl[j];
+            T.cand[base + j] = (t0 + v.x) | ((uint64_t)v.y << 48) | CAND_KNOWN;
+        }
+    } else {
+        const uint32_t *bm = T.dense_bits + (size_t)(meta & ~DENSE_BIT) * (T.tile / 32);
+        uint64_t o = base;
+        for (uint32_t wi = 0; wi < T.tile / 32; ++wi) {
+            uint32_t m = bm[wi];
+            while (m) {
+                const uint32_t r = wi * 32 + (uint32_t)__builtin_ctz(m);
+                m &= m - 1;
+                T.cand[o++] = t0 + r;
             }
         }
-        ++t;
     }
-    return false;
 }
 
-// First chunk-local hit in [a, b) for a chunk starting at a (b - a <= 63).
+// ---------------------------------------------------------------------------
+// Resolve: one lane per file walks compute_file_chunks' loop over the sorted
+// candidate array.
+// ---------------------------------------------------------------------------
+// First chunk-local hit in [a, b) for a chunk starting at a (b - a <= 63);
+// all loads issued up front (no early exit in the load stream).
 __device__ uint64_t head_scan(const uint8_t *data, uint64_t a, uint64_t b, uint32_t mask) {
+    const uint32_t n = (uint32_t)(b - a);
+    uint32_t x[63];
+#pragma unroll
+    for (uint32_t k = 0; k < 63; ++k) x[k] = k < n ? data[a + k] : 0u;
     uint32_t S = 0, W = 0;
-    for (uint64_t q = a; q < b; ++q) {
-        S += data[q];
+    uint64_t hit = NONE;
+#pragma unroll
+    for (uint32_t k = 0; k < 63; ++k) {
+        S += x[k];
         W += S;
-        if (hit_exact(S, W, mask)) return q;
+        if (hit == NONE && k < n && hit_exact(S, W, mask)) hit = a + k;
     }
-    return NONE;
+    return hit;
 }
 
-__global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restrict__ data,
-                                                         KParams P, Tables T) {
-    const uint32_t k = blockIdx.x * 64 + threadIdx.x;
-    if (k >= T.nfiles) return;
-    const uint32_t i = T.order[k];
+__global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restrict__ data, KParams P,
+                                                         Tables T) {
+    const uint32_t kf = blockIdx.x * 64 + threadIdx.x;
+    if (kf >= T.nfiles) return;
+    const uint32_t i = T.order[kf];
     const uint64_t F = T.flen[i], g0 = T.foff[i];
     DevCut *out = T.cuts + T.cut_base[i];
     const uint32_t cap = T.cut_cap[i];
     const uint64_t MAX = P.max_chunk;
     const uint64_t CAP = P.read_cap ? P.read_cap : ~0ull;
+    const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
+    const uint64_t ncand = min(total, T.cand_cap);
+    // first candidate at or after the file start
+    uint64_t j = 0;
+    if (F) {
+        const uint32_t w = (uint32_t)((g0 / T.tile) >> 6);
+        uint64_t lo = T.super_off[w], hi = min(T.super_off[w + 1], ncand);
+        while (lo < hi) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            if ((T.cand[mid] & CAND_POS_MASK) < g0) lo = mid + 1; else hi = mid;
+        }
+        j = lo;
+    }
+    uint64_t cv = j < ncand ? T.cand[j] : NONE;         // current candidate word
     uint64_t cnt = 0;
     // compute_file_chunks (file_operations.rs:737-784): R = bytes buffered.
     uint64_t R = min(min(F, MAX), CAP);                   // first read :738
@@ -402,29 +593,35 @@ __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restri
     uint32_t fix = 0;
     while (s < R) {                                       // n = R - s > 0  :747
         const uint64_t lim = R;                           // endofs = min(MAX, n) :749-752
-        Cand c;
-        bool found = false, known = false;
-        uint32_t cfix = 0;
         uint64_t e = NONE;
-        if (head == 0) {
-            if (find_cand(T, g0 + s, g0 + lim, &c)) { e = c.pos - g0; found = true; known = c.fix_known; cfix = c.fix; }
-        } else {
+        bool known = false;
+        uint32_t cfix = 0;
+        uint64_t from = s;                                // G applies from here
+        if (head != 0) {
             uint64_t hh = NONE;
             if (head == 1) {
                 if (fix) hh = s - 1 + fix;
             } else {
-                const uint64_t hb = min(s + 63, lim);
-                const uint64_t h = head_scan(data, g0 + s, g0 + hb, P.mask);
+                const uint64_t h = head_scan(data, g0 + s, g0 + min(s + 63, lim), P.mask);
                 if (h != NONE) hh = h - g0;
             }
-            if (hh != NONE && hh < lim) {
-                e = hh; found = true; known = false;      // chunk-local head hit
-            } else if (s + 63 < lim && find_cand(T, g0 + s + 63, g0 + lim, &c)) {
-                e = c.pos - g0; found = true; known = c.fix_known; cfix = c.fix;
+            if (hh != NONE && hh < lim) e = hh;           // chunk-local head hit
+            from = s + 63;
+        }
+        if (e == NONE && from < lim) {
+            const uint64_t a = g0 + from, b = g0 + lim;
+            while (j < ncand && (cv & CAND_POS_MASK) < a) {
+                ++j;
+                cv = j < ncand ? T.cand[j] : NONE;
+            }
+            if (j < ncand && (cv & CAND_POS_MASK) < b) {
+                e = (cv & CAND_POS_MASK) - g0;
+                known = (cv & CAND_KNOWN) != 0;
+                cfix = (uint32_t)(cv >> 48) & 0xffu;
             }
         }
         uint64_t cut;                                     // edge or endofs :754-755
-        if (found) { cut = e + 1; head = known ? 1 : 2; fix = cfix; }
+        if (e != NONE) { cut = e + 1; head = known ? 1 : 2; fix = cfix; }
         else { cut = lim; head = 2; }
         if (cnt < cap) {
             DevCut d;
@@ -479,24 +676,79 @@ __global__ __launch_bounds__(256) void cdc_gen_kernel(uint8_t *__restrict__ base
     for (int k = 0; k < GEN_JUMPS; ++k)
         if ((steps >> k) & 1ull) x = gf2_apply(jump + k * 64, x);
     uint8_t *p = base + foff[i] + start;
-    for (uint64_t j = 0; j < n; ++j) {
+    uint64_t j = 0;
+    for (; j < n && ((uintptr_t)(p + j) & 3u); ++j) {   // head to 4-byte alignment
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        p[j] = (uint8_t)(x >> 32);
+    }
+    for (; j + 4 <= n; j += 4) {
+        uint32_t wv = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            wv |= (uint32_t)(uint8_t)(x >> 32) << (8 * b);
+        }
+        *(uint32_t *)(p + j) = wv;
+    }
+    for (; j < n; ++j) {
         x ^= x << 13; x ^= x >> 7; x ^= x << 17;
         p[j] = (uint8_t)(x >> 32);
     }
 }
 
 // ---------------------------------------------------------------------------
-hipError_t launch_scan(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
+bool run_supported(int run) { return run == 48 || run == 80 || run == 112 || run == 144 || run == 176; }
+
+template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN>; }
+
+static const void *scan_kernel_ptr(int run) {
+    switch (run) {
+        case 48: return scan_fn<48>();
+        case 80: return scan_fn<80>();
+        case 112: return scan_fn<112>();
+        case 144: return scan_fn<144>();
+        case 176: return scan_fn<176>();
+        default: return nullptr;
+    }
+}
+
+int scan_blocks_per_cu(int run) {
+    int n = 0;
+    const void *f = scan_kernel_ptr(run);
+    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 64, lds_wave_bytes(run)) != hipSuccess)
+        return 1;
+    return n > 0 ? n : 1;
+}
+
+template <int RUN>
+static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
+    hipLaunchKernelGGL(cdc_scan_kernel<RUN>, dim3(grid), dim3(64), lds_wave_bytes(RUN), s, d, p, t);
+}
+
+hipError_t launch_scan(int run, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
+                       hipStream_t s) {
     if (!t.ntiles) return hipSuccess;
-    const uint32_t blocks = (t.ntiles + WAVES - 1) / WAVES;
-    hipLaunchKernelGGL(cdc_scan_kernel, dim3(blocks), dim3(64 * WAVES), LDS_BLOCK, s, d, p, t);
+    grid = grid < t.ntiles ? grid : t.ntiles;
+    switch (run) {
+        case 48: launch_scan_t<48>(grid, d, p, t, s); break;
+        case 80: launch_scan_t<80>(grid, d, p, t, s); break;
+        case 112: launch_scan_t<112>(grid, d, p, t, s); break;
+        case 144: launch_scan_t<144>(grid, d, p, t, s); break;
+        case 176: launch_scan_t<176>(grid, d, p, t, s); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_dense(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    if (!t.ntiles || !t.dense_cap) return hipSuccess;
-    const uint32_t blocks = t.dense_cap < 2048u ? t.dense_cap : 2048u;
-    hipLaunchKernelGGL(cdc_dense_kernel, dim3(blocks), dim3(64), 0, s, d, p, t);
+hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s,
+                       hipEvent_t) {
+    if (!t.ntiles) return hipSuccess;
+    if (t.dense_cap) {
+        const uint32_t blocks = t.dense_cap < 2048u ? t.dense_cap : 2048u;
+        hipLaunchKernelGGL(cdc_dense_kernel, dim3(blocks), dim3(64), 0, s, d, p, t);
+    }
+    hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
+    hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4), dim3(256), 0, s, t);
     return hipGetLastError();
 }
 

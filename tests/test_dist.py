@@ -1,0 +1,66 @@
+"""Multi-GPU path on CPU: per-file LPT sharding and the control-plane reductions
+bench.py uses (gloo, world_size 2).  No data-path collective exists: files are
+independent, so ranks only agree on the step time."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import bench
+
+
+def test_lpt_shard_partition_and_balance():
+    sizes, idx, _ = bench.workload("zipf10k", 8)
+    assert sizes.size == 80000 and np.array_equal(idx, np.arange(80000))
+    parts = bench.lpt_shard(sizes, 8)
+    allf = np.sort(np.concatenate(parts))
+    assert np.array_equal(allf, np.arange(sizes.size))          # every file exactly once
+    loads = np.array([int(sizes[p].sum()) for p in parts])
+    assert loads.max() / loads.mean() < 1.01                     # LPT balance
+    assert abs(loads.mean() / 2**30 - 9.73) < 0.02               # fixed work per GPU (weak scaling)
+
+
+def test_zipf_config_matches_survey():
+    s = bench.zipf_sizes()
+    assert s.size == 10000 and int(s.max()) == 128 << 20
+    assert int((s == (128 << 20)).sum()) == 39 and int((s > (2 << 20)).sum()) == 305
+    assert int(np.median(s)) == 8192
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    d = bench.Dist()
+    sizes, _, _ = bench.workload("uniform1k", world)
+    mine = bench.lpt_shard(sizes, world)[d.rank]
+    span = float(sizes[mine].sum())
+    d.barrier()
+    tot = d.reduce(span, "sum")
+    mx = d.reduce(float(rank + 1), "max")
+    q.put((rank, len(mine), tot, mx))
+    d.close()
+
+
+def test_gloo_world2_reductions():
+    torch = pytest.importorskip("torch")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [1024, 1024]
+    assert all(r[2] == 2048 * (1 << 20) for r in res)           # sum over ranks
+    assert all(r[3] == 2.0 for r in res)                         # max over ranks

