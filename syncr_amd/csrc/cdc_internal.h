@@ -42,6 +42,8 @@ struct KParams {
     uint32_t k;        // scalar k
     uint64_t max_chunk;
     uint64_t read_cap; // 0 = unlimited (ideal semantics)
+    uint32_t ablate;   // timing-only diagnostics (SYNCR_CDC_ABLATE): 1 = no rolling, 2 = no DMA
+    uint32_t prio;     // raise wave priority while staging a tile (SYNCR_CDC_PRIO, default on)
 };
 
 struct DevCut {        // == syncr_cut

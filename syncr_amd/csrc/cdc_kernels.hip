@@ -39,6 +39,14 @@ __device__ __forceinline__ uint32_t lower_bound_serial(const uint64_t *a, uint32
     return lo;
 }
 
+// tv = a*b + c on packed u16 pairs, pinned to ONE v_pk_mad_u16: left to itself
+// hipcc re-associates two dependent mads into mul + mad + add (3 VOP3P).
+__device__ __forceinline__ u16x2 pk_mad(uint32_t a, uint32_t b_uniform, u16x2 c) {
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b_uniform), "v"(as_u32(c)));
+    return as_u16x2(r);
+}
+
 // LDS byte address of a generic pointer into dynamic shared memory.
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
@@ -188,8 +196,8 @@ __device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
             const int i = g * 16 + jj;
             const uint32_t x = pair_at<RUN>(A, B, HALO + i), d = pair_at<RUN>(A, B, i);
             S = S + x - d;
-            Tv = as_u16x2(S) * kk + Tv;
-            Tv = as_u16x2(d) * km + Tv;
+            Tv = pk_mad(S, P.kk, Tv);
+            Tv = pk_mad(d, P.kmv, Tv);
             acc = __builtin_elementwise_min(acc, Tv);
         }
         const uint32_t a = as_u32(acc);
@@ -347,7 +355,10 @@ __device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, u
 // path), then roll.  The DMA latency hides under the rolling of this tile and
 // under the other resident waves.
 // ---------------------------------------------------------------------------
-template <int RUN>
+// MODE 0 is the product; MODE 1 (staging only) and 2 (no DMA) are timing-only
+// ablations selected by SYNCR_CDC_ABLATE, compiled separately so they cannot
+// perturb the product's register allocation.
+template <int RUN, int MODE>
 __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P,
                                                       Tables T) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -386,7 +397,12 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
         }
         const bool starts = trange.y > trange.x;                     // wave-uniform
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");           // runs are in registers
-        if (!starts && next < T.ntiles) issue_tile<RUN>(data, T.span, next, lds0, lane);
+        if (!starts && next < T.ntiles && MODE != 2) issue_tile<RUN>(data, T.span, next, lds0, lane);
+        if constexpr (MODE == 1) {                                   // diagnostics: staging only
+#pragma unroll
+            for (int q = 0; q < NQ * 4; ++q) asm volatile("" ::"v"(A[q]), "v"(B[q]));
+            continue;
+        }
 
         // which of my runs straddle a file start (rare; bytes stay in LDS)
         const int64_t rsA = t0 + (int64_t)lane * RUN;
@@ -415,7 +431,7 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
             if (slowA) roll_with_resets(byte, rsA, RUN, T.fstart, trange.x, trange.y, P.mask, rec);
             if (slowB) roll_with_resets(byte, rsB, RUN, T.fstart, trange.x, trange.y, P.mask, rec);
         }
-        if (starts && next < T.ntiles) {
+        if (starts && next < T.ntiles && MODE != 2) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // slow-path LDS reads done
             issue_tile<RUN>(data, T.span, next, lds0, lane);
         }
@@ -699,7 +715,7 @@ __global__ __launch_bounds__(256) void cdc_gen_kernel(uint8_t *__restrict__ base
 // ---------------------------------------------------------------------------
 bool run_supported(int run) { return run == 48 || run == 80 || run == 112 || run == 144 || run == 176; }
 
-template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN>; }
+template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN, 0>; }
 
 static const void *scan_kernel_ptr(int run) {
     switch (run) {
@@ -722,7 +738,14 @@ int scan_blocks_per_cu(int run) {
 
 template <int RUN>
 static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    hipLaunchKernelGGL(cdc_scan_kernel<RUN>, dim3(grid), dim3(64), lds_wave_bytes(RUN), s, d, p, t);
+    if (p.ablate == 1u && (RUN == DEFAULT_RUN || RUN == 144))
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, (RUN == DEFAULT_RUN || RUN == 144) ? 1 : 0>), dim3(grid),
+                           dim3(64), lds_wave_bytes(RUN), s, d, p, t);
+    else if (p.ablate == 2u && (RUN == DEFAULT_RUN || RUN == 144))
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, (RUN == DEFAULT_RUN || RUN == 144) ? 2 : 0>), dim3(grid),
+                           dim3(64), lds_wave_bytes(RUN), s, d, p, t);
+    else
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 0>), dim3(grid), dim3(64), lds_wave_bytes(RUN), s, d, p, t);
 }
 
 hipError_t launch_scan(int run, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,

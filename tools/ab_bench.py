@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of engine variants in ONE process on ONE device.
+
+Variants are environment settings read by syncr_cdc_open (SYNCR_CDC_RUN,
+SYNCR_CDC_PRIO, SYNCR_CDC_ABLATE, SYNCR_CDC_SCAN_GRID, ...).  The corpus is
+generated once; each round times every variant for --steps launches; the
+median scan-kernel time and step time per variant are printed.  Cross-call
+comparisons are not trusted (devices and clocks differ between gpurun boxes).
+
+    python tools/ab_bench.py "SYNCR_CDC_RUN=80" "SYNCR_CDC_RUN=144" --rounds 5
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+import syncr_amd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--workload", default="zipf10k")
+    args = ap.parse_args()
+    sizes, idx, _ = bench.workload(args.workload, 1)
+    offs = np.zeros_like(sizes)
+    offs[1:] = np.cumsum(sizes)[:-1]
+    span = int(sizes.sum())
+    base = syncr_amd.Chunker()
+    buf = syncr_amd.DeviceBuffer(base, span)
+    buf.gen_corpus(offs, sizes, indices=idx)
+    handles = []
+    for v in args.variants:
+        saved = dict(os.environ)
+        for kv in filter(None, v.split(",")):
+            k, val = kv.split("=", 1)
+            os.environ[k] = val
+        c = syncr_amd.Chunker()
+        os.environ.clear()
+        os.environ.update(saved)
+        c.plan(offs, sizes, span)
+        c.launch(buf.ptr)
+        ref = c.fetch()
+        handles.append((v, c, sum(x.size for x in ref)))
+    res = {v: ([], []) for v, _, _ in handles}
+    for _ in range(args.rounds):
+        for v, c, _ in handles:
+            c.synchronize()
+            c.set_timing(True)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                c.launch(buf.ptr)
+            c.synchronize()
+            dt = (time.perf_counter() - t0) / args.steps * 1e3
+            ms, n = c.kernel_times()
+            c.set_timing(False)
+            res[v][0].append(ms[0] / n)
+            res[v][1].append(dt)
+    for v, c, ncuts in handles:
+        sc, st = res[v]
+        print(f"{v:40s} scan med {statistics.median(sc):.4f} min {min(sc):.4f} ms  "
+              f"({span / statistics.median(sc) / 1e6:.0f} GB/s)  step med {statistics.median(st):.4f} ms  "
+              f"cuts {ncuts}  {c.info()['scan_grid']} waves")
+    buf.free()
+
+
+if __name__ == "__main__":
+    main()
