@@ -286,8 +286,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     h->params = prm;
     h->kp = make_kparams(prm);
     if (const char *a = getenv("SYNCR_CDC_ABLATE")) h->kp.ablate = (uint32_t)atoi(a);  // timing-only
-    h->kp.prio = 1;
-    if (const char *pr = getenv("SYNCR_CDC_PRIO")) h->kp.prio = (uint32_t)atoi(pr);
+    if (const char *rs = getenv("SYNCR_CDC_RESOLVE")) h->kp.resolve_lane = strcmp(rs, "lane") == 0;
     if (const char *r = getenv("SYNCR_CDC_RUN")) {
         const int v = atoi(r);
         if (run_supported(v)) h->run = v;

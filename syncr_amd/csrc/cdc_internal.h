@@ -43,7 +43,7 @@ struct KParams {
     uint64_t max_chunk;
     uint64_t read_cap; // 0 = unlimited (ideal semantics)
     uint32_t ablate;   // timing-only diagnostics (SYNCR_CDC_ABLATE): 1 = no rolling, 2 = no DMA
-    uint32_t prio;     // raise wave priority while staging a tile (SYNCR_CDC_PRIO, default on)
+    uint32_t resolve_lane;  // 1: lane-per-file resolve (SYNCR_CDC_RESOLVE=lane); 0: wave-per-file
 };
 
 struct DevCut {        // == syncr_cut

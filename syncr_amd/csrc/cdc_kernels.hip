@@ -658,6 +658,118 @@ __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restri
 }
 
 // ---------------------------------------------------------------------------
+// Resolve, one WAVE per file (default).  The wave holds a window of 64
+// consecutive sorted candidates (one coalesced load); the next candidate at
+// or after `a` is the first set bit of a ballot.  An unknown head fix-up is one
+// coalesced 63-byte load plus two wave prefix sums (S, then W).  All control
+// state is wave-uniform, so the serial compute_file_chunks walk costs a few
+// scalar/vector ops per cut instead of a dependent memory round trip.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(v, off);
+        if (lane >= off) v += u;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t k) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__restrict__ data,
+                                                               KParams P, Tables T) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t kf = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (kf >= T.nfiles) return;
+    const uint32_t i = T.order[kf];
+    const uint64_t F = T.flen[i], g0 = T.foff[i];
+    DevCut *out = T.cuts + T.cut_base[i];
+    const uint32_t cap = T.cut_cap[i];
+    const uint64_t MAX = P.max_chunk;
+    const uint64_t CAP = P.read_cap ? P.read_cap : ~0ull;
+    const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
+    const uint64_t ncand = min(total, T.cand_cap);
+    // candidate window: wv = cand[wb + lane] (NONE past the end)
+    uint64_t wb = 0;
+    if (F) {
+        const uint32_t w = (uint32_t)((g0 / T.tile) >> 6);
+        wb = T.super_off[w];                               // first candidate of the file's 64-tile group
+    }
+    uint64_t wv = wb + lane < ncand ? T.cand[wb + lane] : NONE;
+    uint64_t cnt = 0;
+    uint64_t R = min(min(F, MAX), CAP);                   // first read (file_operations.rs:738)
+    uint64_t s = 0;
+    int head = 0;            // 0: file start (G is chunk-local), 1: fix known, 2: unknown
+    uint32_t fix = 0;
+    while (s < R) {                                       // :747
+        const uint64_t lim = R;                           // :749-752
+        uint64_t e = NONE;
+        bool known = false;
+        uint32_t cfix = 0;
+        uint64_t from = s;
+        if (head != 0) {
+            uint64_t hh = NONE;
+            if (head == 1) {
+                if (fix) hh = s - 1 + fix;
+            } else {                                      // wave head scan of [s, min(s+63, lim))
+                const uint32_t n = (uint32_t)min<uint64_t>(63ull, lim - s);
+                const uint32_t x = (uint32_t)lane < n ? data[g0 + s + lane] : 0u;
+                const uint32_t S = wave_incl_scan(x, lane);
+                const uint32_t W = wave_incl_scan(S, lane);
+                const unsigned long long m = __ballot((uint32_t)lane < n && hit_exact(S, W, P.mask));
+                if (m) hh = s + (uint64_t)__builtin_ctzll(m);
+            }
+            if (hh != NONE && hh < lim) e = hh;
+            from = s + 63;
+        }
+        if (e == NONE && from < lim) {
+            const uint64_t a = g0 + from, b = g0 + lim;
+            for (;;) {
+                const unsigned long long m = __ballot(wv != NONE && (wv & CAND_POS_MASK) >= a);
+                if (m) {
+                    const uint64_t c = readlane64(wv, (uint32_t)__builtin_ctzll(m));
+                    if ((c & CAND_POS_MASK) < b) {
+                        e = (c & CAND_POS_MASK) - g0;
+                        known = (c & CAND_KNOWN) != 0;
+                        cfix = (uint32_t)(c >> 48) & 0xffu;
+                    }
+                    break;
+                }
+                // whole window below a: slide (positions are sorted)
+                const uint64_t last = readlane64(wv, 63);
+                if (last == NONE || wb + 64 >= ncand) break;
+                wb += 64;
+                wv = wb + lane < ncand ? T.cand[wb + lane] : NONE;
+            }
+        }
+        uint64_t cut;                                     // :754-755
+        if (e != NONE) { cut = e + 1; head = known ? 1 : 2; fix = cfix; }
+        else { cut = lim; head = 2; }
+        if (lane == 0 && cnt < cap) {
+            DevCut d;
+            d.offset = s;
+            d.len = (uint32_t)(cut - s);
+            d.file = i;
+            out[cnt] = d;
+        }
+        ++cnt;
+        s = cut;                                          // :771
+        uint64_t rd = MAX - (R - s);                      // :776
+        rd = min(rd, CAP);
+        rd = min(rd, F - R);
+        R += rd;
+    }
+    if (lane == 0) {
+        T.counts[i] = cnt;
+        if (cnt > cap) atomicOr(&T.ctr[CTR_FLAGS], FLAG_CUT_OVERFLOW);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic corpus generator (bench/tests): xorshift64 with GF(2) jump-ahead
 // so every thread writes its own 4 KiB segment of some file.
 // ---------------------------------------------------------------------------
@@ -777,7 +889,10 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
 
 hipError_t launch_resolve(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
     if (!t.nfiles) return hipSuccess;
-    hipLaunchKernelGGL(cdc_resolve_kernel, dim3((t.nfiles + 63) / 64), dim3(64), 0, s, d, p, t);
+    if (p.resolve_lane)
+        hipLaunchKernelGGL(cdc_resolve_kernel, dim3((t.nfiles + 63) / 64), dim3(64), 0, s, d, p, t);
+    else
+        hipLaunchKernelGGL(cdc_resolve_wave_kernel, dim3((t.nfiles + 3) / 4), dim3(256), 0, s, d, p, t);
     return hipGetLastError();
 }
 

@@ -272,3 +272,26 @@ def test_kernel_timing_api(chunkers):
         assert st["tiles"] >= data_len // (144 * 128) and st["flags"] == 0
     finally:
         buf.free()
+
+
+def test_resolve_variants_agree(kat_cases):
+    """Wave-per-file (default) and lane-per-file resolve give identical cuts."""
+    import os
+    sel = [c for c in kat_cases if c["len"] <= 8 * M]
+    os.environ["SYNCR_CDC_RESOLVE"] = "lane"
+    try:
+        lanes = {}
+        for c in sel:
+            key = (c["chunk_bits"], c["max_chunk"], c["read_cap"])
+            if key not in lanes:
+                lanes[key] = syncr_amd.Chunker(*key)
+    finally:
+        del os.environ["SYNCR_CDC_RESOLVE"]
+    try:
+        for c in sel:
+            data = make_input(c["recipe"])
+            ch = lanes[(c["chunk_bits"], c["max_chunk"], c["read_cap"])]
+            assert ends_of(ch.cut_array(data)) == c["ends"], c["name"]
+    finally:
+        for ch in lanes.values():
+            ch.close()

@@ -51,7 +51,7 @@ def main():
         c.launch(buf.ptr)
         ref = c.fetch()
         handles.append((v, c, sum(x.size for x in ref)))
-    res = {v: ([], []) for v, _, _ in handles}
+    res = {v: ([], [], [], []) for v, _, _ in handles}
     for _ in range(args.rounds):
         for v, c, _ in handles:
             c.synchronize()
@@ -65,10 +65,13 @@ def main():
             c.set_timing(False)
             res[v][0].append(ms[0] / n)
             res[v][1].append(dt)
+            res[v][2].append(ms[1] / n)
+            res[v][3].append(ms[2] / n)
     for v, c, ncuts in handles:
-        sc, st = res[v]
+        sc, st, po, rz = res[v]
         print(f"{v:40s} scan med {statistics.median(sc):.4f} min {min(sc):.4f} ms  "
               f"({span / statistics.median(sc) / 1e6:.0f} GB/s)  step med {statistics.median(st):.4f} ms  "
+              f"post {statistics.median(po):.4f} resolve {statistics.median(rz):.4f} ms  "
               f"cuts {ncuts}  {c.info()['scan_grid']} waves")
     buf.free()
 
