@@ -23,7 +23,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def counters(path):
     agg = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        agg[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        if "cdc_scan_kernel" in name:
+            name = "cdc::cdc_scan_kernel"
+        agg[(name, r["Counter_Name"])].append(float(r["Counter_Value"]))
     return agg
 
 
