@@ -97,8 +97,9 @@ class Dist:
             self.pg.destroy_process_group()
 
 
-def load_traffic(workload_name: str, span: int):
-    """HBM bytes per scan launch from the committed rocprofv3 PMC summary."""
+def load_traffic(workload_name: str, span: int, run_bytes: int):
+    """HBM bytes per scan launch from the committed rocprofv3 PMC summary of
+    the same workload, span and scan geometry (profiles/*_pmc_traffic.json)."""
     import glob
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
@@ -106,7 +107,8 @@ def load_traffic(workload_name: str, span: int):
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("workload") == workload_name and int(d.get("span", -1)) == span:
+        if (d.get("workload") == workload_name and int(d.get("span", -1)) == span
+                and d.get("run_bytes") == run_bytes):
             best = d
     return best
 
@@ -208,7 +210,7 @@ def main(argv=None):
 
     scan_ms = kms[0] / max(nl, 1)
     achieved = span / (scan_ms / 1e3) / 1e9 if scan_ms > 0 else 0.0
-    tr = load_traffic(args.workload, span)
+    tr = load_traffic(args.workload, span, engine_info["run_bytes"])
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -54,6 +54,7 @@ def main(tag, src=None):
     hbm = 2 * fetch_kib * 1024 + write_kib * 1024
     out = {
         "kernel": k, "workload": fb.get("config", {}).get("workload", "").split(":")[0],
+        "run_bytes": fb.get("config", {}).get("engine", {}).get("run_bytes"),
         "span": span, "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
         "hbm_bytes_per_launch": int(hbm), "algorithmic_bytes_per_launch": span,
         "traffic_over_algorithmic": (hbm / span) if span else None,
