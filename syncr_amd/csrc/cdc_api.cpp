@@ -62,7 +62,7 @@ struct syncr_cdc {
     uint64_t total_cut_cap = 0;
     std::vector<uint64_t> h_foff, h_flen, h_cut_base;
     std::vector<uint32_t> h_cut_cap;
-    DevBuf fstart, foff, flen, order, cut_base, cut_cap, tile_range, tile_meta, slots, zeroed,
+    DevBuf fstart, foff, flen, order, cut_base, cut_cap, bmask, tile_meta, slots, zeroed,
         dense_list, dense_cnt, dense_bits, super_off, cand, cuts, counts;
 
     // launch
@@ -135,8 +135,7 @@ Tables make_tables(syncr_cdc *h) {
     t.nwords = h->nwords;
     t.nstarts = h->nstarts;
     t.fstart = h->fstart.as<uint64_t>();
-    t.tile_range = h->tile_range.as<uint2>();
-    t.nfiles = h->nfiles;
+        t.nfiles = h->nfiles;
     t.foff = h->foff.as<uint64_t>();
     t.flen = h->flen.as<uint64_t>();
     t.order = h->order.as<uint32_t>();
@@ -156,6 +155,7 @@ Tables make_tables(syncr_cdc *h) {
     t.cand_cap = h->cand_cap;
     t.cuts = h->cuts.as<DevCut>();
     t.counts = h->counts.as<uint64_t>();
+    t.bmask = h->bmask.as<uint64_t>();
     return t;
 }
 
@@ -313,7 +313,7 @@ void syncr_cdc_close(syncr_cdc *h) {
     (void)hipStreamSynchronize(h->stream);
     drain_timing(h);
     DevBuf *bufs[] = {&h->fstart, &h->foff, &h->flen, &h->order, &h->cut_base, &h->cut_cap,
-                      &h->tile_range, &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
+                      &h->bmask, &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
                       &h->dense_cnt, &h->dense_bits, &h->super_off, &h->cand, &h->cuts,
                       &h->counts, &h->stage};
     for (DevBuf *b : bufs) b->release();
@@ -359,18 +359,6 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         h->h_foff.assign(file_off, file_off + nfiles);
         h->h_flen.assign(file_len, file_len + nfiles);
 
-        // per-tile range of relevant file starts: [t0-63, t0+TILE)
-        std::vector<uint2> tr(std::max<uint32_t>(h->ntiles, 1));
-        {
-            size_t lo = 0, hi = 0;
-            for (uint32_t t = 0; t < h->ntiles; t++) {
-                const int64_t t0 = (int64_t)t * TILE;
-                while (lo < starts.size() && (int64_t)starts[lo] < t0 - 63) lo++;
-                if (hi < lo) hi = lo;
-                while (hi < starts.size() && (int64_t)starts[hi] < t0 + TILE) hi++;
-                tr[t] = make_uint2((uint32_t)lo, (uint32_t)hi);
-            }
-        }
         // resolve order: largest files first (longest serial chains start first)
         std::vector<uint32_t> order(nfiles);
         std::iota(order.begin(), order.end(), 0u);
@@ -384,7 +372,7 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         CHECK_HIP(h->flen.ensure(std::max<size_t>(nfiles, 1) * 8));
         CHECK_HIP(h->order.ensure(std::max<size_t>(nfiles, 1) * 4));
         CHECK_HIP(h->counts.ensure(std::max<size_t>(nfiles, 1) * 8));
-        CHECK_HIP(h->tile_range.ensure(tr.size() * sizeof(uint2)));
+        CHECK_HIP(h->bmask.ensure(std::max<size_t>(nfiles, 1) * 8));
         CHECK_HIP(h->tile_meta.ensure(std::max<size_t>(h->ntiles, 1) * 4));
         CHECK_HIP(h->slots.ensure(std::max<size_t>(h->ntiles, 1) * LISTCAP * sizeof(uint2)));
         CHECK_HIP(h->zeroed.ensure(zeroed_bytes(h)));
@@ -403,7 +391,6 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
             CHECK_HIP(hipMemcpy(h->flen.p, file_len, nfiles * 8ull, hipMemcpyHostToDevice));
             CHECK_HIP(hipMemcpy(h->order.p, order.data(), nfiles * 4ull, hipMemcpyHostToDevice));
         }
-        CHECK_HIP(hipMemcpy(h->tile_range.p, tr.data(), tr.size() * sizeof(uint2), hipMemcpyHostToDevice));
         rc = upload_cut_tables(h);
         if (rc) return rc;
         h->planned = true;

@@ -59,7 +59,6 @@ struct Tables {
     uint32_t nwords;               // ceil(ntiles / 64)
     uint32_t nstarts;              // non-empty files (sorted starts)
     const uint64_t *fstart;        // [nstarts] sorted file starts
-    const uint2 *tile_range;       // [ntiles] {lo, hi} into fstart: starts in [t0-63, t0+TILE)
     uint32_t nfiles;
     const uint64_t *foff, *flen;   // [nfiles] file table (caller order)
     const uint32_t *order;         // [nfiles] resolve order (largest first)
@@ -79,6 +78,7 @@ struct Tables {
     uint64_t cand_cap;
     DevCut *cuts;                  // [sum cut_cap]
     uint64_t *counts;              // [nfiles]
+    uint64_t *bmask;               // [nfiles] exact G hits of each file's first 63 bytes
 };
 
 // launchers (cdc_kernels.hip)

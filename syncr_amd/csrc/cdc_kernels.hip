@@ -351,9 +351,9 @@ __device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, u
 // ---------------------------------------------------------------------------
 // Scan kernel: persistent, one wave per block, one LDS landing buffer.  Per
 // tile: wait for its DMA, copy the runs into registers, hand the buffer to the
-// next tile's DMA (unless a file start needs the bytes in LDS for the slow
-// path), then roll.  The DMA latency hides under the rolling of this tile and
-// under the other resident waves.
+// next tile's DMA, then roll.  The DMA latency hides under the rolling of this
+// tile and under the other resident waves.  The scan knows nothing about files:
+// it computes G over the batch as one continuous stream (see cdc_boundary_kernel).
 // ---------------------------------------------------------------------------
 // MODE 0 is the product; MODE 1 (staging only) and 2 (no DMA) are timing-only
 // ablations selected by SYNCR_CDC_ABLATE, compiled separately so they cannot
@@ -379,8 +379,6 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
     issue_tile<RUN>(data, T.span, tile, lds0, lane);
     for (; tile < T.ntiles; tile += stride) {
         const uint32_t next = tile + stride;
-        const uint64_t tr64 = sload_u64(T.tile_range + tile);       // scalar: no vmcnt
-        const uint2 trange = make_uint2((uint32_t)tr64, (uint32_t)(tr64 >> 32));
         const int64_t t0 = (int64_t)tile * TILE;
         if (lane == 0) { *wcount = 0u; *dcount = 0u; }
         wait_vmcnt<0>();                                             // this tile has landed
@@ -395,27 +393,16 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
                 B[4 * q + 0] = b.x; B[4 * q + 1] = b.y; B[4 * q + 2] = b.z; B[4 * q + 3] = b.w;
             }
         }
-        const bool starts = trange.y > trange.x;                     // wave-uniform
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");           // runs are in registers
-        if (!starts && next < T.ntiles && MODE != 2) issue_tile<RUN>(data, T.span, next, lds0, lane);
+        if (next < T.ntiles && MODE != 2) issue_tile<RUN>(data, T.span, next, lds0, lane);
         if constexpr (MODE == 1) {                                   // diagnostics: staging only
 #pragma unroll
             for (int q = 0; q < NQ * 4; ++q) asm volatile("" ::"v"(A[q]), "v"(B[q]));
             continue;
         }
-
-        // which of my runs straddle a file start (rare; bytes stay in LDS)
-        const int64_t rsA = t0 + (int64_t)lane * RUN;
-        const int64_t rsB = t0 + (int64_t)(lane + 64) * RUN;
-        bool slowA = false, slowB = false;
-        if (starts) {
-            uint32_t j = lower_bound_serial(T.fstart, trange.x, trange.y, rsA - 62);
-            slowA = j < trange.y && (int64_t)T.fstart[j] <= rsA + RUN - 1;
-            j = lower_bound_serial(T.fstart, trange.x, trange.y, rsB - 62);
-            slowB = j < trange.y && (int64_t)T.fstart[j] <= rsB + RUN - 1;
-        }
         const int64_t lim_rel = span - t0;                           // positions >= span are not bytes
-        roll_fast<RUN>(A, B, P, lane, !slowA, !slowB, dcount, dslots);
+        roll_fast<RUN>(A, B, P, lane, true, true, dcount, dslots);
+        if constexpr (MODE == 2) continue;                          // diagnostics: rolling only
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         const uint32_t nd = __builtin_amdgcn_readfirstlane(
@@ -423,21 +410,36 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
                               __HIP_MEMORY_SCOPE_WAVEFRONT));
         if (nd) rewalk_dirty<RUN>(P, lane, nd < (uint32_t)DIRTYCAP ? nd : (uint32_t)DIRTYCAP, dslots,
                                   lim_rel, wcount, wlist);
-        if (slowA || slowB) {
-            auto byte = [&](int64_t q) -> uint32_t { return wl[q - t0 + HALO]; };
-            auto rec = [&](int64_t q) {
-                if (q - t0 < lim_rel) record(wcount, wlist, (uint32_t)(q - t0));
-            };
-            if (slowA) roll_with_resets(byte, rsA, RUN, T.fstart, trange.x, trange.y, P.mask, rec);
-            if (slowB) roll_with_resets(byte, rsB, RUN, T.fstart, trange.x, trange.y, P.mask, rec);
-        }
-        if (starts && next < T.ntiles && MODE != 2) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // slow-path LDS reads done
-            issue_tile<RUN>(data, T.span, next, lds0, lane);
-        }
         publish_tile(data, P, T, tile, t0, wlist, wcount, lane, nd > (uint32_t)DIRTYCAP);
     }
 }
+
+// ---------------------------------------------------------------------------
+// File starts: the scan treats the batch as ONE byte stream, so its G is exact
+// for p >= f+63 inside a file starting at f.  The 63 head positions of every
+// file are recomputed here with a fresh window at f (bit k of bmask[i] = hit at
+// f+k); the resolve uses this mask at s = 0 and the candidates from f+63 on.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cdc_boundary_kernel(const uint8_t *__restrict__ data,
+                                                           KParams P, Tables T) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= T.nfiles) return;
+    const uint64_t F = T.flen[i], g0 = T.foff[i];
+    const uint32_t n = (uint32_t)min<uint64_t>(F, 63ull);
+    uint32_t x[63];
+#pragma unroll
+    for (int k = 0; k < 63; ++k) x[k] = (uint32_t)k < n ? data[g0 + k] : 0u;
+    uint32_t S = 0, W = 0;
+    uint64_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 63; ++k) {
+        S += x[k];
+        W += S;
+        if ((uint32_t)k < n && hit_exact(S, W, P.mask)) m |= 1ull << k;
+    }
+    T.bmask[i] = m;
+}
+
 // ---------------------------------------------------------------------------
 // Dense tiles (more than LISTCAP candidates: low-entropy / adversarial data at
 // small chunk_bits): recompute G for the whole tile into a bitmap, count it.
@@ -456,11 +458,10 @@ __global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict
         uint32_t *out = T.dense_bits + (size_t)idx * (T.tile / 32) + lane * words_lane;
         for (int w = 0; w < words_lane; ++w) out[w] = 0u;
         auto byte = [&](int64_t q) -> uint32_t { return (q >= 0 && q < span) ? data[q] : 0u; };
-        const uint32_t lo = lower_bound_serial(T.fstart, 0, T.nstarts, rs - 64);
-        const uint32_t hi = lower_bound_serial(T.fstart, lo, T.nstarts, rs + per_lane);
         uint32_t word = 0, cnt = 0;
         int cur = 0;
-        roll_with_resets(byte, rs, per_lane, T.fstart, lo, hi, P.mask, [&](int64_t q) {
+        // stream semantics like the scan (no resets: file heads come from the boundary masks)
+        roll_with_resets(byte, rs, per_lane, T.fstart, 0u, 0u, P.mask, [&](int64_t q) {
             if (q < span) {
                 const int r = (int)(q - rs);
                 if ((r >> 5) != cur) { out[cur] = word; word = 0; cur = r >> 5; }
@@ -601,28 +602,31 @@ __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restri
         j = lo;
     }
     uint64_t cv = j < ncand ? T.cand[j] : NONE;         // current candidate word
+    const uint64_t bm = T.bmask[i];                      // exact hits of the file's first 63 bytes
     uint64_t cnt = 0;
     // compute_file_chunks (file_operations.rs:737-784): R = bytes buffered.
     uint64_t R = min(min(F, MAX), CAP);                   // first read :738
     uint64_t s = 0;
-    int head = 0;            // 0: file start (G is chunk-local), 1: fix known, 2: unknown
+    int head = 0;            // 0: file start (boundary mask), 1: fix known, 2: unknown
     uint32_t fix = 0;
     while (s < R) {                                       // n = R - s > 0  :747
         const uint64_t lim = R;                           // endofs = min(MAX, n) :749-752
         uint64_t e = NONE;
         bool known = false;
         uint32_t cfix = 0;
-        uint64_t from = s;                                // G applies from here
-        if (head != 0) {
+        uint64_t from = s + 63;                           // stream G applies from here
+        {
             uint64_t hh = NONE;
-            if (head == 1) {
+            if (head == 0) {
+                const uint64_t m = lim < 63 ? bm & ((1ull << lim) - 1) : bm;
+                if (m) hh = (uint64_t)__builtin_ctzll(m);
+            } else if (head == 1) {
                 if (fix) hh = s - 1 + fix;
             } else {
                 const uint64_t h = head_scan(data, g0 + s, g0 + min(s + 63, lim), P.mask);
                 if (h != NONE) hh = h - g0;
             }
             if (hh != NONE && hh < lim) e = hh;           // chunk-local head hit
-            from = s + 63;
         }
         if (e == NONE && from < lim) {
             const uint64_t a = g0 + from, b = g0 + lim;
@@ -700,20 +704,24 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
         wb = T.super_off[w];                               // first candidate of the file's 64-tile group
     }
     uint64_t wv = wb + lane < ncand ? T.cand[wb + lane] : NONE;
+    const uint64_t bm = T.bmask[i];                      // exact hits of the file's first 63 bytes
     uint64_t cnt = 0;
     uint64_t R = min(min(F, MAX), CAP);                   // first read (file_operations.rs:738)
     uint64_t s = 0;
-    int head = 0;            // 0: file start (G is chunk-local), 1: fix known, 2: unknown
+    int head = 0;            // 0: file start (boundary mask), 1: fix known, 2: unknown
     uint32_t fix = 0;
     while (s < R) {                                       // :747
         const uint64_t lim = R;                           // :749-752
         uint64_t e = NONE;
         bool known = false;
         uint32_t cfix = 0;
-        uint64_t from = s;
-        if (head != 0) {
+        const uint64_t from = s + 63;                     // stream G applies from here
+        {
             uint64_t hh = NONE;
-            if (head == 1) {
+            if (head == 0) {
+                const uint64_t m = lim < 63 ? bm & ((1ull << lim) - 1) : bm;
+                if (m) hh = (uint64_t)__builtin_ctzll(m);
+            } else if (head == 1) {
                 if (fix) hh = s - 1 + fix;
             } else {                                      // wave head scan of [s, min(s+63, lim))
                 const uint32_t n = (uint32_t)min<uint64_t>(63ull, lim - s);
@@ -724,7 +732,6 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
                 if (m) hh = s + (uint64_t)__builtin_ctzll(m);
             }
             if (hh != NONE && hh < lim) e = hh;
-            from = s + 63;
         }
         if (e == NONE && from < lim) {
             const uint64_t a = g0 + from, b = g0 + lim;
@@ -882,6 +889,8 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
         const uint32_t blocks = t.dense_cap < 2048u ? t.dense_cap : 2048u;
         hipLaunchKernelGGL(cdc_dense_kernel, dim3(blocks), dim3(64), 0, s, d, p, t);
     }
+    if (t.nfiles)
+        hipLaunchKernelGGL(cdc_boundary_kernel, dim3((t.nfiles + 255) / 256), dim3(256), 0, s, d, p, t);
     hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
     hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4), dim3(256), 0, s, t);
     return hipGetLastError();
