@@ -26,6 +26,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-mllvm", "-amdgpu-mfma-vgpr-form",  # MFMA results in VGPRs: no accvgpr reads
            "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
            "-o", LIB + ".tmp", *SOURCES]
     if verbose:

@@ -50,7 +50,7 @@ struct syncr_cdc {
     syncr_cdc_params params{};
     KParams kp{};
     hipStream_t stream = nullptr;
-    int run = DEFAULT_RUN;          // scan geometry (bytes per lane-run)
+    ScanGeom geom{SCAN_MFMA, DEFAULT_NB, MFV_SINGLE | MFV_NOPIPE};  // scan kernel and tile geometry
     uint32_t scan_grid = 0;         // persistent scan grid (CUs x resident blocks)
 
     // plan
@@ -116,6 +116,7 @@ KParams make_kparams(const syncr_cdc_params &p) {
     k.kmv = km | (km << 16);
     k.max_chunk = p.max_chunk;
     k.read_cap = p.read_cap;
+    k.nt = 1;              // tile bytes are read once: non-temporal loads (SYNCR_CDC_NT=0 to disable)
     return k;
 }
 
@@ -131,7 +132,7 @@ Tables make_tables(syncr_cdc *h) {
     Tables t{};
     t.span = h->span;
     t.ntiles = h->ntiles;
-    t.tile = (uint32_t)tile_bytes(h->run);
+    t.tile = (uint32_t)scan_tile_bytes(h->geom);
     t.nwords = h->nwords;
     t.nstarts = h->nstarts;
     t.fstart = h->fstart.as<uint64_t>();
@@ -181,7 +182,7 @@ int32_t ensure_dense(syncr_cdc *h, uint32_t cap) {
     h->dense_cap = cap;
     CHECK_HIP(h->dense_list.ensure(std::max<size_t>(cap, 1) * 4));
     CHECK_HIP(h->dense_cnt.ensure(std::max<size_t>(cap, 1) * 4));
-    CHECK_HIP(h->dense_bits.ensure(std::max<size_t>(cap, 1) * (size_t)(tile_bytes(h->run) / 32) * 4));
+    CHECK_HIP(h->dense_bits.ensure(std::max<size_t>(cap, 1) * (size_t)(scan_tile_bytes(h->geom) / 32) * 4));
     return SYNCR_CDC_OK;
 }
 
@@ -218,7 +219,7 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     }
     CHECK_HIP(hipMemsetAsync(h->zeroed.p, 0, zeroed_bytes(h), s));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[0], s));
-    CHECK_HIP(launch_scan(h->run, h->scan_grid, d_bytes, kp, t, s));
+    CHECK_HIP(launch_scan(h->geom, h->scan_grid, d_bytes, kp, t, s));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[1], s));
     CHECK_HIP(launch_post(d_bytes, kp, t, s, nullptr));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[2], s));
@@ -286,15 +287,27 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     h->params = prm;
     h->kp = make_kparams(prm);
     if (const char *a = getenv("SYNCR_CDC_ABLATE")) h->kp.ablate = (uint32_t)atoi(a);  // timing-only
+    if (const char *nt = getenv("SYNCR_CDC_NT")) h->kp.nt = (uint32_t)atoi(nt);
     if (const char *rs = getenv("SYNCR_CDC_RESOLVE")) h->kp.resolve_lane = strcmp(rs, "lane") == 0;
-    if (const char *r = getenv("SYNCR_CDC_RUN")) {
-        const int v = atoi(r);
-        if (run_supported(v)) h->run = v;
+    // scan variant (timing / A-B only; every variant is exact)
+    if (const char *k = getenv("SYNCR_CDC_SCAN")) {
+        if (strcmp(k, "valu") == 0) h->geom = ScanGeom{SCAN_VALU, DEFAULT_RUN, 0};
+    }
+    if (const char *r = getenv("SYNCR_CDC_RUN")) {      // implies the VALU scan
+        const ScanGeom g{SCAN_VALU, atoi(r), 0};
+        if (scan_supported(g)) h->geom = g;
+    }
+    if (const char *r = getenv("SYNCR_CDC_NB")) {       // implies the MFMA scan
+        const ScanGeom g{SCAN_MFMA, atoi(r), h->geom.kind == SCAN_MFMA ? h->geom.var : 0};
+        if (scan_supported(g)) h->geom = g;
+    }
+    if (const char *v = getenv("SYNCR_CDC_MFVAR")) {    // MFV_* bits of the MFMA scan
+        if (h->geom.kind == SCAN_MFMA) h->geom.var = atoi(v) & 3;
     }
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
         cus = 256;
-    h->scan_grid = (uint32_t)(cus * scan_blocks_per_cu(h->run));
+    h->scan_grid = (uint32_t)(cus * scan_blocks_per_cu(h->geom));
     if (const char *g = getenv("SYNCR_CDC_SCAN_GRID")) {
         const int v = atoi(g);
         if (v > 0) h->scan_grid = (uint32_t)v;
@@ -348,7 +361,7 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
             starts[j] = file_off[ne[j]];
             if (j && file_off[ne[j - 1]] + file_len[ne[j - 1]] > starts[j]) return SYNCR_CDC_EINVAL;
         }
-        const int TILE = tile_bytes(h->run);
+        const int TILE = scan_tile_bytes(h->geom);
         const uint64_t ntiles64 = (span + TILE - 1) / TILE;
         if (ntiles64 > 0x7fffffffull) return SYNCR_CDC_EINVAL;
         h->nfiles = nfiles;
@@ -655,12 +668,12 @@ extern "C" int32_t syncr_cdc_get_info(const syncr_cdc *h, uint64_t *info8) {
     if (!h || !info8) return SYNCR_CDC_EINVAL;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) cus = 0;
-    info8[0] = (uint64_t)h->run;
-    info8[1] = (uint64_t)tile_bytes(h->run);
+    info8[0] = (uint64_t)(h->geom.kind * 1000 + h->geom.param);
+    info8[1] = (uint64_t)scan_tile_bytes(h->geom);
     info8[2] = h->scan_grid;
     info8[3] = (uint64_t)cus;
-    info8[4] = (uint64_t)scan_blocks_per_cu(h->run);
-    info8[5] = (uint64_t)lds_wave_bytes(h->run);
+    info8[4] = (uint64_t)scan_blocks_per_cu(h->geom);
+    info8[5] = (uint64_t)scan_lds_bytes(h->geom);
     info8[6] = (uint64_t)h->device;
     info8[7] = SYNCR_CDC_ABI_VERSION;
     return SYNCR_CDC_OK;

@@ -18,6 +18,27 @@ constexpr uint32_t DENSE_BIT = 0x80000000u;
 constexpr uint64_t NONE = ~0ull;
 constexpr int DEFAULT_RUN = 80;
 
+// MFMA scan (cdc_scan_mfma_kernel): a wave tile is 32 streams x NB blocks of
+// 32 bytes; W for a 32-position block is a Toeplitz product of the block and
+// its two predecessors (three v_mfma_i32_32x32x32_i8).
+constexpr int MF_STREAMS = 32;
+constexpr int DEFAULT_NB = 10;
+__host__ __device__ constexpr int mf_tile_bytes(int nb) { return 1024 * nb; }
+__host__ __device__ constexpr int mf_buf_bytes(int nb) { return HALO + 1024 * nb; }
+// landing buffers (2: tile t+1 in flight while tile t is filtered; 1: the
+// buffer is recycled as soon as the tile is in registers) + candidate list
+__host__ __device__ constexpr int mf_lds_bytes(int nb, int nbuf) { return nbuf * mf_buf_bytes(nb) + LISTCAP * 4 + 16; }
+
+// Scan geometry: kind 0 = packed-u16 VALU roll (param = RUN bytes per lane
+// run), kind 1 = MFMA Toeplitz filter (param = NB blocks per stream).
+enum { SCAN_VALU = 0, SCAN_MFMA = 1 };
+enum { MFV_SINGLE = 1, MFV_NOPIPE = 2 };   // MFMA scan variants (ScanGeom::var)
+struct ScanGeom {
+    int kind;
+    int param;
+    int var;     // MFMA: MFV_* bits
+};
+
 __host__ __device__ constexpr int tile_bytes(int run) { return run * RUNS; }
 __host__ __device__ constexpr int buf_bytes(int run) { return HALO + run * RUNS; }
 // LDS per wave: one tile landing buffer + 16 dirty-group slots (80 B) +
@@ -42,7 +63,8 @@ struct KParams {
     uint32_t k;        // scalar k
     uint64_t max_chunk;
     uint64_t read_cap; // 0 = unlimited (ideal semantics)
-    uint32_t ablate;   // timing-only diagnostics (SYNCR_CDC_ABLATE): 1 = no rolling, 2 = no DMA
+    uint32_t ablate;   // timing-only diagnostics (SYNCR_CDC_ABLATE): 1 = no rolling, 2 = no DMA, 3 = 1 with nt
+    uint32_t nt;       // 1: non-temporal tile loads (SYNCR_CDC_NT=1)
     uint32_t resolve_lane;  // 1: lane-per-file resolve (SYNCR_CDC_RESOLVE=lane); 0: wave-per-file
 };
 
@@ -55,7 +77,7 @@ struct DevCut {        // == syncr_cut
 struct Tables {
     uint64_t span;                 // bytes [0, span) of d_bytes are addressable
     uint32_t ntiles;
-    uint32_t tile;                 // bytes per tile (= RUN * RUNS)
+    uint32_t tile;                 // bytes per tile (scan_tile_bytes)
     uint32_t nwords;               // ceil(ntiles / 64)
     uint32_t nstarts;              // non-empty files (sorted starts)
     const uint64_t *fstart;        // [nstarts] sorted file starts
@@ -82,9 +104,11 @@ struct Tables {
 };
 
 // launchers (cdc_kernels.hip)
-bool run_supported(int run);
-int scan_blocks_per_cu(int run);
-hipError_t launch_scan(int run, uint32_t grid, const uint8_t *d_bytes, const KParams &p, const Tables &t,
+bool scan_supported(ScanGeom g);
+int scan_tile_bytes(ScanGeom g);
+int scan_lds_bytes(ScanGeom g);
+int scan_blocks_per_cu(ScanGeom g);
+hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d_bytes, const KParams &p, const Tables &t,
                        hipStream_t s);
 hipError_t launch_post(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s,
                        hipEvent_t after_dense);

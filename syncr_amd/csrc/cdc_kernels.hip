@@ -47,6 +47,14 @@ __device__ __forceinline__ u16x2 pk_mad(uint32_t a, uint32_t b_uniform, u16x2 c)
     return as_u16x2(r);
 }
 
+// min of the low 16-bit halves of three registers.  Plain C, not
+// inline asm: the operands come straight from MFMA results, and only
+// compiler-visible instructions get the MFMA -> VALU wait states.
+__device__ __forceinline__ uint32_t min3_lo16(uint32_t a, uint32_t b, uint32_t c) {
+    const unsigned short x = (unsigned short)a, y = (unsigned short)b, z = (unsigned short)c;
+    return __builtin_elementwise_min(__builtin_elementwise_min(x, y), z);
+}
+
 // LDS byte address of a generic pointer into dynamic shared memory.
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
@@ -73,17 +81,29 @@ template <int N> __device__ __forceinline__ void wait_vmcnt() {
 // 16 B per lane, HBM -> LDS (M0 = wave-uniform LDS base; lane l lands at +16*l).
 // Written as inline asm so hipcc does not drain it with vmcnt(0) before the
 // ds_reads of the OTHER buffer; completion is tracked by hand (wait_vmcnt).
+template <bool NT>
 __device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds) {
     uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds)
-        : "memory");
+    if constexpr (NT)
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off nt\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(gsrc), "s"(lds)
+            : "memory");
+    else
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(gsrc), "s"(lds)
+            : "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -184,7 +204,6 @@ __device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
     const uint32_t tA = ((124993u + WA) * P.k) & 0xffffu;
     const uint32_t tB = ((124993u + WB) * P.k) & 0xffffu;
     u16x2 Tv = as_u16x2(tA | (tB << 16));
-    const u16x2 kk = as_u16x2(P.kk), km = as_u16x2(P.kmv);
     const uint32_t want = (recA ? 1u : 0u) | (recB ? 2u : 0u);
 #pragma unroll
     for (int g = 0; g < RUN / 16; ++g) {
@@ -249,20 +268,29 @@ __device__ __forceinline__ void rewalk_dirty(const KParams &P, int lane, uint32_
     }
 }
 
-// First chunk-local hit in [e+1, e+63] from global memory (all loads issued up front).
+// First chunk-local hit in [e+1, e+63] from global memory.  Bytes are loaded
+// 16 at a time (one chunk's loads in flight) to bound the register footprint
+// of the scan kernels that inline it; it runs once per recorded edge.
 __device__ __forceinline__ uint32_t head_fix_global(const uint8_t *data, uint64_t span, uint64_t e,
                                                     uint32_t mask) {
-    uint32_t x[63];
+    uint32_t S = 0, W = 0;
+#pragma unroll 1
+    for (int k0 = 0; k0 < 64; k0 += 16) {
+        uint32_t x[16];
 #pragma unroll
-    for (int k = 0; k < 63; ++k) x[k] = (e + 1 + k < span) ? data[e + 1 + k] : 0u;
-    uint32_t S = 0, W = 0, found = 0;
+        for (int k = 0; k < 16; ++k) {
+            const uint64_t q = e + 1 + (uint64_t)(k0 + k);
+            x[k] = (k0 + k < 63 && q < span) ? data[q] : 0u;
+        }
 #pragma unroll
-    for (int k = 0; k < 63; ++k) {
-        S += x[k];
-        W += S;
-        if (!found && e + 1 + k < span && hit_exact(S, W, mask)) found = (uint32_t)k + 1;
+        for (int k = 0; k < 16; ++k) {
+            S += x[k];
+            W += S;
+            const uint64_t q = e + 1 + (uint64_t)(k0 + k);
+            if (k0 + k < 63 && q < span && hit_exact(S, W, mask)) return (uint32_t)(k0 + k) + 1;
+        }
     }
-    return found;
+    return 0;
 }
 
 // Publish this tile's candidates (sorted, with head fix-ups) or mark it dense.
@@ -295,8 +323,9 @@ __device__ __forceinline__ void publish_tile(const uint8_t *__restrict__ data, c
     uint32_t rank = 0;
     for (uint32_t m = 0; m < n; ++m) rank += wlist[m] < e;
     if ((uint32_t)lane < n) {
-        const uint32_t fix = head_fix_global(data, T.span, (uint64_t)t0 + e, P.mask);
-        T.slots[(size_t)tile * LISTCAP + rank] = make_uint2(e, fix);
+        // head fix-ups are computed by cdc_fix_kernel: a global load here would
+        // be waited with vmcnt, which drains the in-flight tile DMA
+        T.slots[(size_t)tile * LISTCAP + rank] = make_uint2(e, 0u);
     }
     if (lane == 0) {
         T.tile_meta[tile] = n;
@@ -305,25 +334,39 @@ __device__ __forceinline__ void publish_tile(const uint8_t *__restrict__ data, c
 }
 
 // 16 B per lane from a wave-uniform SGPR base + per-lane VGPR offset into LDS.
+// NT: non-temporal policy (the bytes are read exactly once).
+template <bool NT>
 __device__ __forceinline__ void dma16_s(uint32_t voff, uint64_t sbase, uint32_t lds) {
     uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %3\n\t"
-        "s_nop 4\n\t"
-        "global_load_lds_dwordx4 %1, %2\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(voff), "s"(sbase), "s"(lds)
-        : "memory");
+    if constexpr (NT)
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %3\n\t"
+            "s_nop 4\n\t"
+            "global_load_lds_dwordx4 %1, %2 nt\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(sbase), "s"(lds)
+            : "memory");
+    else
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %3\n\t"
+            "s_nop 4\n\t"
+            "global_load_lds_dwordx4 %1, %2\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(sbase), "s"(lds)
+            : "memory");
 }
 
-template <int RUN>
-__device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, uint32_t tile,
-                                           uint32_t lds_buf, int lane) {
-    constexpr int BUF = buf_bytes(RUN);
+// DMA of tile `tile`'s bytes [tile*TILE - HALO, tile*TILE + TILE) into the
+// wave's LDS landing buffer (BUF = HALO + TILE bytes).
+template <int BUF, int TILE, bool NT>
+__device__ __forceinline__ void issue_buf(const uint8_t *data, uint64_t span, uint32_t tile,
+                                          uint32_t lds_buf, int lane) {
     constexpr int NDMA = (BUF + 1023) / 1024;
-    const int64_t base = (int64_t)tile * tile_bytes(RUN) - HALO;
+    const int64_t base = (int64_t)tile * TILE - HALO;
     if (base >= 0 && (uint64_t)base + BUF <= span) {      // interior tile: SGPR base + lane*16
         const uint64_t b = (uint64_t)(data + base);
         const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
@@ -332,7 +375,7 @@ __device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, u
 #pragma unroll
         for (int i = 0; i < NDMA; ++i) {
             if (i < NDMA - 1 || i * 1024 + lane * 16 < BUF)
-                dma16_s((uint32_t)lane * 16u, ub + (uint64_t)i * 1024u, lds_buf + (uint32_t)(i * 1024));
+                dma16_s<NT>((uint32_t)lane * 16u, ub + (uint64_t)i * 1024u, lds_buf + (uint32_t)(i * 1024));
         }
         return;
     }
@@ -344,8 +387,14 @@ __device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, u
         const int off = i * 1024 + lane * 16;
         int64_t g = base + off;
         g = g < 0 ? 0 : (g > last ? last : g);
-        if (i < NDMA - 1 || off < BUF) dma16(data + g, lds_buf + (uint32_t)(i * 1024));
+        if (i < NDMA - 1 || off < BUF) dma16<NT>(data + g, lds_buf + (uint32_t)(i * 1024));
     }
+}
+
+template <int RUN, bool NT>
+__device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, uint32_t tile,
+                                           uint32_t lds_buf, int lane) {
+    issue_buf<buf_bytes(RUN), tile_bytes(RUN), NT>(data, span, tile, lds_buf, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -355,9 +404,10 @@ __device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, u
 // tile and under the other resident waves.  The scan knows nothing about files:
 // it computes G over the batch as one continuous stream (see cdc_boundary_kernel).
 // ---------------------------------------------------------------------------
-// MODE 0 is the product; MODE 1 (staging only) and 2 (no DMA) are timing-only
-// ablations selected by SYNCR_CDC_ABLATE, compiled separately so they cannot
-// perturb the product's register allocation.
+// MODE bits 0-1: 0 is the product; 1 (staging only) and 2 (no DMA) are
+// timing-only ablations selected by SYNCR_CDC_ABLATE, compiled separately so
+// they cannot perturb the product's register allocation.  Bit 2: non-temporal
+// tile loads (SYNCR_CDC_NT).
 template <int RUN, int MODE>
 __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P,
                                                       Tables T) {
@@ -376,7 +426,7 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
     uint32_t tile = blockIdx.x;
     if (tile >= T.ntiles) return;
     const int64_t span = (int64_t)T.span;
-    issue_tile<RUN>(data, T.span, tile, lds0, lane);
+    issue_tile<RUN, (MODE & 4) != 0>(data, T.span, tile, lds0, lane);
     for (; tile < T.ntiles; tile += stride) {
         const uint32_t next = tile + stride;
         const int64_t t0 = (int64_t)tile * TILE;
@@ -394,15 +444,15 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");           // runs are in registers
-        if (next < T.ntiles && MODE != 2) issue_tile<RUN>(data, T.span, next, lds0, lane);
-        if constexpr (MODE == 1) {                                   // diagnostics: staging only
+        if (next < T.ntiles && (MODE & 3) != 2) issue_tile<RUN, (MODE & 4) != 0>(data, T.span, next, lds0, lane);
+        if constexpr ((MODE & 3) == 1) {                                   // diagnostics: staging only
 #pragma unroll
             for (int q = 0; q < NQ * 4; ++q) asm volatile("" ::"v"(A[q]), "v"(B[q]));
             continue;
         }
         const int64_t lim_rel = span - t0;                           // positions >= span are not bytes
         roll_fast<RUN>(A, B, P, lane, true, true, dcount, dslots);
-        if constexpr (MODE == 2) continue;                          // diagnostics: rolling only
+        if constexpr ((MODE & 3) == 2) continue;                          // diagnostics: rolling only
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         const uint32_t nd = __builtin_amdgcn_readfirstlane(
@@ -411,6 +461,199 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
         if (nd) rewalk_dirty<RUN>(P, lane, nd < (uint32_t)DIRTYCAP ? nd : (uint32_t)DIRTYCAP, dslots,
                                   lim_rel, wcount, wlist);
         publish_tile(data, P, T, tile, t0, wlist, wcount, lane, nd > (uint32_t)DIRTYCAP);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA scan.  W at position n is a 64-tap FIR of the bytes:
+//     W(n) = sum_{a=0..63} (a+1) * x[n-a],    S(n) = sum_{a=0..63} x[n-a]
+// (the closed form of Bup's s2 / s1 recurrences).  For a block of 32
+// positions [32b, 32b+32) of one stream it is a product with three constant
+// 32x32 Toeplitz matrices:  W_b = M0 X_b + M1 X_{b-1} + M2 X_{b-2}, where
+// X_b is the block's bytes and Mq[i][k] = w(32q + i - k), w(a) = a+1 on
+// [0, 63].  v_mfma_i32_32x32x32_i8 evaluates it for 32 streams at once: the
+// stream is the MFMA column, lane (c, h) holds 16 bytes of block b of stream
+// c, so the two predecessor blocks are the same lane's previous registers.
+// Bytes enter as signed i8 (x ^ 0x80 = x - 128); the 128*2080 bias and the
+// hit target are folded into the accumulator's initial value.
+//
+// The filter tests only the s2 half of the digest (W + 124993 == 0 mod 2^bw,
+// bw = min(bits, 16)), a superset of the edges.  A wave that sees a filter
+// hit anywhere in its tile redoes the tile exactly (W and S by MFMA, then the
+// full digest test) and records the true edges.  Expected filter hits per
+// 8 KiB tile at bits = 20: 0.125.
+// ---------------------------------------------------------------------------
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int FIR_SUM_W = 2080;          // sum of the weights 1..64
+constexpr int S2_BIAS = 124993;          // s2 + 1 = 124993 + W (Bup's CHAR_OFFSET terms)
+
+// Lane fragment of Mq (A operand): lane (i = l&31, h = l>>5) byte j holds
+// Mq[i][16h + j] (verified on gfx950 by tools/mfma_i8_check.hip).
+__device__ __forceinline__ v4i fir_matrix(int q, int lane, bool ones) {
+    const int i = lane & 31, h = lane >> 5;
+    int d[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int a = 32 * q + i - (16 * h + 4 * m + b);
+            const uint32_t w = (a >= 0 && a <= 63) ? (ones ? 1u : (uint32_t)(a + 1)) : 0u;
+            v |= w << (8 * b);
+        }
+        d[m] = (int)v;
+    }
+    return v4i{d[0], d[1], d[2], d[3]};
+}
+
+// output row of accumulator register v on lane half h (gfx950 32x32 C/D map)
+__device__ __forceinline__ int mf_row(int v, int h) { return (v & 3) + 8 * (v >> 2) + 4 * h; }
+
+__device__ __forceinline__ v16i splat16(int x) {
+    v16i c;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) c[v] = x;
+    return c;
+}
+
+// MODE bits as cdc_scan_kernel (0 product, 1 staging only, 2 no DMA; 4 nt),
+// plus 8: one landing buffer, 16: no software pipelining of the MFMA chains.
+// LOW16: bits >= 16 (the filter tests whole low halves, no scaling).
+template <int NB, int MODE, bool LOW16>
+__global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__restrict__ data, KParams P,
+                                                           Tables T) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int BUF = mf_buf_bytes(NB);
+    constexpr int TILE = mf_tile_bytes(NB);
+    constexpr int L = 32 * NB;                        // bytes per stream
+    constexpr bool NT = (MODE & 4) != 0;
+    const int lane = threadIdx.x, c = lane & 31, h = lane >> 5;
+    constexpr int NDMA = (BUF + 1023) / 1024;         // DMA instructions per tile
+    constexpr bool DB = (MODE & 8) == 0;              // double-buffered landing
+    constexpr bool PIPE = (MODE & 16) == 0;
+    uint8_t *wl = smem;                               // landing buffers wl[0..BUF), wl[BUF..2BUF)
+    uint32_t *wlist = (uint32_t *)(smem + (DB ? 2 : 1) * BUF);
+    uint32_t *wcount = wlist + LISTCAP;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
+    const uint32_t stride = gridDim.x;
+    uint32_t tile = blockIdx.x;
+    if (tile >= T.ntiles) return;
+    const int64_t span = (int64_t)T.span;
+    const v4i M0 = fir_matrix(0, lane, false), M1 = fir_matrix(1, lane, false),
+              M2 = fir_matrix(2, lane, false);
+    const int cinit = 128 * FIR_SUM_W + S2_BIAS;      // D = W + 124993
+    const u16x2 kk = as_u16x2(P.kk);
+    issue_buf<BUF, TILE, NT>(data, T.span, tile, lds0, lane);
+    if (DB && tile + stride < T.ntiles && (MODE & 3) != 2)
+        issue_buf<BUF, TILE, NT>(data, T.span, tile + stride, lds0 + BUF, lane);
+    uint32_t cur = 0;                                 // buffer of this tile
+    for (; tile < T.ntiles; tile += stride, cur ^= (DB ? 1u : 0u)) {
+        const uint32_t after = tile + (DB ? 2 : 1) * stride;   // lands in this tile's buffer
+        const int64_t t0 = (int64_t)tile * TILE;
+        if (lane == 0) *wcount = 0u;
+        // this tile has landed (vm ops complete in order: at most the next
+        // tile's NDMA loads, or anything younger, may still be in flight)
+        if (DB && tile + stride < T.ntiles && (MODE & 3) != 2) wait_vmcnt<NDMA>(); else wait_vmcnt<0>();
+        v4i X[NB + 2];                                // X[b] = block b-2 of stream c, half h
+        {
+            const uint8_t *lp = wl + cur * BUF + HALO + c * L + 16 * h - 64;
+#pragma unroll
+            for (int b = 0; b < NB + 2; ++b) X[b] = *(const v4i *)(lp + 32 * b);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (after < T.ntiles && (MODE & 3) != 2)
+            issue_buf<BUF, TILE, NT>(data, T.span, after, lds0 + cur * BUF, lane);
+        if constexpr ((MODE & 3) == 1) {
+#pragma unroll
+            for (int b = 0; b < NB + 2; ++b) asm volatile("" ::"v"(X[b]));
+            continue;
+        }
+#pragma unroll
+        for (int b = 0; b < NB + 2; ++b) X[b] ^= (int)0x80808080;
+        // filter, software-pipelined: block b+1's MFMA chain is issued before
+        // block b's test so the matrix pipe runs under the VALU work
+        auto chain = [&](const v4i &x0, const v4i &x1, const v4i &x2) -> v16i {
+            v16i d = splat16(cinit);
+            d = __builtin_amdgcn_mfma_i32_32x32x32_i8(M0, x0, d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_i32_32x32x32_i8(M1, x1, d, 0, 0, 0);
+            return __builtin_amdgcn_mfma_i32_32x32x32_i8(M2, x2, d, 0, 0, 0);
+        };
+        uint32_t acc = 0xffffffffu;
+        v16i dn = chain(X[2], X[1], X[0]);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            v16i d = dn;
+            if constexpr (PIPE) {
+                if (b + 1 < NB) dn = chain(X[b + 3], X[b + 2], X[b + 1]);
+            } else if (b > 0) {
+                d = chain(X[b + 2], X[b + 1], X[b]);
+            }
+            if constexpr (LOW16) {
+#pragma unroll
+                for (int v = 0; v < 16; v += 2) acc = min3_lo16(acc, (uint32_t)d[v], (uint32_t)d[v + 1]);
+            } else {
+#pragma unroll
+                for (int v = 0; v < 16; v += 2) {
+                    u16x2 q = as_u16x2(__builtin_amdgcn_perm((uint32_t)d[v + 1], (uint32_t)d[v], 0x05040100u));
+                    q = q * kk;                       // keep the low bw bits only
+                    acc = as_u32(__builtin_elementwise_min(as_u16x2(acc), q));
+                }
+            }
+            // bound the live accumulators to two blocks (the scheduler would
+            // otherwise hoist every block's MFMAs and spill)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const bool z = LOW16 ? (acc & 0xffffu) == 0u : ((acc & 0xffffu) == 0u || (acc >> 16) == 0u);
+        if constexpr ((MODE & 3) == 2) {              // diagnostics: filter only (stale LDS bytes)
+            if (z) record(wcount, wlist, 0u);
+            continue;
+        }
+        if (__builtin_expect(__ballot(z) != 0ull, 0)) {
+            // exact pass over the tile: W and S for every position, full digest
+            // test.  W and S are taken one after the other (16 accumulator
+            // registers live).
+            auto ones = [](v4i m) {                   // byte != 0 -> 1 (bytes <= 64)
+                asm volatile("" : "+v"(m));           // opaque: not hoisted into the hot loop
+                v4i o;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    o[q] = (int)((((uint32_t)m[q] + 0x7f7f7f7fu) >> 7) & 0x01010101u);
+                return o;
+            };
+            const int64_t lim_rel = span - t0;
+            const uint32_t bw = P.bits < 16 ? P.bits : 16u;
+            const uint32_t wmask = (1u << bw) - 1u;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const v16i w = chain(X[b + 2], X[b + 1], X[b]);
+                uint32_t hm = 0;                      // s2 half of the digest
+#pragma unroll
+                for (int v = 0; v < 16; ++v) hm |= (((uint32_t)w[v] & wmask) == 0u ? 1u : 0u) << v;
+                __builtin_amdgcn_sched_barrier(0);
+                // s1 half: (1984 + S) & m1 == m1.  Wave-uniform branch: an MFMA
+                // reads operands from every lane, so none may be masked off.
+                if (P.m1 && __ballot(hm != 0u) != 0ull) {
+                    v16i sm = __builtin_amdgcn_mfma_i32_32x32x32_i8(ones(M0), X[b + 2], splat16(0), 0, 0, 0);
+                    sm = __builtin_amdgcn_mfma_i32_32x32x32_i8(ones(M1), X[b + 1], sm, 0, 0, 0);
+                    sm = __builtin_amdgcn_mfma_i32_32x32x32_i8(ones(M2), X[b], sm, 0, 0, 0);
+                    uint32_t sh = 0;                  // S = sm + 128 * 64
+#pragma unroll
+                    for (int v = 0; v < 16; ++v)
+                        sh |= (((1984u + 8192u + (uint32_t)sm[v]) & P.m1) == P.m1 ? 1u : 0u) << v;
+                    hm &= sh;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                while (hm) {
+                    const int v = __builtin_ctz(hm);
+                    hm &= hm - 1u;
+                    const uint32_t rel = (uint32_t)(c * L + 32 * b + mf_row(v, h));
+                    if ((int64_t)rel < lim_rel) record(wcount, wlist, rel);
+                }
+            }
+        }
+        publish_tile(data, P, T, tile, t0, wlist, wcount, lane, false);
     }
 }
 
@@ -540,7 +783,7 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
         const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
         for (uint32_t j = 0; j < c; ++j) {
             const uint2 v = sl[j];
-            T.cand[base + j] = (t0 + v.x) | ((uint64_t)v.y << 48) | CAND_KNOWN;
+            T.cand[base + j] = t0 + v.x;               // fix-up: cdc_fix_kernel
         }
     } else {
         const uint32_t *bm = T.dense_bits + (size_t)(meta & ~DENSE_BIT) * (T.tile / 32);
@@ -553,6 +796,19 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
                 T.cand[o++] = t0 + r;
             }
         }
+    }
+}
+
+// Head fix-up of every candidate e (first chunk-local hit in [e+1, e+63]),
+// one thread per candidate, so the resolve walk never waits on byte loads.
+__global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict__ data, KParams P,
+                                                      Tables T) {
+    const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
+    const uint64_t n = total < T.cand_cap ? total : T.cand_cap;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t e = T.cand[i] & CAND_POS_MASK;
+        const uint32_t fix = head_fix_global(data, T.span, e, P.mask);
+        T.cand[i] = e | ((uint64_t)fix << 48) | CAND_KNOWN;
     }
 }
 
@@ -832,12 +1088,39 @@ __global__ __launch_bounds__(256) void cdc_gen_kernel(uint8_t *__restrict__ base
 }
 
 // ---------------------------------------------------------------------------
-bool run_supported(int run) { return run == 48 || run == 80 || run == 112 || run == 144 || run == 176; }
+static bool valu_run_ok(int run) { return run == 48 || run == 80 || run == 112 || run == 144 || run == 176; }
+static bool mfma_nb_ok(int nb) { return nb == 4 || nb == 6 || nb == 8 || nb == 10 || nb == 12; }
 
-template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN, 0>; }
+bool scan_supported(ScanGeom g) {
+    return g.kind == SCAN_VALU ? valu_run_ok(g.param) : (g.kind == SCAN_MFMA && mfma_nb_ok(g.param));
+}
+int scan_tile_bytes(ScanGeom g) { return g.kind == SCAN_VALU ? tile_bytes(g.param) : mf_tile_bytes(g.param); }
+int scan_lds_bytes(ScanGeom g) {
+    return g.kind == SCAN_VALU ? lds_wave_bytes(g.param) : mf_lds_bytes(g.param, (g.var & MFV_SINGLE) ? 1 : 2);
+}
 
-static const void *scan_kernel_ptr(int run) {
-    switch (run) {
+template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN, 4>; }
+template <int NB> static const void *mfma_fn(int var) {
+    switch (var & 3) {
+        case 0: return (const void *)&cdc_scan_mfma_kernel<NB, 4, true>;
+        case 1: return (const void *)&cdc_scan_mfma_kernel<NB, 4 | 8, true>;
+        case 2: return (const void *)&cdc_scan_mfma_kernel<NB, 4 | 16, true>;
+        default: return (const void *)&cdc_scan_mfma_kernel<NB, 4 | 8 | 16, true>;
+    }
+}
+
+static const void *scan_kernel_ptr(ScanGeom g) {
+    if (g.kind == SCAN_MFMA) {
+        switch (g.param) {
+            case 4: return mfma_fn<4>(g.var);
+            case 6: return mfma_fn<6>(g.var);
+            case 8: return mfma_fn<8>(g.var);
+            case 10: return mfma_fn<10>(g.var);
+            case 12: return mfma_fn<12>(g.var);
+            default: return nullptr;
+        }
+    }
+    switch (g.param) {
         case 48: return scan_fn<48>();
         case 80: return scan_fn<80>();
         case 112: return scan_fn<112>();
@@ -847,31 +1130,76 @@ static const void *scan_kernel_ptr(int run) {
     }
 }
 
-int scan_blocks_per_cu(int run) {
+int scan_blocks_per_cu(ScanGeom g) {
     int n = 0;
-    const void *f = scan_kernel_ptr(run);
-    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 64, lds_wave_bytes(run)) != hipSuccess)
+    const void *f = scan_kernel_ptr(g);
+    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 64, scan_lds_bytes(g)) != hipSuccess)
         return 1;
     return n > 0 ? n : 1;
 }
 
 template <int RUN>
 static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    if (p.ablate == 1u && (RUN == DEFAULT_RUN || RUN == 144))
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, (RUN == DEFAULT_RUN || RUN == 144) ? 1 : 0>), dim3(grid),
-                           dim3(64), lds_wave_bytes(RUN), s, d, p, t);
-    else if (p.ablate == 2u && (RUN == DEFAULT_RUN || RUN == 144))
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, (RUN == DEFAULT_RUN || RUN == 144) ? 2 : 0>), dim3(grid),
-                           dim3(64), lds_wave_bytes(RUN), s, d, p, t);
+    constexpr bool ABL = RUN == DEFAULT_RUN || RUN == 144;     // ablation instances
+    const size_t lds = lds_wave_bytes(RUN);
+    if (ABL && p.ablate == 1u)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, ABL ? 1 : 0>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (ABL && p.ablate == 2u)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, ABL ? 2 : 0>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (ABL && p.ablate == 3u)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, ABL ? 5 : 0>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.nt)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 4>), dim3(grid), dim3(64), lds, s, d, p, t);
     else
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 0>), dim3(grid), dim3(64), lds_wave_bytes(RUN), s, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 0>), dim3(grid), dim3(64), lds, s, d, p, t);
 }
 
-hipError_t launch_scan(int run, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
+template <int NB, int V>
+static void launch_mfma_v(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
+    constexpr int VM = ((V & MFV_SINGLE) ? 8 : 0) | ((V & MFV_NOPIPE) ? 16 : 0);
+    const size_t lds = mf_lds_bytes(NB, (V & MFV_SINGLE) ? 1 : 2);
+    const bool low16 = p.bits >= 16;
+    if (p.ablate == 1u || p.ablate == 3u)
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 5, true>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 2u)
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 2, true>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (low16 && p.nt)
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, true>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (low16)
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, true>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.nt)
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, false>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, false>), dim3(grid), dim3(64), lds, s, d, p, t);
+}
+
+template <int NB>
+static void launch_mfma_t(int var, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
+                          hipStream_t s) {
+    switch (var & 3) {
+        case 0: launch_mfma_v<NB, 0>(grid, d, p, t, s); break;
+        case 1: launch_mfma_v<NB, 1>(grid, d, p, t, s); break;
+        case 2: launch_mfma_v<NB, 2>(grid, d, p, t, s); break;
+        default: launch_mfma_v<NB, 3>(grid, d, p, t, s); break;
+    }
+}
+
+hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
                        hipStream_t s) {
     if (!t.ntiles) return hipSuccess;
     grid = grid < t.ntiles ? grid : t.ntiles;
-    switch (run) {
+    if (g.kind == SCAN_MFMA) {
+        switch (g.param) {
+            case 4: launch_mfma_t<4>(g.var, grid, d, p, t, s); break;
+            case 6: launch_mfma_t<6>(g.var, grid, d, p, t, s); break;
+            case 8: launch_mfma_t<8>(g.var, grid, d, p, t, s); break;
+            case 10: launch_mfma_t<10>(g.var, grid, d, p, t, s); break;
+            case 12: launch_mfma_t<12>(g.var, grid, d, p, t, s); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    switch (g.param) {
         case 48: launch_scan_t<48>(grid, d, p, t, s); break;
         case 80: launch_scan_t<80>(grid, d, p, t, s); break;
         case 112: launch_scan_t<112>(grid, d, p, t, s); break;
@@ -893,6 +1221,11 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
         hipLaunchKernelGGL(cdc_boundary_kernel, dim3((t.nfiles + 255) / 256), dim3(256), 0, s, d, p, t);
     hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
     hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4), dim3(256), 0, s, t);
+    {
+        const uint64_t want = (t.cand_cap + 255) / 256;
+        const uint32_t blocks = (uint32_t)(want < 2048 ? (want ? want : 1) : 2048);
+        hipLaunchKernelGGL(cdc_fix_kernel, dim3(blocks), dim3(256), 0, s, d, p, t);
+    }
     return hipGetLastError();
 }
 
