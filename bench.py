@@ -215,7 +215,7 @@ def main(argv=None):
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": (int(tr["hbm_bytes_per_launch"]) if tr else None),
-        "kernel": "cdc_scan_kernel", "kernel_ms": round(scan_ms, 4),
+        "kernel": engine_info["scan_kernel"], "kernel_ms": round(scan_ms, 4),
         "algorithmic_bytes_per_launch": span,
         "dense_ms": round(kms[1] / max(nl, 1), 4), "resolve_ms": round(kms[2] / max(nl, 1), 4),
         "traffic_source": (tr.get("source") if tr else None),

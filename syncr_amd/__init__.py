@@ -265,7 +265,12 @@ class Chunker:
         _check(library().syncr_cdc_get_info(self._h, v), "syncr_cdc_get_info")
         keys = ("run_bytes", "tile_bytes", "scan_grid", "compute_units", "scan_blocks_per_cu",
                 "lds_bytes_per_scan_block", "device", "abi_version")
-        return {k: int(x) for k, x in zip(keys, v)}
+        d = {k: int(x) for k, x in zip(keys, v)}
+        # info8[0] = kind * 1000 + param (cdc_api.cpp syncr_cdc_get_info)
+        d["scan_kernel"] = "cdc_scan_mfma_kernel" if d["run_bytes"] >= 1000 else "cdc_scan_kernel"
+        if d["run_bytes"] >= 1000:
+            d["mfma_blocks"] = d["run_bytes"] - 1000
+        return d
 
     def synchronize(self) -> None:
         _check(library().syncr_cdc_synchronize(self._h), "syncr_cdc_synchronize")

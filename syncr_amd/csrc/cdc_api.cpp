@@ -50,7 +50,10 @@ struct syncr_cdc {
     syncr_cdc_params params{};
     KParams kp{};
     hipStream_t stream = nullptr;
-    ScanGeom geom{SCAN_MFMA, DEFAULT_NB, MFV_SINGLE | MFV_NOPIPE};  // scan kernel and tile geometry
+    // scan kernel and tile geometry: the packed-u16 VALU roll (north_star: integer
+    // work, no MFMA).  The MFMA Toeplitz variant is an opt-in experiment
+    // (SYNCR_CDC_SCAN=mfma).
+    ScanGeom geom{SCAN_VALU, DEFAULT_RUN, 0};
     uint32_t scan_grid = 0;         // persistent scan grid (CUs x resident blocks)
 
     // plan
@@ -62,7 +65,7 @@ struct syncr_cdc {
     uint64_t total_cut_cap = 0;
     std::vector<uint64_t> h_foff, h_flen, h_cut_base;
     std::vector<uint32_t> h_cut_cap;
-    DevBuf fstart, foff, flen, order, cut_base, cut_cap, bmask, tile_meta, slots, zeroed,
+    DevBuf fstart, foff, flen, order, cut_base, cut_cap, tile_meta, slots, zeroed,
         dense_list, dense_cnt, dense_bits, super_off, cand, cuts, counts;
 
     // launch
@@ -156,7 +159,6 @@ Tables make_tables(syncr_cdc *h) {
     t.cand_cap = h->cand_cap;
     t.cuts = h->cuts.as<DevCut>();
     t.counts = h->counts.as<uint64_t>();
-    t.bmask = h->bmask.as<uint64_t>();
     return t;
 }
 
@@ -292,13 +294,14 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     // scan variant (timing / A-B only; every variant is exact)
     if (const char *k = getenv("SYNCR_CDC_SCAN")) {
         if (strcmp(k, "valu") == 0) h->geom = ScanGeom{SCAN_VALU, DEFAULT_RUN, 0};
+        if (strcmp(k, "mfma") == 0) h->geom = ScanGeom{SCAN_MFMA, DEFAULT_NB, MFV_SINGLE | MFV_NOPIPE};
     }
     if (const char *r = getenv("SYNCR_CDC_RUN")) {      // implies the VALU scan
         const ScanGeom g{SCAN_VALU, atoi(r), 0};
         if (scan_supported(g)) h->geom = g;
     }
     if (const char *r = getenv("SYNCR_CDC_NB")) {       // implies the MFMA scan
-        const ScanGeom g{SCAN_MFMA, atoi(r), h->geom.kind == SCAN_MFMA ? h->geom.var : 0};
+        const ScanGeom g{SCAN_MFMA, atoi(r), h->geom.kind == SCAN_MFMA ? h->geom.var : MFV_SINGLE | MFV_NOPIPE};
         if (scan_supported(g)) h->geom = g;
     }
     if (const char *v = getenv("SYNCR_CDC_MFVAR")) {    // MFV_* bits of the MFMA scan
@@ -326,7 +329,7 @@ void syncr_cdc_close(syncr_cdc *h) {
     (void)hipStreamSynchronize(h->stream);
     drain_timing(h);
     DevBuf *bufs[] = {&h->fstart, &h->foff, &h->flen, &h->order, &h->cut_base, &h->cut_cap,
-                      &h->bmask, &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
+                      &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
                       &h->dense_cnt, &h->dense_bits, &h->super_off, &h->cand, &h->cuts,
                       &h->counts, &h->stage};
     for (DevBuf *b : bufs) b->release();
@@ -385,7 +388,6 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         CHECK_HIP(h->flen.ensure(std::max<size_t>(nfiles, 1) * 8));
         CHECK_HIP(h->order.ensure(std::max<size_t>(nfiles, 1) * 4));
         CHECK_HIP(h->counts.ensure(std::max<size_t>(nfiles, 1) * 8));
-        CHECK_HIP(h->bmask.ensure(std::max<size_t>(nfiles, 1) * 8));
         CHECK_HIP(h->tile_meta.ensure(std::max<size_t>(h->ntiles, 1) * 4));
         CHECK_HIP(h->slots.ensure(std::max<size_t>(h->ntiles, 1) * LISTCAP * sizeof(uint2)));
         CHECK_HIP(h->zeroed.ensure(zeroed_bytes(h)));

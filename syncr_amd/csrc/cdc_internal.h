@@ -16,7 +16,7 @@ constexpr int HALO = 64;                 // window warm-up bytes before the tile
 constexpr int LISTCAP = 64;              // candidate slots per tile
 constexpr uint32_t DENSE_BIT = 0x80000000u;
 constexpr uint64_t NONE = ~0ull;
-constexpr int DEFAULT_RUN = 80;
+constexpr int DEFAULT_RUN = 144;
 
 // MFMA scan (cdc_scan_mfma_kernel): a wave tile is 32 streams x NB blocks of
 // 32 bytes; W for a 32-position block is a Toeplitz product of the block and
@@ -100,7 +100,6 @@ struct Tables {
     uint64_t cand_cap;
     DevCut *cuts;                  // [sum cut_cap]
     uint64_t *counts;              // [nfiles]
-    uint64_t *bmask;               // [nfiles] exact G hits of each file's first 63 bytes
 };
 
 // launchers (cdc_kernels.hip)

@@ -657,32 +657,10 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
     }
 }
 
-// ---------------------------------------------------------------------------
 // File starts: the scan treats the batch as ONE byte stream, so its G is exact
-// for p >= f+63 inside a file starting at f.  The 63 head positions of every
-// file are recomputed here with a fresh window at f (bit k of bmask[i] = hit at
-// f+k); the resolve uses this mask at s = 0 and the candidates from f+63 on.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void cdc_boundary_kernel(const uint8_t *__restrict__ data,
-                                                           KParams P, Tables T) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= T.nfiles) return;
-    const uint64_t F = T.flen[i], g0 = T.foff[i];
-    const uint32_t n = (uint32_t)min<uint64_t>(F, 63ull);
-    uint32_t x[63];
-#pragma unroll
-    for (int k = 0; k < 63; ++k) x[k] = (uint32_t)k < n ? data[g0 + k] : 0u;
-    uint32_t S = 0, W = 0;
-    uint64_t m = 0;
-#pragma unroll
-    for (int k = 0; k < 63; ++k) {
-        S += x[k];
-        W += S;
-        if ((uint32_t)k < n && hit_exact(S, W, P.mask)) m |= 1ull << k;
-    }
-    T.bmask[i] = m;
-}
-
+// for p >= f+63 inside a file starting at f.  The 63 head positions of a file
+// are the resolve's head scan at s = 0 (a fresh window at f, exactly as after
+// any cut), so file starts need no kernel of their own.
 // ---------------------------------------------------------------------------
 // Dense tiles (more than LISTCAP candidates: low-entropy / adversarial data at
 // small chunk_bits): recompute G for the whole tile into a bitmap, count it.
@@ -703,7 +681,7 @@ __global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict
         auto byte = [&](int64_t q) -> uint32_t { return (q >= 0 && q < span) ? data[q] : 0u; };
         uint32_t word = 0, cnt = 0;
         int cur = 0;
-        // stream semantics like the scan (no resets: file heads come from the boundary masks)
+        // stream semantics like the scan (no resets: file heads are the resolve's head scan)
         roll_with_resets(byte, rs, per_lane, T.fstart, 0u, 0u, P.mask, [&](int64_t q) {
             if (q < span) {
                 const int r = (int)(q - rs);
@@ -721,32 +699,59 @@ __global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict
     }
 }
 
-// Exclusive prefix of the per-64-tile candidate counts (one block).
+// Exclusive prefix of the per-64-tile candidate counts (one block).  Each
+// pass covers 4096 words: thread t loads words 4t..4t+3 (one coalesced 16-byte
+// load), the 1024 partial sums are scanned by wave shuffles plus one LDS pass
+// over the 16 wave totals, and the running carry moves to the next pass.
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t u = __shfl_up(v, off);
+        if (lane >= off) v += u;
+    }
+    return v;
+}
+
 __global__ __launch_bounds__(1024) void cdc_prefix_kernel(Tables T) {
-    __shared__ uint64_t part[1024];
+    __shared__ uint64_t wsum[16];
     const uint32_t n = T.nwords, t = threadIdx.x;
-    const uint32_t per = (n + 1023) / 1024;
-    const uint32_t a = min(n, t * per), b = min(n, a + per);
-    uint64_t s = 0;
-    for (uint32_t i = a; i < b; ++i) s += T.super_cnt[i];
-    part[t] = s;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        const uint64_t v = t >= off ? part[t - off] : 0ull;
+    const int lane = t & 63, wv = t >> 6;
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < n; base += 4096) {
+        const uint32_t i0 = base + 4 * t;
+        uint32_t c[4];
+        if (i0 + 3 < n && (n & 3) == 0) {
+            const uint4 v = *(const uint4 *)(T.super_cnt + i0);
+            c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) c[k] = i0 + k < n ? T.super_cnt[i0 + k] : 0u;
+        }
+        const uint64_t mine = (uint64_t)c[0] + c[1] + c[2] + c[3];
+        const uint64_t incl = wave_incl_scan64(mine, lane);
+        if (lane == 63) wsum[wv] = incl;
         __syncthreads();
-        part[t] += v;
-        __syncthreads();
+        uint64_t before = carry, total = carry;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint64_t x = wsum[k];
+            before += k < wv ? x : 0ull;
+            total += x;
+        }
+        __syncthreads();                                  // wsum reused next pass
+        uint64_t run = before + incl - mine;              // exclusive
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (i0 + k < n) T.super_off[i0 + k] = run;
+            run += c[k];
+        }
+        carry = total;
     }
-    uint64_t run = part[t] - s;                         // exclusive
-    for (uint32_t i = a; i < b; ++i) {
-        T.super_off[i] = run;
-        run += T.super_cnt[i];
-    }
-    if (t == 1023) {
-        T.super_off[n] = part[1023];
-        T.ctr[CTR_CANDS_LO] = (uint32_t)part[1023];
-        T.ctr[CTR_CANDS_HI] = (uint32_t)(part[1023] >> 32);
-        if (part[1023] > T.cand_cap) T.ctr[CTR_FLAGS] |= FLAG_CAND_OVERFLOW;
+    if (t == 0) {
+        T.super_off[n] = carry;
+        T.ctr[CTR_CANDS_LO] = (uint32_t)carry;
+        T.ctr[CTR_CANDS_HI] = (uint32_t)(carry >> 32);
+        if (carry > T.cand_cap) T.ctr[CTR_FLAGS] |= FLAG_CAND_OVERFLOW;
     }
 }
 
@@ -858,12 +863,11 @@ __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restri
         j = lo;
     }
     uint64_t cv = j < ncand ? T.cand[j] : NONE;         // current candidate word
-    const uint64_t bm = T.bmask[i];                      // exact hits of the file's first 63 bytes
     uint64_t cnt = 0;
     // compute_file_chunks (file_operations.rs:737-784): R = bytes buffered.
     uint64_t R = min(min(F, MAX), CAP);                   // first read :738
     uint64_t s = 0;
-    int head = 0;            // 0: file start (boundary mask), 1: fix known, 2: unknown
+    int head = 2;            // 1: fix known, 2: unknown (head scan; also at the file start)
     uint32_t fix = 0;
     while (s < R) {                                       // n = R - s > 0  :747
         const uint64_t lim = R;                           // endofs = min(MAX, n) :749-752
@@ -873,10 +877,7 @@ __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restri
         uint64_t from = s + 63;                           // stream G applies from here
         {
             uint64_t hh = NONE;
-            if (head == 0) {
-                const uint64_t m = lim < 63 ? bm & ((1ull << lim) - 1) : bm;
-                if (m) hh = (uint64_t)__builtin_ctzll(m);
-            } else if (head == 1) {
+            if (head == 1) {
                 if (fix) hh = s - 1 + fix;
             } else {
                 const uint64_t h = head_scan(data, g0 + s, g0 + min(s + 63, lim), P.mask);
@@ -960,11 +961,10 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
         wb = T.super_off[w];                               // first candidate of the file's 64-tile group
     }
     uint64_t wv = wb + lane < ncand ? T.cand[wb + lane] : NONE;
-    const uint64_t bm = T.bmask[i];                      // exact hits of the file's first 63 bytes
     uint64_t cnt = 0;
     uint64_t R = min(min(F, MAX), CAP);                   // first read (file_operations.rs:738)
     uint64_t s = 0;
-    int head = 0;            // 0: file start (boundary mask), 1: fix known, 2: unknown
+    int head = 2;            // 1: fix known, 2: unknown (head scan; also at the file start)
     uint32_t fix = 0;
     while (s < R) {                                       // :747
         const uint64_t lim = R;                           // :749-752
@@ -974,10 +974,7 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
         const uint64_t from = s + 63;                     // stream G applies from here
         {
             uint64_t hh = NONE;
-            if (head == 0) {
-                const uint64_t m = lim < 63 ? bm & ((1ull << lim) - 1) : bm;
-                if (m) hh = (uint64_t)__builtin_ctzll(m);
-            } else if (head == 1) {
+            if (head == 1) {
                 if (fix) hh = s - 1 + fix;
             } else {                                      // wave head scan of [s, min(s+63, lim))
                 const uint32_t n = (uint32_t)min<uint64_t>(63ull, lim - s);
@@ -1217,8 +1214,6 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
         const uint32_t blocks = t.dense_cap < 2048u ? t.dense_cap : 2048u;
         hipLaunchKernelGGL(cdc_dense_kernel, dim3(blocks), dim3(64), 0, s, d, p, t);
     }
-    if (t.nfiles)
-        hipLaunchKernelGGL(cdc_boundary_kernel, dim3((t.nfiles + 255) / 256), dim3(256), 0, s, d, p, t);
     hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
     hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4), dim3(256), 0, s, t);
     {
