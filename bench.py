@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s chunked device-resident (bytes→cut offsets); bit-exact vs ref"
+METRIC_HASHED = "GiB/s chunked+BLAKE3-hashed device-resident (bytes→ChunkInfo); bit-exact vs ref"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 M = 1 << 20
 
@@ -113,10 +114,11 @@ def load_traffic(workload_name: str, span: int, run_bytes: int):
     return best
 
 
-def cpu_baseline(chunker, dbuf, offs, lens, cuts, sample_gib: float):
+def cpu_baseline(chunker, dbuf, offs, lens, cuts, sample_gib: float, hashed: bool = False):
     """Oracle (oracle/bup_oracle.c, the literal compute_file_chunks restatement)
     timed on this host on a bounded sample of the same bytes.  Also checks the
-    GPU cuts of the sampled files against it."""
+    GPU cuts of the sampled files against it.  hashed: the oracle also BLAKE3s
+    every chunk (oracle/blake3_oracle.c) and the GPU hashes are checked."""
     from oracle import oracle as O
     take, tot = [], 0
     for i in range(lens.size):
@@ -130,23 +132,47 @@ def cpu_baseline(chunker, dbuf, offs, lens, cuts, sample_gib: float):
     host = dbuf.download(hi - lo, offset=lo)
     s_offs = (offs[take] - np.uint64(lo)).astype(np.uint64)
     s_lens = lens[take]
+    def chunk_offsets(ref):
+        o, n = [], []
+        for j in range(take.size):
+            ends = ref[j].astype(np.uint64)
+            starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64)
+            o.append(starts + s_offs[j])
+            n.append(ends - starts)
+        return (np.concatenate(o) if o else np.zeros(0, np.uint64),
+                np.concatenate(n) if n else np.zeros(0, np.uint64))
+
+    def run(nthreads):
+        r = O.chunk_batch(host, s_offs, s_lens, nthreads=nthreads)
+        hs = None
+        if hashed:
+            co, cn = chunk_offsets(r)
+            hs = O.blake3_batch(host, co, cn, nthreads=nthreads)
+        return r, hs
+
     t = time.perf_counter()
-    ref = O.chunk_batch(host, s_offs, s_lens, nthreads=1)
+    ref, ref_h = run(1)
     dt1 = time.perf_counter() - t
     nthr = min(16, os.cpu_count() or 1)
     t = time.perf_counter()
-    O.chunk_batch(host, s_offs, s_lens, nthreads=nthr)
+    run(nthr)
     dtn = time.perf_counter() - t
     mism = 0
+    k = 0
     for j, i in enumerate(take.tolist()):
         c = cuts[i]
         e = (c["offset"].astype(np.uint64) + c["len"].astype(np.uint64)).tolist()
-        mism += e != ref[j].tolist()
+        bad = e != ref[j].tolist()
+        if hashed and not bad:
+            bad = not np.array_equal(c["hash"], ref_h[k:k + c.size])
+        k += c.size
+        mism += bad
     gib = tot / 2**30
     return {
         "value": round(gib / dt1, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
         "sample": f"first {take.size} files of rank 0's batch ({gib:.2f} GiB), production semantics, "
-                  f"oracle/bup_oracle.c literal compute_file_chunks loop (gcc -O3), chunking only",
+                  f"oracle/bup_oracle.c literal compute_file_chunks loop (gcc -O3), "
+                  + ("plus oracle/blake3_oracle.c per chunk (portable C, no SIMD)" if hashed else "chunking only"),
         "threads_value": round(gib / dtn, 4), "threads": nthr,
         "gpu_cuts_match_sample": mism == 0, "sample_files_mismatched": int(mism),
     }
@@ -161,6 +187,9 @@ def main(argv=None):
     ap.add_argument("--mode", default="production", choices=["production", "ideal"])
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hashed", action="store_true",
+                    help="also BLAKE3 every chunk on the GPU (SURVEY §8f next #1); reports the "
+                         "chunk+hash rate as its own metric, not the BASELINE metric")
     args = ap.parse_args(argv)
 
     d = Dist()
@@ -182,7 +211,7 @@ def main(argv=None):
     ch.plan(offs, lens, span)
 
     for _ in range(args.warmup):
-        ch.launch(dbuf.ptr)
+        ch.launch(dbuf.ptr, hashed=args.hashed)
     ch.synchronize()
 
     d.barrier()
@@ -190,7 +219,7 @@ def main(argv=None):
     ch.set_timing(True)                       # HIP events around each kernel, same stream
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ch.launch(dbuf.ptr)
+        ch.launch(dbuf.ptr, hashed=args.hashed)
     ch.synchronize()
     dt = time.perf_counter() - t0
     d.barrier()
@@ -202,7 +231,7 @@ def main(argv=None):
     step_s = dt_max / max(args.steps, 1)
     value = total_bytes / step_s / 2**30
 
-    cuts = ch.fetch()
+    cuts = ch.fetch(hashed=args.hashed)
     stats = ch.last_stats()
     engine_info = ch.info()
     ncuts = int(sum(c.size for c in cuts))
@@ -218,17 +247,18 @@ def main(argv=None):
         "kernel": engine_info["scan_kernel"], "kernel_ms": round(scan_ms, 4),
         "algorithmic_bytes_per_launch": span,
         "dense_ms": round(kms[1] / max(nl, 1), 4), "resolve_ms": round(kms[2] / max(nl, 1), 4),
+        "hash_ms": round(kms[3] / max(nl, 1), 4) if args.hashed else None,
         "traffic_source": (tr.get("source") if tr else None),
     }
     cpu = None
     if d.rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(ch, dbuf, offs, lens, cuts, args.cpu_sample_gib)
+        cpu = cpu_baseline(ch, dbuf, offs, lens, cuts, args.cpu_sample_gib, hashed=args.hashed)
     dbuf.free()
     ch.close()
 
     if d.rank == 0:
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+            "metric": METRIC_HASHED if args.hashed else METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: per-file xorshift64 corpus generated in HBM (SURVEY §8d seed rule)",

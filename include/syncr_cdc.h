@@ -8,8 +8,10 @@
  * inside the driver loop compute_file_chunks()     src/protocol/file_operations.rs:721-788
  * (and its dead duplicate get_file_chunks(), :190-248).  The entry points below
  * replace that loop: bytes in, chunk boundaries (offset, size) out, bit-exact.
- * The caller keeps hashing each returned chunk (util::hash_binary, src/util.rs:57-59)
- * and feeding DumpState::add_chunk (src/serve.rs:36-42) exactly as before.
+ * The *_hashed variants also return each chunk's BLAKE3 hash, computed on the GPU
+ * (util::hash_binary, src/util.rs:57-59, called per chunk at file_operations.rs:757),
+ * i.e. complete ChunkInfo records; the caller keeps feeding DumpState::add_chunk
+ * (src/serve.rs:36-42) exactly as before.
  *
  * Conventions: every function returns 0 on success or a negative errno-style
  * code (SYNCR_CDC_E*); no C++ exception crosses this boundary.  Inputs and
@@ -26,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SYNCR_CDC_ABI_VERSION 1
+#define SYNCR_CDC_ABI_VERSION 2
 
 /* error codes (negative errno values) */
 #define SYNCR_CDC_OK 0
@@ -55,6 +57,16 @@ typedef struct syncr_cut {
     uint32_t file;   /* file index in the batch     */
 } syncr_cut;
 
+/* One chunk with its hash: ChunkInfo{hash: [u8; 32], offset: u64, size: u32}
+ * (src/protocol/types.rs:24-29) plus the file index.  hash = blake3::hash of the
+ * chunk's bytes (util::hash_binary, src/util.rs:57-59). */
+typedef struct syncr_chunk_info {
+    uint64_t offset;  /* byte offset within its file */
+    uint32_t len;     /* chunk size                  */
+    uint32_t file;    /* file index in the batch     */
+    uint8_t hash[32]; /* BLAKE3-256 of the chunk     */
+} syncr_chunk_info;
+
 typedef struct syncr_cdc syncr_cdc;
 
 int32_t syncr_cdc_abi_version(void);
@@ -80,6 +92,15 @@ int32_t syncr_cdc_chunk_batch_host(syncr_cdc *h, const uint8_t *data, uint64_t s
                                    uint32_t nfiles, syncr_cut *out, uint64_t cap,
                                    uint64_t *per_file_count, uint64_t *n_out);
 
+/* As above, with each chunk's BLAKE3 hash (compute_file_chunks' ChunkInfo list,
+ * file_operations.rs:746-784 including the hash_binary call at :757). */
+int32_t syncr_cdc_chunk_host_hashed(syncr_cdc *h, const uint8_t *data, uint64_t len,
+                                    syncr_chunk_info *out, uint64_t cap, uint64_t *n_out);
+int32_t syncr_cdc_chunk_batch_host_hashed(syncr_cdc *h, const uint8_t *data, uint64_t span,
+                                          const uint64_t *file_off, const uint64_t *file_len,
+                                          uint32_t nfiles, syncr_chunk_info *out, uint64_t cap,
+                                          uint64_t *per_file_count, uint64_t *n_out);
+
 /* --- device-resident entry points (what the throughput metric times) ------- */
 /* plan: validate + upload the file table (host arrays) for bytes that will be
  * resident in device memory at [d_bytes, d_bytes+span).  Files must not overlap.
@@ -92,6 +113,12 @@ int32_t syncr_cdc_launch(syncr_cdc *h, const uint8_t *d_bytes, void *stream);
 /* fetch: wait for the last launch, copy cuts to the host (file by file). */
 int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap,
                         uint64_t *per_file_count, uint64_t *n_out);
+/* launch_hashed: launch, then BLAKE3 of every chunk on the same stream
+ * (asynchronous, allocation-free).  fetch_hashed: like fetch, with hashes;
+ * returns SYNCR_CDC_ESTATE unless the last launch was a launch_hashed. */
+int32_t syncr_cdc_launch_hashed(syncr_cdc *h, const uint8_t *d_bytes, void *stream);
+int32_t syncr_cdc_fetch_hashed(syncr_cdc *h, syncr_chunk_info *out, uint64_t cap,
+                               uint64_t *per_file_count, uint64_t *n_out);
 /* plan + launch + fetch */
 int32_t syncr_cdc_chunk_batch_device(syncr_cdc *h, const uint8_t *d_bytes, uint64_t span,
                                      const uint64_t *file_off, const uint64_t *file_len,
@@ -119,6 +146,8 @@ int32_t syncr_cdc_gen_corpus(syncr_cdc *h, uint8_t *d_bytes, const uint64_t *fil
  * [scan, dense, resolve] since the last reset and the number of launches. */
 int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable);
 int32_t syncr_cdc_kernel_times(syncr_cdc *h, double *ms3, uint64_t *launches);
+/* The same for up to 4 phases: [scan, dense+compaction, resolve, hash]. */
+int32_t syncr_cdc_kernel_times_ex(syncr_cdc *h, double *ms, uint32_t n, uint64_t *launches);
 /* Diagnostics of the last fetched launch: [candidates, dense_tiles, tiles, overflow]. */
 int32_t syncr_cdc_last_stats(syncr_cdc *h, uint64_t *stats4);
 /* Engine geometry: [run_bytes, tile_bytes, scan_grid, compute_units,

@@ -3,7 +3,8 @@
 //
 //   syncr::chunking::{CHUNK_BITS, MAX_CHUNK_SIZE_FACTOR, MAX_CHUNK_SIZE}
 //                                     src/chunking.rs:7,10,13
-//   syncr::ChunkInfo                  src/protocol/types.rs:24-29 (hash left to the caller)
+//   syncr::ChunkInfo                  src/protocol/types.rs:24-29 (hash = BLAKE3, util.rs:57-59,
+//                                     computed on the GPU by chunk_hashed())
 //   syncr::compute_file_chunks()      src/protocol/file_operations.rs:721-788
 //   syncr::chunk_data()               tests/chunking_test.rs:170-192
 //
@@ -12,6 +13,7 @@
 // failure) throw syncr::CdcError -- there is no silent CPU fallback.
 #pragma once
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <fstream>
@@ -33,7 +35,7 @@ constexpr uint64_t TOKIO_READ_CAP = 2ull * 1024 * 1024;               // tokio F
 }  // namespace chunking
 
 struct ChunkInfo {
-    std::array<uint8_t, 32> hash{};  // BLAKE3 of the chunk; filled by the caller (util.rs:57-59)
+    std::array<uint8_t, 32> hash{};  // BLAKE3 of the chunk (util::hash_binary, util.rs:57-59)
     uint64_t offset = 0;
     uint32_t size = 0;
 };
@@ -87,18 +89,38 @@ class Chunker {
     }
     std::vector<ChunkInfo> chunk(const std::vector<uint8_t> &v) { return chunk(v.data(), v.size()); }
 
+    // bytes -> complete ChunkInfo{hash, offset, size} (boundaries + BLAKE3 on the GPU)
+    std::vector<ChunkInfo> chunk_hashed(const uint8_t *data, uint64_t len) {
+        std::vector<syncr_chunk_info> cuts(len / 4096 + 64);
+        uint64_t n = 0;
+        int32_t rc = syncr_cdc_chunk_host_hashed(h_, data, len, cuts.data(), cuts.size(), &n);
+        if (rc == SYNCR_CDC_ERANGE) {
+            cuts.resize(n);
+            rc = syncr_cdc_chunk_host_hashed(h_, data, len, cuts.data(), cuts.size(), &n);
+        }
+        cdc_check(rc, "syncr_cdc_chunk_host_hashed");
+        std::vector<ChunkInfo> out(n);
+        for (uint64_t i = 0; i < n; i++) {
+            out[i].offset = cuts[i].offset;
+            out[i].size = cuts[i].len;
+            std::copy(cuts[i].hash, cuts[i].hash + 32, out[i].hash.begin());
+        }
+        return out;
+    }
+    std::vector<ChunkInfo> chunk_hashed(const std::vector<uint8_t> &v) { return chunk_hashed(v.data(), v.size()); }
+
   private:
     syncr_cdc *h_ = nullptr;
 };
 
-// compute_file_chunks (file_operations.rs:721-788) with the reference's error
-// behaviour: open/read failure -> empty list.
-inline std::vector<ChunkInfo> compute_file_chunks(const std::string &path, Chunker &c) {
+// compute_file_chunks (file_operations.rs:721-788, hashes as at :757) with the
+// reference's error behaviour: open/read failure -> empty list.
+inline std::vector<ChunkInfo> compute_file_chunks(const std::string &path, Chunker &c, bool hashed = true) {
     std::ifstream f(path, std::ios::binary);
     if (!f) return {};
     std::vector<uint8_t> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
     if (f.bad()) return {};
-    return c.chunk(buf);
+    return hashed ? c.chunk_hashed(buf) : c.chunk(buf);
 }
 
 // chunk_data (tests/chunking_test.rs:170-192): ideal in-memory semantics,

@@ -9,6 +9,8 @@ Reference semantics restated (paths relative to /root/reference):
   * ideal driver       tests/chunking_test.rs:170-192
   * parameters         src/chunking.rs:7-13
   * rollsum::Bup       rollsum 0.3 (Cargo.toml:24; crate not on disk)
+  * util::hash_binary  blake3::hash, blake3 1.8 (Cargo.toml:14; crate not on disk),
+                       src/util.rs:57-59, restated in oracle/blake3_oracle.c
 """
 from __future__ import annotations
 
@@ -42,7 +44,8 @@ def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(_LIB_PATH) or (
-            os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "bup_oracle.c"))
+            os.path.getmtime(_LIB_PATH) < max(os.path.getmtime(os.path.join(_HERE, f))
+                                              for f in ("bup_oracle.c", "blake3_oracle.c"))
         ):
             build()
         L = ctypes.CDLL(_LIB_PATH)
@@ -70,6 +73,10 @@ def lib():
                                       ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, _u64p, _u64p,
                                       _u64p, _u64p, ctypes.c_int]
         L.orc_chunk_batch.restype = ctypes.c_int
+        L.orc_blake3.argtypes = [_u8p, ctypes.c_uint64, _u8p]
+        L.orc_blake3.restype = None
+        L.orc_blake3_batch.argtypes = [_u8p, _u64p, _u64p, ctypes.c_uint64, _u8p, ctypes.c_int]
+        L.orc_blake3_batch.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -195,3 +202,32 @@ def chunk_batch(base, offs, lens, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE,
         else:
             out.append(ends[int(ob[i]): int(ob[i]) + c].copy())
     return out
+
+
+def blake3(data) -> bytes:
+    """blake3::hash(data) (util::hash_binary, src/util.rs:57-59)."""
+    a = np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8) if not isinstance(data, np.ndarray) \
+        else np.ascontiguousarray(data.reshape(-1).view(np.uint8))
+    out = np.zeros(32, np.uint8)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    lib().orc_blake3(_p8(buf), a.size, _p8(out))
+    return out.tobytes()
+
+
+def blake3_batch(base: np.ndarray, offs, lens, nthreads: int = 1) -> np.ndarray:
+    """[n, 32] uint8: blake3 of base[offs[i] : offs[i] + lens[i]] for every i."""
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    out = np.zeros((offs.size, 32), np.uint8)
+    buf = base if base.size else np.zeros(1, np.uint8)
+    rc = lib().orc_blake3_batch(_p8(buf), offs.ctypes.data_as(_u64p), lens.ctypes.data_as(_u64p),
+                                offs.size, out.ctypes.data_as(_u8p), nthreads)
+    if rc:
+        raise RuntimeError("orc_blake3_batch failed")
+    return out
+
+
+def hash_to_base64(h: bytes) -> str:
+    """util::hash_to_base64: base64 URL_SAFE with padding (src/util.rs:62-64)."""
+    import base64
+    return base64.urlsafe_b64encode(h).decode()

@@ -48,9 +48,11 @@ EXPORTED_SYMBOLS = (
     "syncr_cdc_memcpy_h2d", "syncr_cdc_memcpy_d2h", "syncr_cdc_synchronize", "syncr_cdc_stream",
     "syncr_cdc_gen_corpus", "syncr_cdc_set_timing", "syncr_cdc_kernel_times",
     "syncr_cdc_last_stats", "syncr_cdc_get_info",
+    "syncr_cdc_chunk_host_hashed", "syncr_cdc_chunk_batch_host_hashed", "syncr_cdc_launch_hashed",
+    "syncr_cdc_fetch_hashed", "syncr_cdc_kernel_times_ex",
 )
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 E_RANGE = -34
 
 
@@ -72,6 +74,9 @@ class Cut(ctypes.Structure):
 
 CUT_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("file", "<u4")])
 assert CUT_DTYPE.itemsize == ctypes.sizeof(Cut) == 16
+# syncr_chunk_info: ChunkInfo{hash, offset, size} + file (include/syncr_cdc.h)
+CHUNK_INFO_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("file", "<u4"), ("hash", "u1", (32,))])
+assert CHUNK_INFO_DTYPE.itemsize == 48
 
 _lib = None
 _vp, _u64, _u32, _i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32
@@ -113,6 +118,11 @@ def library():
             "syncr_cdc_kernel_times": ([_vp, ctypes.POINTER(ctypes.c_double), _pu64], _i32),
             "syncr_cdc_last_stats": ([_vp, _pu64], _i32),
             "syncr_cdc_get_info": ([_vp, _pu64], _i32),
+            "syncr_cdc_chunk_host_hashed": ([_vp, _vp, _u64, _vp, _u64, _pu64], _i32),
+            "syncr_cdc_chunk_batch_host_hashed": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u64, _vp, _pu64], _i32),
+            "syncr_cdc_launch_hashed": ([_vp, _vp, _vp], _i32),
+            "syncr_cdc_fetch_hashed": ([_vp, _vp, _u64, _vp, _pu64], _i32),
+            "syncr_cdc_kernel_times_ex": ([_vp, ctypes.POINTER(ctypes.c_double), _u32, _pu64], _i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -139,9 +149,9 @@ def device_count() -> int:
 class ChunkInfo:
     """ChunkInfo{hash, offset, size} (src/protocol/types.rs:24-29).
 
-    `hash` (BLAKE3, util::hash_binary, src/util.rs:57-59) is computed by the
-    caller per chunk, exactly as in compute_file_chunks (file_operations.rs:757);
-    it is None here until filled in."""
+    `hash` is BLAKE3 (util::hash_binary, src/util.rs:57-59) of the chunk's
+    bytes, as in compute_file_chunks (file_operations.rs:757); None when the
+    boundaries were requested without hashes."""
     offset: int
     size: int
     hash: Optional[bytes] = None
@@ -198,10 +208,17 @@ class Chunker:
         a = _u8(data)
         return self.batch_arrays(a, [0], [a.size])[0]
 
-    def chunk_bytes(self, data) -> list[ChunkInfo]:
-        return [ChunkInfo(int(o), int(n)) for o, n, _ in self.cut_array(data).tolist()]
+    def chunk_bytes(self, data, hashed: bool = False) -> list[ChunkInfo]:
+        """compute_file_chunks' ChunkInfo list for one file's bytes; with
+        hashed=True each chunk carries its BLAKE3 hash (computed on the GPU)."""
+        a = _u8(data)
+        cuts = self.batch_arrays(a, [0], [a.size], hashed=hashed)[0]
+        if hashed:
+            return [ChunkInfo(int(c["offset"]), int(c["len"]), bytes(c["hash"])) for c in cuts]
+        return [ChunkInfo(int(o), int(n)) for o, n, _ in cuts.tolist()]
 
-    def batch_arrays(self, buf, offsets: Sequence[int], lengths: Sequence[int]) -> list[np.ndarray]:
+    def batch_arrays(self, buf, offsets: Sequence[int], lengths: Sequence[int],
+                     hashed: bool = False) -> list[np.ndarray]:
         L = library()
         a = _u8(buf)
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -210,15 +227,15 @@ class Chunker:
         counts = np.zeros(max(nf, 1), np.uint64)
         n = ctypes.c_uint64(0)
         cap = max(16, a.size // (1 << max(0, self.params.chunk_bits - 2)) + 4 * nf + 16)
+        fn = L.syncr_cdc_chunk_batch_host_hashed if hashed else L.syncr_cdc_chunk_batch_host
         for _ in range(3):
-            out = np.zeros(cap, CUT_DTYPE)
-            rc = L.syncr_cdc_chunk_batch_host(self._h, a.ctypes.data if a.size else None, a.size,
-                                              offs.ctypes.data, lens.ctypes.data, nf,
-                                              out.ctypes.data, cap, counts.ctypes.data, ctypes.byref(n))
+            out = np.zeros(cap, CHUNK_INFO_DTYPE if hashed else CUT_DTYPE)
+            rc = fn(self._h, a.ctypes.data if a.size else None, a.size, offs.ctypes.data, lens.ctypes.data,
+                    nf, out.ctypes.data, cap, counts.ctypes.data, ctypes.byref(n))
             if rc == E_RANGE:
                 cap = int(n.value)
                 continue
-            _check(rc, "syncr_cdc_chunk_batch_host")
+            _check(rc, "syncr_cdc_chunk_batch_host" + ("_hashed" if hashed else ""))
             break
         return _split(out[: int(n.value)], counts[:nf])
 
@@ -230,30 +247,34 @@ class Chunker:
                "syncr_cdc_plan")
         self._nfiles = offs.size
 
-    def launch(self, d_bytes: int, stream: int = 0) -> None:
-        _check(library().syncr_cdc_launch(self._h, d_bytes, stream or None), "syncr_cdc_launch")
+    def launch(self, d_bytes: int, stream: int = 0, hashed: bool = False) -> None:
+        """Asynchronous scan + resolve (+ BLAKE3 of every chunk when hashed)."""
+        fn = library().syncr_cdc_launch_hashed if hashed else library().syncr_cdc_launch
+        _check(fn(self._h, d_bytes, stream or None), "syncr_cdc_launch" + ("_hashed" if hashed else ""))
 
-    def fetch(self) -> list[np.ndarray]:
+    def fetch(self, hashed: bool = False) -> list[np.ndarray]:
+        """Per-file structured arrays (offset, len, file[, hash])."""
         L = library()
+        fn = L.syncr_cdc_fetch_hashed if hashed else L.syncr_cdc_fetch
         nf = self._nfiles
         counts = np.zeros(max(nf, 1), np.uint64)
         n = ctypes.c_uint64(0)
-        rc = L.syncr_cdc_fetch(self._h, None, 0, counts.ctypes.data, ctypes.byref(n))
+        rc = fn(self._h, None, 0, counts.ctypes.data, ctypes.byref(n))
         if rc not in (0, E_RANGE):
             _check(rc, "syncr_cdc_fetch")
-        out = np.zeros(max(int(n.value), 1), CUT_DTYPE)
-        _check(L.syncr_cdc_fetch(self._h, out.ctypes.data, out.size, counts.ctypes.data, ctypes.byref(n)),
-               "syncr_cdc_fetch")
+        out = np.zeros(max(int(n.value), 1), CHUNK_INFO_DTYPE if hashed else CUT_DTYPE)
+        _check(fn(self._h, out.ctypes.data, out.size, counts.ctypes.data, ctypes.byref(n)), "syncr_cdc_fetch")
         return _split(out[: int(n.value)], counts[:nf])
 
     def set_timing(self, on: bool) -> None:
         _check(library().syncr_cdc_set_timing(self._h, 1 if on else 0), "syncr_cdc_set_timing")
 
     def kernel_times(self) -> tuple[list[float], int]:
-        ms = (ctypes.c_double * 3)()
+        """Summed ms of [scan, dense+compaction, resolve, hash] since set_timing(True)."""
+        ms = (ctypes.c_double * 4)()
         n = ctypes.c_uint64(0)
-        _check(library().syncr_cdc_kernel_times(self._h, ms, ctypes.byref(n)), "syncr_cdc_kernel_times")
-        return [ms[0], ms[1], ms[2]], int(n.value)
+        _check(library().syncr_cdc_kernel_times_ex(self._h, ms, 4, ctypes.byref(n)), "syncr_cdc_kernel_times_ex")
+        return [ms[0], ms[1], ms[2], ms[3]], int(n.value)
 
     def last_stats(self) -> dict:
         st = (ctypes.c_uint64 * 4)()
@@ -336,17 +357,18 @@ def _default_chunker() -> Chunker:
     return _default
 
 
-def compute_file_chunks(path, chunker: Optional[Chunker] = None) -> list[ChunkInfo]:
+def compute_file_chunks(path, chunker: Optional[Chunker] = None, hashed: bool = True) -> list[ChunkInfo]:
     """compute_file_chunks (src/protocol/file_operations.rs:721-788): chunk one
-    file with production semantics.  Like the reference, an unreadable file is
-    logged and yields an empty list (:727-744); GPU errors raise."""
+    file with production semantics and hash every chunk (BLAKE3, :757), both on
+    the GPU.  Like the reference, an unreadable file is logged and yields an
+    empty list (:727-744); GPU errors raise."""
     try:
         with open(path, "rb") as f:
             data = f.read()
     except OSError as e:
         log.warning("Cannot open file %s: %s", path, e)
         return []
-    return (chunker or _default_chunker()).chunk_bytes(data)
+    return (chunker or _default_chunker()).chunk_bytes(data, hashed=hashed)
 
 
 def chunk_data(data, chunk_bits: int = 13, max_chunk: Optional[int] = None,

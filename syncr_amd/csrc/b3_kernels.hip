@@ -1,0 +1,438 @@
+// b3_kernels.hip -- gfx950 BLAKE3 of every chunk of a launch.
+//
+// Replaces the per-chunk hash of compute_file_chunks:
+//     let hash_binary = util::hash_binary(&buf[..count]);   src/protocol/file_operations.rs:757
+//     util::hash_binary(buf) = *blake3::hash(buf).as_bytes()  src/util.rs:57-59
+// so a launch yields complete ChunkInfo{hash, offset, size} (src/protocol/types.rs:24-29).
+//
+// BLAKE3 splits a chunk of `len` bytes into 1 KiB leaves (16 blocks of 64 B,
+// compressed in sequence) whose chaining values (CVs) are merged in a
+// left-balanced binary tree of PARENT compressions; the last compression of
+// the root gets the ROOT flag.  Leaves are independent; a lane TASK is
+// LPL = B3_LANE_LEAVES consecutive leaves (contiguous bytes):
+//   b3_items_kernel  one wave per file: a chunk of T <= 64 tasks goes to packed
+//                    class c = ceil(log2 T) (64 >> c chunks share a wave, each
+//                    in an aligned run of 2^c lanes); a bigger chunk becomes
+//                    ceil(T / 64) group items plus a tree entry;
+//   b3_leaf_kernel   persistent waves pull wave items (group items first, then
+//                    packed classes 6..0): each lane compresses its task's
+//                    leaves, folds them into one subtree CV, then the lanes of
+//                    each chunk merge by shuffles -> the hash of a packed chunk,
+//                    or one CV per group item;
+//   b3_tree_kernel   one wave per multi-item chunk merges its group CVs.
+// Any aligned power-of-two run of leaves (or the run's tail) is a subtree of
+// the left-balanced tree, so these partial merges are the tree's own nodes.
+//
+// Compute bound: 7 rounds x 8 G x 12 integer ops per 64-byte block
+// (~10.5 VALU ops per byte); the 1 byte/byte HBM read is not the limit.
+#include "cdc_internal.h"
+
+namespace cdc {
+
+namespace {
+
+constexpr uint32_t B3_START = 1u, B3_END = 2u, B3_PARENT = 4u, B3_ROOT = 8u;
+constexpr uint32_t IV0 = 0x6A09E667u, IV1 = 0xBB67AE85u, IV2 = 0x3C6EF372u, IV3 = 0xA54FF53Au,
+                   IV4 = 0x510E527Fu, IV5 = 0x9B05688Cu, IV6 = 0x1F83D9ABu, IV7 = 0x5BE0CD19u;
+
+// message word schedule: SCHED[r][k] = index of the original word used at
+// position k of round r (the spec permutes the message between rounds)
+struct Sched {
+    uint8_t s[7][16];
+};
+constexpr uint8_t PERM[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+constexpr Sched make_sched() {
+    Sched t{};
+    for (int k = 0; k < 16; ++k) t.s[0][k] = (uint8_t)k;
+    for (int r = 1; r < 7; ++r)
+        for (int k = 0; k < 16; ++k) t.s[r][k] = t.s[r - 1][PERM[k]];
+    return t;
+}
+constexpr Sched SCHED = make_sched();
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_rotateright32(x, n); }
+
+#define B3_G(a, b, c, d, mx, my)      \
+    do {                              \
+        v[a] = v[a] + v[b] + (mx);    \
+        v[d] = rotr(v[d] ^ v[a], 16); \
+        v[c] = v[c] + v[d];           \
+        v[b] = rotr(v[b] ^ v[c], 12); \
+        v[a] = v[a] + v[b] + (my);    \
+        v[d] = rotr(v[d] ^ v[a], 8);  \
+        v[c] = v[c] + v[d];           \
+        v[b] = rotr(v[b] ^ v[c], 7);  \
+    } while (0)
+
+// cv <- first half of compress(cv, m, counter, blen, flags) (the chaining value
+// / the 32-byte hash when flags has ROOT)
+__device__ __forceinline__ void compress(uint32_t cv[8], const uint32_t m[16], uint32_t counter,
+                                         uint32_t blen, uint32_t flags) {
+    uint32_t v[16] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7],
+                      IV0,   IV1,   IV2,   IV3,   counter, 0u, blen, flags};
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+        const uint8_t *s = SCHED.s[r];
+        B3_G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+        B3_G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+        B3_G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+        B3_G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+        B3_G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+        B3_G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+        B3_G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+        B3_G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cv[i] = v[i] ^ v[i + 8];
+}
+#undef B3_G
+
+__device__ __forceinline__ void set_iv(uint32_t cv[8]) {
+    cv[0] = IV0; cv[1] = IV1; cv[2] = IV2; cv[3] = IV3;
+    cv[4] = IV4; cv[5] = IV5; cv[6] = IV6; cv[7] = IV7;
+}
+
+// x <- parent(x, r): a PARENT node over two child CVs (counter 0, 64 bytes)
+__device__ __forceinline__ void parent(uint32_t x[8], const uint32_t r[8], uint32_t extra) {
+    uint32_t m[16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { m[k] = x[k]; m[8 + k] = r[k]; }
+    set_iv(x);
+    compress(x, m, 0u, 64u, B3_PARENT | extra);
+}
+
+// Merge the CVs held by lanes 0..m-1 (level pairing, the last node of an odd
+// level is promoted) into lane 0.  `root`: this is the whole tree, so the
+// final merge gets ROOT.  m, root are wave-uniform.
+__device__ __forceinline__ void wave_merge(uint32_t x[8], uint32_t m, bool root, int lane) {
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        if (m > d) {                               // wave-uniform
+            uint32_t r[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r[k] = (uint32_t)__shfl_down((int)x[k], d);
+            const bool act = ((uint32_t)lane & (2 * d - 1)) == 0 && (uint32_t)lane + d < m;
+            if (act) parent(x, r, (root && m <= 2 * d) ? B3_ROOT : 0u);
+        }
+    }
+}
+
+// The 16 message words of the 64 bytes at batch offset p, bytes at or past
+// `valid` (< 64 only on a chunk's last block) read as zero.  p has any
+// alignment: gfx950 global loads are unaligned-capable (hipcc itself emits
+// global_load_dwordx4 for a byte-aligned 16-byte memcpy).
+template <bool NT>
+__device__ __forceinline__ void load_block(const uint8_t *__restrict__ data, uint64_t span, uint64_t p,
+                                           uint32_t valid, uint32_t m[16]) {
+    if (p + 64 <= span) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v4u v;
+            if constexpr (NT) {
+                v4u t;
+                __builtin_memcpy(&t, data + p + 16 * i, 16);
+                v = __builtin_nontemporal_load(&t);
+            } else {
+                __builtin_memcpy(&v, data + p + 16 * i, 16);
+            }
+            m[4 * i] = v.x; m[4 * i + 1] = v.y; m[4 * i + 2] = v.z; m[4 * i + 3] = v.w;
+        }
+    } else {                                   // the batch's last bytes: guarded byte loads
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            uint32_t w = 0;
+            for (int b = 0; b < 4; ++b) {
+                const uint64_t a = p + 4 * k + b;
+                if (a < span && (uint32_t)(4 * k + b) < valid) w |= (uint32_t)data[a] << (8 * b);
+            }
+            m[k] = w;
+        }
+    }
+    if (valid < 64) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int c = (int)valid - 4 * k;
+            const uint32_t keep = c >= 4 ? 0xffffffffu : (c <= 0 ? 0u : (1u << (8 * c)) - 1u);
+            m[k] &= keep;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)v, off);
+        if (lane >= off) v += u;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t bcast64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t chunk_leaves(uint32_t len) { return len ? (len + 1023u) >> 10 : 1u; }
+__device__ __forceinline__ uint32_t chunk_tasks(uint32_t len) {
+    return (chunk_leaves(len) + B3_LANE_LEAVES - 1) / B3_LANE_LEAVES;
+}
+__device__ __forceinline__ uint32_t ceil_log2(uint32_t t) { return t <= 1 ? 0u : 32u - __builtin_clz(t - 1); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// One wave per file, lanes over its cuts: packed chunks are appended to their
+// class list; big chunks get group items (slot << 24 | group) and a tree
+// entry {slot, first item}.  A file whose cuts overflowed its output slots is
+// skipped (the host re-launches).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (i >= T.nfiles) return;
+    const uint64_t n = T.counts[i];
+    if (n > T.cut_cap[i]) return;
+    const uint64_t cb = T.cut_base[i];
+    for (uint64_t k0 = 0; k0 < n; k0 += 64) {
+        const uint64_t k = k0 + (uint64_t)lane;
+        const uint64_t slot = cb + k;
+        uint32_t ng = 0;
+        if (k < n) {
+            const uint32_t t = chunk_tasks(T.cuts[slot].len);
+            if (t <= 64) {
+                const uint32_t c = ceil_log2(t);
+                const uint64_t idx = atomicAdd((unsigned long long *)&H.ctr[B3C_PK0 + c], 1ull);
+                if (idx < H.packed_cap) H.packed[c * H.packed_cap + idx] = slot;
+            } else {
+                ng = (t + 63) / 64;
+            }
+        }
+        if (!__ballot(ng != 0)) continue;
+        const uint32_t incl = wave_incl_scan_u32(ng, lane);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        uint64_t base = 0;
+        if (lane == 0) base = atomicAdd((unsigned long long *)&H.ctr[B3C_ITEMS], (unsigned long long)tot);
+        base = bcast64(base);
+        const uint64_t first = base + (incl - ng);
+        if (base + tot <= H.items_cap) {
+            for (uint32_t g = 0; g < ng; ++g) H.items[first + g] = (slot << 24) | g;
+        } else if (lane == 0) {
+            atomicOr((unsigned long long *)&H.ctr[B3C_FLAGS], 1ull);
+        }
+        const unsigned long long multi = __ballot(ng != 0);
+        uint64_t tb = 0;
+        if (lane == 0) tb = atomicAdd((unsigned long long *)&H.ctr[B3C_TREES], (unsigned long long)__popcll(multi));
+        tb = bcast64(tb);
+        if (ng) {
+            const uint64_t idx = tb + (uint64_t)__popcll(multi & ((1ull << lane) - 1ull));
+            if (idx < H.trees_cap) H.trees[idx] = make_ulonglong2(slot, first);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent waves pull wave items: the group items of big chunks first, then
+// the packed classes 6..0.  Per lane: a chunk slot, its task k (leaves
+// LPL*k .. LPL*k+LPL-1) and the merge geometry of that chunk within the wave.
+// ---------------------------------------------------------------------------
+template <bool NT, int ABLATE>
+__global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict__ data, Tables T,
+                                                      HashTables H) {
+    constexpr uint32_t LPL = B3_LANE_LEAVES;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nbig = min(H.ctr[B3C_ITEMS], H.items_cap);
+    uint64_t npk[B3_CLASSES], total = nbig;
+#pragma unroll
+    for (int c = 0; c < B3_CLASSES; ++c) {
+        npk[c] = min(H.ctr[B3C_PK0 + c], H.packed_cap);
+        total += (npk[c] + (64u >> c) - 1) >> (6 - c);          // waves of class c
+    }
+    for (;;) {
+        uint64_t w = 0;
+        if (lane == 0) w = atomicAdd((unsigned long long *)&H.ctr[B3C_NEXT], 1ull);
+        w = bcast64(w);
+        if (w >= total) break;
+        // per-lane geometry
+        bool valid;
+        uint64_t slot = 0;
+        uint32_t k;              // task index within the chunk
+        uint32_t km, mm;         // merge index / node count of this lane's chunk in this wave
+        uint32_t dmax;           // merge levels: lanes per chunk in this wave (uniform)
+        bool root;               // this wave finishes the chunk's tree
+        uint64_t out_item = 0;
+        if (w < nbig) {                                          // group item of a big chunk
+            const uint64_t code = H.items[w];
+            slot = code >> 24;
+            const uint32_t g = (uint32_t)code & 0xffffffu;
+            k = g * 64 + (uint32_t)lane;
+            km = (uint32_t)lane;
+            const uint32_t t = chunk_tasks(T.cuts[slot].len);
+            mm = min(64u, t - g * 64);
+            valid = true;
+            dmax = 64;
+            root = false;                                        // t > 64: b3_tree_kernel finishes
+            out_item = w;
+        } else {                                                 // packed chunks
+            uint64_t r = w - nbig;
+            int c = B3_CLASSES - 1;
+            for (; c > 0; --c) {                                 // uniform
+                const uint64_t wc = (npk[c] + (64u >> c) - 1) >> (6 - c);
+                if (r < wc) break;
+                r -= wc;
+            }
+            const uint64_t idx = r * (64u >> c) + ((uint32_t)lane >> c);
+            k = (uint32_t)lane & ((1u << c) - 1u);
+            km = k;
+            valid = idx < npk[c];
+            if (valid) slot = H.packed[c * H.packed_cap + idx];
+            mm = 0;
+            dmax = 1u << c;
+            root = true;
+        }
+        uint32_t len = 0;
+        uint64_t cstart = 0;
+        if (valid) {
+            const DevCut cu = T.cuts[slot];
+            len = cu.len;
+            cstart = T.foff[cu.file] + cu.offset;                // batch offset of the chunk
+            if (w >= nbig) mm = chunk_tasks(len);
+        }
+        const uint32_t nleaves = chunk_leaves(len);
+        const uint32_t j0 = k * LPL;
+        const bool act = valid && j0 < nleaves;
+        const uint64_t lane_off = (uint64_t)j0 << 10;            // chunk-relative byte offset
+        const uint32_t nbytes = act ? (uint32_t)min<uint64_t>(1024ull * LPL, len - lane_off) : 0u;
+        const uint32_t nblk = act ? (nbytes ? (nbytes + 63) >> 6 : 1u) : 0u;
+        const uint32_t nl = (nblk + 15) >> 4;                    // leaves of this task
+        uint32_t lc[LPL][8];                                     // leaf CVs
+#pragma unroll
+        for (uint32_t jj = 0; jj < LPL; ++jj) {
+            if (jj >= nl) continue;
+            uint32_t cv[8];
+            set_iv(cv);
+            const uint32_t tb = jj * 16;
+            const uint32_t lb = min(16u, nblk - tb);               // blocks of this leaf
+            for (uint32_t b = 0; b < lb; ++b) {
+                const uint32_t off = (tb + b) * 64;
+                const uint32_t vb = nbytes > off ? min(64u, nbytes - off) : 0u;
+                uint32_t m[16];
+                if constexpr (ABLATE == 2) {           // timing only: no loads
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) m[q] = (uint32_t)lane * 0x9E3779B9u + q + off;
+                } else {
+                    load_block<NT>(data, T.span, cstart + lane_off + off, vb, m);
+                }
+                uint32_t fl = (b == 0 ? B3_START : 0u) | (b + 1 == lb ? B3_END : 0u);
+                if (b + 1 == lb && nleaves == 1) fl |= B3_ROOT;
+                if constexpr (ABLATE == 1) {           // timing only: loads, no compression
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) cv[q] ^= m[q] + m[q + 8] + fl;
+                } else {
+                    compress(cv, m, j0 + jj, vb, fl);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) lc[jj][q] = cv[q];
+        }
+        // fold the task's leaves (left-balanced level pairing); ROOT when the
+        // task is the whole chunk
+        const bool task_root = root && mm == 1;
+#pragma unroll
+        for (uint32_t d = 1; d < LPL; d <<= 1)
+#pragma unroll
+            for (uint32_t i = 0; i + d < LPL; i += 2 * d)
+                if (i + d < nl) parent(lc[i], lc[i + d], (task_root && nl <= 2 * d) ? B3_ROOT : 0u);
+        uint32_t x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = lc[0][q];
+        // merge the tasks of each chunk (runs of 2^c lanes, or the 64 lanes of a group)
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            if (d < dmax) {                                      // uniform
+                uint32_t r[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) r[q] = (uint32_t)__shfl_down((int)x[q], d);
+                if (act && (km & (2 * d - 1)) == 0 && km + d < mm)
+                    parent(x, r, (root && mm <= 2 * d) ? B3_ROOT : 0u);
+            }
+        }
+        if (act && km == 0) {
+            uint32_t *dst = root ? H.hashes + slot * 8 : H.gcv + out_item * 8;
+            *(uint4 *)dst = make_uint4(x[0], x[1], x[2], x[3]);
+            *(uint4 *)(dst + 4) = make_uint4(x[4], x[5], x[6], x[7]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// One wave per multi-item chunk: merge its item CVs (batches of 64 aligned
+// nodes are complete subtrees; results are written back in place).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void b3_tree_kernel(Tables T, HashTables H) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t ntrees = min(H.ctr[B3C_TREES], H.trees_cap);
+    for (uint64_t w = blockIdx.x * 4ull + (threadIdx.x >> 6); w < ntrees; w += gridDim.x * 4ull) {
+        const ulonglong2 e = H.trees[w];
+        const uint64_t slot = e.x;
+        uint32_t *nodes = H.gcv + e.y * 8;
+        uint32_t n = (chunk_tasks(T.cuts[slot].len) + 63) / 64;
+        while (n > 1) {
+            const uint32_t nb = (n + 63) / 64;
+            for (uint32_t b = 0; b < nb; ++b) {
+                const uint32_t k = b * 64 + (uint32_t)lane;
+                uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (k < n) {
+                    const uint4 a = *(const uint4 *)(nodes + k * 8);
+                    const uint4 c = *(const uint4 *)(nodes + k * 8 + 4);
+                    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+                    x[4] = c.x; x[5] = c.y; x[6] = c.z; x[7] = c.w;
+                }
+                wave_merge(x, min(64u, n - b * 64), n <= 64, lane);
+                __threadfence();                 // reads of this batch before the in-place write
+                if (lane == 0) {
+                    uint32_t *dst = n <= 64 ? H.hashes + slot * 8 : nodes + b * 8;
+                    *(uint4 *)dst = make_uint4(x[0], x[1], x[2], x[3]);
+                    *(uint4 *)(dst + 4) = make_uint4(x[4], x[5], x[6], x[7]);
+                }
+            }
+            __threadfence();                     // this level's nodes visible to every lane
+            n = nb;
+        }
+    }
+}
+
+template <bool NT, int AB>
+static void launch_leaf(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+        cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)&b3_leaf_kernel<NT, AB>, 256, 0) !=
+            hipSuccess ||
+        per <= 0)
+        per = 1;
+    hipLaunchKernelGGL((b3_leaf_kernel<NT, AB>), dim3((uint32_t)(cus * per)), dim3(256), 0, s, d, t, ht);
+}
+
+hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(ht.ctr, 0, B3C_WORDS * sizeof(uint64_t), s);
+    if (e != hipSuccess) return e;
+    if (!t.nfiles) return hipSuccess;
+    hipLaunchKernelGGL(b3_items_kernel, dim3((t.nfiles + 3) / 4), dim3(256), 0, s, t, ht);
+    switch (ht.ablate * 2 + (ht.nt ? 1 : 0)) {
+        case 0: launch_leaf<false, 0>(device, d, t, ht, s); break;
+        case 1: launch_leaf<true, 0>(device, d, t, ht, s); break;
+        case 2: launch_leaf<false, 1>(device, d, t, ht, s); break;
+        case 3: launch_leaf<true, 1>(device, d, t, ht, s); break;
+        case 4: case 5: launch_leaf<true, 2>(device, d, t, ht, s); break;
+        default: return hipErrorInvalidValue;
+    }
+    const uint64_t want = (ht.trees_cap + 3) / 4;
+    const uint32_t blocks = (uint32_t)(want < 4096 ? (want ? want : 1) : 4096);
+    hipLaunchKernelGGL(b3_tree_kernel, dim3(blocks), dim3(256), 0, s, t, ht);
+    return hipGetLastError();
+}
+
+}  // namespace cdc

@@ -39,8 +39,11 @@ struct DevBuf {
     template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+constexpr int NPHASE = 4;            // scan, dense+compaction, resolve, hash
+
 struct PendingTiming {
-    hipEvent_t ev[4];
+    hipEvent_t ev[NPHASE + 1];
+    int nev;
 };
 
 }  // namespace
@@ -67,6 +70,11 @@ struct syncr_cdc {
     std::vector<uint32_t> h_cut_cap;
     DevBuf fstart, foff, flen, order, cut_base, cut_cap, tile_meta, slots, zeroed,
         dense_list, dense_cnt, dense_bits, super_off, cand, cuts, counts;
+    // BLAKE3 of every chunk (launch_hashed)
+    bool hash_on = false;
+    uint32_t b3_ablate = 0, b3_nt = 0;
+    uint64_t items_cap = 0, trees_cap = 0;
+    DevBuf hctr, items, trees, gcv, hashes, packed;
 
     // launch
     bool launched = false;
@@ -80,7 +88,7 @@ struct syncr_cdc {
     // timing
     bool timing = false;
     std::vector<PendingTiming> pending;
-    double ms[3] = {0, 0, 0};
+    double ms[NPHASE] = {0, 0, 0, 0};
     uint64_t timed_launches = 0;
 };
 
@@ -170,6 +178,19 @@ int32_t upload_cut_tables(syncr_cdc *h) {
         acc += h->h_cut_cap[i];
     }
     h->total_cut_cap = acc;
+    // BLAKE3 items: a chunk of len bytes is ceil(leaves / B3_GROUP_LEAVES) items,
+    // so a file needs at most ceil(F / group bytes) + (its cuts) of them
+    const uint64_t gbytes = 1024ull * B3_GROUP_LEAVES;
+    uint64_t icap = 0;
+    for (uint32_t i = 0; i < h->nfiles; i++) icap += (h->h_flen[i] + gbytes - 1) / gbytes + h->h_cut_cap[i];
+    h->items_cap = std::max<uint64_t>(icap, 1);
+    h->trees_cap = std::max<uint64_t>(acc, 1);
+    CHECK_HIP(h->hctr.ensure(B3C_WORDS * 8));
+    CHECK_HIP(h->items.ensure(h->items_cap * 8));
+    CHECK_HIP(h->trees.ensure(h->trees_cap * 16));
+    CHECK_HIP(h->gcv.ensure(h->items_cap * 32));
+    CHECK_HIP(h->hashes.ensure(std::max<uint64_t>(acc, 1) * 32));
+    CHECK_HIP(h->packed.ensure((size_t)B3_CLASSES * std::max<uint64_t>(acc, 1) * 8));
     CHECK_HIP(h->cut_base.ensure(std::max<size_t>(h->nfiles, 1) * 8));
     CHECK_HIP(h->cut_cap.ensure(std::max<size_t>(h->nfiles, 1) * 4));
     CHECK_HIP(h->cuts.ensure(std::max<uint64_t>(acc, 1) * sizeof(DevCut)));
@@ -178,6 +199,22 @@ int32_t upload_cut_tables(syncr_cdc *h) {
         CHECK_HIP(hipMemcpy(h->cut_cap.p, h->h_cut_cap.data(), h->nfiles * 4ull, hipMemcpyHostToDevice));
     }
     return SYNCR_CDC_OK;
+}
+
+HashTables make_hash_tables(syncr_cdc *h) {
+    HashTables t{};
+    t.ctr = h->hctr.as<uint64_t>();
+    t.items = h->items.as<uint64_t>();
+    t.items_cap = h->items_cap;
+    t.trees = h->trees.as<ulonglong2>();
+    t.trees_cap = h->trees_cap;
+    t.gcv = h->gcv.as<uint32_t>();
+    t.hashes = h->hashes.as<uint32_t>();
+    t.packed = h->packed.as<uint64_t>();
+    t.packed_cap = std::max<uint64_t>(h->total_cut_cap, 1);
+    t.ablate = h->b3_ablate;
+    t.nt = h->b3_nt;
+    return t;
 }
 
 int32_t ensure_dense(syncr_cdc *h, uint32_t cap) {
@@ -200,12 +237,12 @@ size_t zeroed_bytes(const syncr_cdc *h) {
 
 void drain_timing(syncr_cdc *h) {
     for (auto &pt : h->pending) {
-        (void)hipEventSynchronize(pt.ev[3]);
-        for (int k = 0; k < 3; k++) {
+        (void)hipEventSynchronize(pt.ev[pt.nev - 1]);
+        for (int k = 0; k + 1 < pt.nev; k++) {
             float f = 0.f;
             if (hipEventElapsedTime(&f, pt.ev[k], pt.ev[k + 1]) == hipSuccess) h->ms[k] += f;
         }
-        for (int k = 0; k < 4; k++) (void)hipEventDestroy(pt.ev[k]);
+        for (int k = 0; k < pt.nev; k++) (void)hipEventDestroy(pt.ev[k]);
         h->timed_launches++;
     }
     h->pending.clear();
@@ -215,9 +252,10 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     KParams kp = h->kp;
     Tables t = make_tables(h);
     PendingTiming pt{};
+    pt.nev = h->hash_on ? 5 : 4;
     if (h->timing) {
         if (h->pending.size() >= 256) drain_timing(h);
-        for (int k = 0; k < 4; k++) CHECK_HIP(hipEventCreate(&pt.ev[k]));
+        for (int k = 0; k < pt.nev; k++) CHECK_HIP(hipEventCreate(&pt.ev[k]));
     }
     CHECK_HIP(hipMemsetAsync(h->zeroed.p, 0, zeroed_bytes(h), s));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[0], s));
@@ -226,10 +264,12 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     CHECK_HIP(launch_post(d_bytes, kp, t, s, nullptr));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[2], s));
     CHECK_HIP(launch_resolve(d_bytes, kp, t, s));
-    if (h->timing) {
-        CHECK_HIP(hipEventRecord(pt.ev[3], s));
-        h->pending.push_back(pt);
+    if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[3], s));
+    if (h->hash_on) {
+        CHECK_HIP(launch_hash(h->device, d_bytes, t, make_hash_tables(h), s));
+        if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[4], s));
     }
+    if (h->timing) h->pending.push_back(pt);
     h->launched = true;
     h->last_bytes = d_bytes;
     h->last_stream = s;
@@ -291,6 +331,8 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_CDC_ABLATE")) h->kp.ablate = (uint32_t)atoi(a);  // timing-only
     if (const char *nt = getenv("SYNCR_CDC_NT")) h->kp.nt = (uint32_t)atoi(nt);
     if (const char *rs = getenv("SYNCR_CDC_RESOLVE")) h->kp.resolve_lane = strcmp(rs, "lane") == 0;
+    if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
+    if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
     // scan variant (timing / A-B only; every variant is exact)
     if (const char *k = getenv("SYNCR_CDC_SCAN")) {
         if (strcmp(k, "valu") == 0) h->geom = ScanGeom{SCAN_VALU, DEFAULT_RUN, 0};
@@ -331,7 +373,8 @@ void syncr_cdc_close(syncr_cdc *h) {
     DevBuf *bufs[] = {&h->fstart, &h->foff, &h->flen, &h->order, &h->cut_base, &h->cut_cap,
                       &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
                       &h->dense_cnt, &h->dense_bits, &h->super_off, &h->cand, &h->cuts,
-                      &h->counts, &h->stage};
+                      &h->counts, &h->stage, &h->hctr, &h->items, &h->trees, &h->gcv,
+                      &h->hashes, &h->packed};
     for (DevBuf *b : bufs) b->release();
     (void)hipStreamDestroy(h->stream);
     delete h;
@@ -423,13 +466,27 @@ int32_t syncr_cdc_launch(syncr_cdc *h, const uint8_t *d_bytes, void *stream) {
     if (h->span && !d_bytes) return SYNCR_CDC_EINVAL;
     if (((uintptr_t)d_bytes & 15u) != 0) return SYNCR_CDC_EINVAL;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    h->hash_on = false;
     return do_launch(h, d_bytes, s);
 }
 
-int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap, uint64_t *per_file_count,
-                        uint64_t *n_out) {
+int32_t syncr_cdc_launch_hashed(syncr_cdc *h, const uint8_t *d_bytes, void *stream) {
+    if (!h) return SYNCR_CDC_EINVAL;
+    if (!h->planned) return SYNCR_CDC_ESTATE;
+    if (h->span && !d_bytes) return SYNCR_CDC_EINVAL;
+    if (((uintptr_t)d_bytes & 15u) != 0) return SYNCR_CDC_EINVAL;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    h->hash_on = true;
+    return do_launch(h, d_bytes, s);
+}
+
+namespace {
+// fetch / fetch_hashed: exactly one of out / hout is used (the other may be null)
+int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool hashed, uint64_t cap,
+                   uint64_t *per_file_count, uint64_t *n_out) {
     if (!h) return SYNCR_CDC_EINVAL;
     if (!h->launched) return SYNCR_CDC_ESTATE;
+    if (hashed && !h->hash_on) return SYNCR_CDC_ESTATE;
     try {
         CHECK_HIP(hipSetDevice(h->device));
         for (int attempt = 0; attempt < 8; attempt++) {
@@ -477,17 +534,34 @@ int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap, uint64_t *pe
             if (per_file_count)
                 for (uint32_t i = 0; i < h->nfiles; i++) per_file_count[i] = counts[i];
             if (n_out) *n_out = total;
-            if (total > cap || (total && !out)) return SYNCR_CDC_ERANGE;
+            if (total > cap || (total && !(hashed ? (void *)hout : (void *)out))) return SYNCR_CDC_ERANGE;
             if (total) {
                 std::vector<DevCut> all(h->total_cut_cap);
                 CHECK_HIP(hipMemcpy(all.data(), h->cuts.p, h->total_cut_cap * sizeof(DevCut), hipMemcpyDeviceToHost));
+                std::vector<uint8_t> hs;
+                if (hashed) {
+                    uint64_t hc[B3C_WORDS];
+                    CHECK_HIP(hipMemcpy(hc, h->hctr.p, sizeof hc, hipMemcpyDeviceToHost));
+                    if (hc[B3C_FLAGS] || hc[B3C_ITEMS] > h->items_cap || hc[B3C_TREES] > h->trees_cap)
+                        return SYNCR_CDC_EIO;          // capacities are exact bounds: cannot happen
+                    hs.resize(h->total_cut_cap * 32);
+                    CHECK_HIP(hipMemcpy(hs.data(), h->hashes.p, hs.size(), hipMemcpyDeviceToHost));
+                }
                 uint64_t o = 0;
                 for (uint32_t i = 0; i < h->nfiles; i++) {
-                    const DevCut *src = all.data() + h->h_cut_base[i];
+                    const uint64_t b = h->h_cut_base[i];
                     for (uint64_t j = 0; j < counts[i]; j++, o++) {
-                        out[o].offset = src[j].offset;
-                        out[o].len = src[j].len;
-                        out[o].file = src[j].file;
+                        const DevCut &c = all[b + j];
+                        if (hashed) {
+                            hout[o].offset = c.offset;
+                            hout[o].len = c.len;
+                            hout[o].file = c.file;
+                            memcpy(hout[o].hash, hs.data() + (b + j) * 32, 32);
+                        } else {
+                            out[o].offset = c.offset;
+                            out[o].len = c.len;
+                            out[o].file = c.file;
+                        }
                     }
                 }
             }
@@ -499,6 +573,17 @@ int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap, uint64_t *pe
     } catch (...) {
         return SYNCR_CDC_EIO;
     }
+}
+}  // namespace
+
+int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap, uint64_t *per_file_count,
+                        uint64_t *n_out) {
+    return fetch_impl(h, out, nullptr, false, cap, per_file_count, n_out);
+}
+
+int32_t syncr_cdc_fetch_hashed(syncr_cdc *h, syncr_chunk_info *out, uint64_t cap, uint64_t *per_file_count,
+                               uint64_t *n_out) {
+    return fetch_impl(h, nullptr, out, true, cap, per_file_count, n_out);
 }
 
 int32_t syncr_cdc_chunk_batch_device(syncr_cdc *h, const uint8_t *d_bytes, uint64_t span,
@@ -522,6 +607,28 @@ int32_t syncr_cdc_chunk_batch_host(syncr_cdc *h, const uint8_t *data, uint64_t s
     if (span) CHECK_HIP(hipMemcpyAsync(h->stage.p, data, span, hipMemcpyHostToDevice, h->stream));
     return syncr_cdc_chunk_batch_device(h, h->stage.as<uint8_t>(), span, file_off, file_len, nfiles,
                                         out, cap, per_file_count, n_out, h->stream);
+}
+
+int32_t syncr_cdc_chunk_batch_host_hashed(syncr_cdc *h, const uint8_t *data, uint64_t span,
+                                          const uint64_t *file_off, const uint64_t *file_len,
+                                          uint32_t nfiles, syncr_chunk_info *out, uint64_t cap,
+                                          uint64_t *per_file_count, uint64_t *n_out) {
+    if (!h || (span && !data)) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    CHECK_HIP(h->stage.ensure(std::max<uint64_t>(span, 16)));
+    if (span) CHECK_HIP(hipMemcpyAsync(h->stage.p, data, span, hipMemcpyHostToDevice, h->stream));
+    int32_t rc = syncr_cdc_plan(h, file_off, file_len, nfiles, span);
+    if (rc) return rc;
+    rc = syncr_cdc_launch_hashed(h, h->stage.as<uint8_t>(), h->stream);
+    if (rc) return rc;
+    return syncr_cdc_fetch_hashed(h, out, cap, per_file_count, n_out);
+}
+
+int32_t syncr_cdc_chunk_host_hashed(syncr_cdc *h, const uint8_t *data, uint64_t len, syncr_chunk_info *out,
+                                    uint64_t cap, uint64_t *n_out) {
+    const uint64_t off = 0;
+    uint64_t cnt = 0;
+    return syncr_cdc_chunk_batch_host_hashed(h, data, len, &off, &len, 1, out, cap, &cnt, n_out);
 }
 
 int32_t syncr_cdc_chunk_host(syncr_cdc *h, const uint8_t *data, uint64_t len, syncr_cut *out,
@@ -644,7 +751,7 @@ int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable) {
     (void)hipSetDevice(h->device);
     drain_timing(h);
     h->timing = enable != 0;
-    h->ms[0] = h->ms[1] = h->ms[2] = 0;
+    for (double &m : h->ms) m = 0;
     h->timed_launches = 0;
     return SYNCR_CDC_OK;
 }
@@ -654,6 +761,15 @@ int32_t syncr_cdc_kernel_times(syncr_cdc *h, double *ms3, uint64_t *launches) {
     (void)hipSetDevice(h->device);
     drain_timing(h);
     if (ms3) for (int k = 0; k < 3; k++) ms3[k] = h->ms[k];
+    if (launches) *launches = h->timed_launches;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_kernel_times_ex(syncr_cdc *h, double *ms, uint32_t n, uint64_t *launches) {
+    if (!h || (n && !ms)) return SYNCR_CDC_EINVAL;
+    (void)hipSetDevice(h->device);
+    drain_timing(h);
+    for (uint32_t k = 0; k < n; k++) ms[k] = k < (uint32_t)NPHASE ? h->ms[k] : 0.0;
     if (launches) *launches = h->timed_launches;
     return SYNCR_CDC_OK;
 }

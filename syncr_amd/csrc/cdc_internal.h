@@ -102,6 +102,30 @@ struct Tables {
     uint64_t *counts;              // [nfiles]
 };
 
+// ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------
+// A lane TASK is B3_LANE_LEAVES consecutive 1 KiB leaves of one chunk.  A chunk
+// of T <= 64 tasks is PACKED: class c = ceil(log2 T), 64 >> c such chunks per
+// wave, each in an aligned run of 2^c lanes.  A chunk of T > 64 tasks is split
+// into GROUP items of 64 tasks (one wave each) merged by b3_tree_kernel.
+constexpr uint32_t B3_LANE_LEAVES = 4;                      // 1 KiB leaves per lane task
+constexpr uint32_t B3_GROUP_LEAVES = 64 * B3_LANE_LEAVES;   // leaves per group item (one wave)
+constexpr int B3_CLASSES = 7;                               // packed classes: <= 1, 2, 4, ..., 64 tasks
+enum { B3C_ITEMS = 0, B3C_TREES = 1, B3C_NEXT = 2, B3C_FLAGS = 3, B3C_PK0 = 4, B3C_WORDS = 4 + B3_CLASSES };
+
+struct HashTables {
+    uint64_t *ctr;                 // [B3C_WORDS] (zeroed per hashed launch)
+    uint64_t *items;               // [items_cap] slot << 24 | group (group items of big chunks)
+    uint64_t items_cap;
+    uint64_t *packed;              // [B3_CLASSES * packed_cap] chunk slots by packed class
+    uint64_t packed_cap;
+    ulonglong2 *trees;             // [trees_cap] {slot, first item} of multi-item chunks
+    uint64_t trees_cap;
+    uint32_t *gcv;                 // [items_cap * 8] item chaining values
+    uint32_t *hashes;              // [sum cut_cap * 8] BLAKE3 of each cut slot
+    uint32_t ablate;               // timing-only (SYNCR_B3_ABLATE): 1 = loads only, 2 = no loads
+    uint32_t nt;                   // 1: non-temporal chunk loads (SYNCR_B3_NT)
+};
+
 // launchers (cdc_kernels.hip)
 bool scan_supported(ScanGeom g);
 int scan_tile_bytes(ScanGeom g);
@@ -115,6 +139,8 @@ hipError_t launch_resolve(const uint8_t *d_bytes, const KParams &p, const Tables
 hipError_t launch_gen(uint8_t *d_base, const uint64_t *d_foff, const uint64_t *d_flen,
                       const uint64_t *d_findex, const uint64_t *d_seg_prefix, uint32_t nfiles,
                       uint64_t nseg, uint64_t first_index, const uint64_t *d_jump, hipStream_t s);
+hipError_t launch_hash(int device, const uint8_t *d_bytes, const Tables &t, const HashTables &ht,
+                       hipStream_t s);
 constexpr int GEN_SEG = 4096;     // bytes generated per thread
 constexpr int GEN_JUMPS = 48;     // xorshift jump matrices M^(2^k), k < 48
 

@@ -52,7 +52,7 @@ def test_gfx950_code_object(lib):
 
 def test_abi_and_defaults(lib):
     import syncr_amd
-    assert lib.syncr_cdc_abi_version() == 1
+    assert lib.syncr_cdc_abi_version() == syncr_amd.ABI_VERSION == 2
     p = syncr_amd.Params()
     lib.syncr_cdc_default_params(ctypes.byref(p))
     # src/chunking.rs:7-13 and the 2 MiB tokio read of file_operations.rs:738,776

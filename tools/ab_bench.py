@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--workload", default="zipf10k")
+    ap.add_argument("--hashed", action="store_true", help="launch_hashed (BLAKE3 of every chunk)")
     args = ap.parse_args()
     sizes, idx, _ = bench.workload(args.workload, 1)
     offs = np.zeros_like(sizes)
@@ -48,17 +49,17 @@ def main():
         os.environ.clear()
         os.environ.update(saved)
         c.plan(offs, sizes, span)
-        c.launch(buf.ptr)
-        ref = c.fetch()
+        c.launch(buf.ptr, hashed=args.hashed)
+        ref = c.fetch(hashed=args.hashed)
         handles.append((v, c, sum(x.size for x in ref)))
-    res = {v: ([], [], [], []) for v, _, _ in handles}
+    res = {v: ([], [], [], [], []) for v, _, _ in handles}
     for _ in range(args.rounds):
         for v, c, _ in handles:
             c.synchronize()
             c.set_timing(True)
             t0 = time.perf_counter()
             for _ in range(args.steps):
-                c.launch(buf.ptr)
+                c.launch(buf.ptr, hashed=args.hashed)
             c.synchronize()
             dt = (time.perf_counter() - t0) / args.steps * 1e3
             ms, n = c.kernel_times()
@@ -67,11 +68,14 @@ def main():
             res[v][1].append(dt)
             res[v][2].append(ms[1] / n)
             res[v][3].append(ms[2] / n)
+            res[v][4].append(ms[3] / n)
     for v, c, ncuts in handles:
-        sc, st, po, rz = res[v]
+        sc, st, po, rz, hs = res[v]
         print(f"{v:40s} scan med {statistics.median(sc):.4f} min {min(sc):.4f} ms  "
               f"({span / statistics.median(sc) / 1e6:.0f} GB/s)  step med {statistics.median(st):.4f} ms  "
               f"post {statistics.median(po):.4f} resolve {statistics.median(rz):.4f} ms  "
+              + (f"hash {statistics.median(hs):.4f} ms ({span / statistics.median(hs) / 1e6:.0f} GB/s)  "
+                 if args.hashed else "") +
               f"cuts {ncuts}  {c.info()['scan_grid']} waves")
     buf.free()
 
