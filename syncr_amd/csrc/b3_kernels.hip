@@ -308,6 +308,20 @@ __global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict_
         const uint32_t nblk = act ? (nbytes ? (nbytes + 63) >> 6 : 1u) : 0u;
         const uint32_t nl = (nblk + 15) >> 4;                    // leaves of this task
         uint32_t lc[LPL][8];                                     // leaf CVs
+        // block t of the task (t < nblk) is at task offset 64*t; the next
+        // block's loads are issued before the current block is compressed
+        auto fetch = [&](uint32_t t, uint32_t m[16]) {
+            const uint32_t off = t * 64;
+            const uint32_t vb = nbytes > off ? min(64u, nbytes - off) : 0u;
+            if constexpr (ABLATE == 2) {               // timing only: no loads
+#pragma unroll
+                for (int q = 0; q < 16; ++q) m[q] = (uint32_t)lane * 0x9E3779B9u + q + off;
+            } else {
+                load_block<NT>(data, T.span, cstart + lane_off + off, vb, m);
+            }
+        };
+        uint32_t m[16];
+        if (nblk) fetch(0, m);
 #pragma unroll
         for (uint32_t jj = 0; jj < LPL; ++jj) {
             if (jj >= nl) continue;
@@ -316,15 +330,12 @@ __global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict_
             const uint32_t tb = jj * 16;
             const uint32_t lb = min(16u, nblk - tb);               // blocks of this leaf
             for (uint32_t b = 0; b < lb; ++b) {
-                const uint32_t off = (tb + b) * 64;
+                const uint32_t t = tb + b;
+                uint32_t mn[16];
+                const bool more = t + 1 < nblk;
+                if (more) fetch(t + 1, mn);
+                const uint32_t off = t * 64;
                 const uint32_t vb = nbytes > off ? min(64u, nbytes - off) : 0u;
-                uint32_t m[16];
-                if constexpr (ABLATE == 2) {           // timing only: no loads
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) m[q] = (uint32_t)lane * 0x9E3779B9u + q + off;
-                } else {
-                    load_block<NT>(data, T.span, cstart + lane_off + off, vb, m);
-                }
                 uint32_t fl = (b == 0 ? B3_START : 0u) | (b + 1 == lb ? B3_END : 0u);
                 if (b + 1 == lb && nleaves == 1) fl |= B3_ROOT;
                 if constexpr (ABLATE == 1) {           // timing only: loads, no compression
@@ -333,12 +344,18 @@ __global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict_
                 } else {
                     compress(cv, m, j0 + jj, vb, fl);
                 }
+                if (more) {
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) m[q] = mn[q];
+                }
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) lc[jj][q] = cv[q];
         }
         // fold the task's leaves (left-balanced level pairing); ROOT when the
-        // task is the whole chunk
+        // task is the whole chunk.  (A cooperative variant -- 4 lanes load one
+        // task's 64 contiguous bytes, LDS transpose -- cut the load-only time
+        // 4.5 -> 3.6 ms but cost a wave per SIMD and was slower overall.)
         const bool task_root = root && mm == 1;
 #pragma unroll
         for (uint32_t d = 1; d < LPL; d <<= 1)
