@@ -136,7 +136,7 @@ def cpu_baseline(chunker, dbuf, offs, lens, cuts, sample_gib: float, hashed: boo
         o, n = [], []
         for j in range(take.size):
             ends = ref[j].astype(np.uint64)
-            starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64)
+            starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64)[:ends.size]
             o.append(starts + s_offs[j])
             n.append(ends - starts)
         return (np.concatenate(o) if o else np.zeros(0, np.uint64),

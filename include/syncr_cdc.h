@@ -125,6 +125,36 @@ int32_t syncr_cdc_chunk_batch_device(syncr_cdc *h, const uint8_t *d_bytes, uint6
                                      uint32_t nfiles, syncr_cut *out, uint64_t cap,
                                      uint64_t *per_file_count, uint64_t *n_out, void *stream);
 
+/* --- batched ingest pipeline (a whole directory walk) ------------------------
+ * Replaces the serial per-file loop of traverse_and_stream
+ * (src/protocol/file_operations.rs:544-715, which awaits compute_file_chunks per
+ * file at :599-605): files are appended to pinned staging batches of
+ * `batch_bytes`; a full batch is copied to the device and chunked + BLAKE3-hashed
+ * on its own stream while the next one fills (`depth` batches in flight).  Each
+ * file's ChunkInfo list comes back through `cb`, in submission order, on the
+ * thread that called submit / flush.  `status` is 0, or -errno for a file that
+ * could not be opened or read (then n = 0: the reference's empty list,
+ * file_operations.rs:727-744).  In callbacks chunk.file is 0.  A file larger than
+ * batch_bytes gets a batch of its own.  copy_threads: host threads used for
+ * large copies / reads into pinned memory (1 = the caller only). */
+typedef struct syncr_ingest syncr_ingest;
+typedef void (*syncr_ingest_cb)(void *ctx, uint64_t tag, int32_t status, const syncr_chunk_info *chunks,
+                                uint64_t n);
+int32_t syncr_ingest_open(int32_t device, const syncr_cdc_params *p, uint64_t batch_bytes, uint32_t depth,
+                          uint32_t copy_threads, syncr_ingest_cb cb, void *ctx, syncr_ingest **out);
+/* bytes already in memory (copied into the staging batch) */
+int32_t syncr_ingest_submit(syncr_ingest *g, const uint8_t *data, uint64_t len, uint64_t tag);
+/* a file read with pread straight into pinned staging */
+int32_t syncr_ingest_submit_file(syncr_ingest *g, const char *path, uint64_t tag);
+/* zero-copy: reserve `len` bytes of pinned staging, fill them, then commit */
+int32_t syncr_ingest_reserve(syncr_ingest *g, uint64_t len, uint8_t **dst);
+int32_t syncr_ingest_commit(syncr_ingest *g, uint64_t tag);
+/* seal the current batch and deliver every outstanding file */
+int32_t syncr_ingest_flush(syncr_ingest *g);
+/* [files, bytes, batches, chunks] so far */
+int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4);
+void syncr_ingest_close(syncr_ingest *g);
+
 /* --- device memory / stream / timing helpers (hosts without a GPU framework) -- */
 int32_t syncr_cdc_device_alloc(syncr_cdc *h, uint64_t bytes, void **d_ptr);
 int32_t syncr_cdc_device_free(syncr_cdc *h, void *d_ptr);

@@ -24,7 +24,7 @@ import numpy as np
 
 __all__ = [
     "CHUNK_BITS", "MAX_CHUNK_SIZE_FACTOR", "MAX_CHUNK_SIZE", "TOKIO_READ_CAP",
-    "ChunkInfo", "Chunker", "SyncrCdcError", "compute_file_chunks", "chunk_data",
+    "ChunkInfo", "Chunker", "Ingest", "SyncrCdcError", "compute_file_chunks", "chunk_data",
     "library", "library_path", "EXPORTED_SYMBOLS",
 ]
 
@@ -50,6 +50,8 @@ EXPORTED_SYMBOLS = (
     "syncr_cdc_last_stats", "syncr_cdc_get_info",
     "syncr_cdc_chunk_host_hashed", "syncr_cdc_chunk_batch_host_hashed", "syncr_cdc_launch_hashed",
     "syncr_cdc_fetch_hashed", "syncr_cdc_kernel_times_ex",
+    "syncr_ingest_open", "syncr_ingest_submit", "syncr_ingest_submit_file", "syncr_ingest_reserve",
+    "syncr_ingest_commit", "syncr_ingest_flush", "syncr_ingest_stats", "syncr_ingest_close",
 )
 
 ABI_VERSION = 2
@@ -81,6 +83,8 @@ assert CHUNK_INFO_DTYPE.itemsize == 48
 _lib = None
 _vp, _u64, _u32, _i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32
 _pu64 = ctypes.POINTER(ctypes.c_uint64)
+# syncr_ingest_cb(ctx, tag, status, const syncr_chunk_info *chunks, n)
+_INGEST_CB = ctypes.CFUNCTYPE(None, _vp, _u64, _i32, _vp, _u64)
 
 
 def library():
@@ -123,6 +127,15 @@ def library():
             "syncr_cdc_launch_hashed": ([_vp, _vp, _vp], _i32),
             "syncr_cdc_fetch_hashed": ([_vp, _vp, _u64, _vp, _pu64], _i32),
             "syncr_cdc_kernel_times_ex": ([_vp, ctypes.POINTER(ctypes.c_double), _u32, _pu64], _i32),
+            "syncr_ingest_open": ([_i32, ctypes.POINTER(Params), _u64, _u32, _u32, _INGEST_CB, _vp,
+                                   ctypes.POINTER(_vp)], _i32),
+            "syncr_ingest_submit": ([_vp, _vp, _u64, _u64], _i32),
+            "syncr_ingest_submit_file": ([_vp, ctypes.c_char_p, _u64], _i32),
+            "syncr_ingest_reserve": ([_vp, _u64, ctypes.POINTER(_vp)], _i32),
+            "syncr_ingest_commit": ([_vp, _u64], _i32),
+            "syncr_ingest_flush": ([_vp], _i32),
+            "syncr_ingest_stats": ([_vp, _pu64], _i32),
+            "syncr_ingest_close": ([_vp], None),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -337,6 +350,82 @@ class DeviceBuffer:
         if self.ptr:
             library().syncr_cdc_device_free(self._c.handle, self.ptr)
             self.ptr = 0
+
+
+class Ingest:
+    """Batched ingest pipeline (syncr_ingest_*): the directory walk of
+    traverse_and_stream (file_operations.rs:544-715) without its serial
+    per-file await.  Files go into pinned staging batches; each sealed batch is
+    chunked + hashed on the GPU while the next fills.  Results arrive in
+    submission order as (tag, status, ChunkInfo structured array) through
+    `on_file`, or are collected in `.results` when no callback is given."""
+
+    def __init__(self, chunk_bits: int = CHUNK_BITS, max_chunk: int = MAX_CHUNK_SIZE,
+                 read_cap: int = TOKIO_READ_CAP, device: int = 0, batch_bytes: int = 256 << 20,
+                 depth: int = 3, copy_threads: int = 8, on_file=None):
+        L = library()
+        self.params = Params(chunk_bits, 0, max_chunk, read_cap)
+        self.results: list[tuple[int, int, np.ndarray]] = []
+        self._user = on_file
+
+        def cb(_ctx, tag, status, ptr, n):
+            a = np.zeros(n, CHUNK_INFO_DTYPE)
+            if n:
+                ctypes.memmove(a.ctypes.data, ptr, n * CHUNK_INFO_DTYPE.itemsize)
+            if self._user is not None:
+                self._user(int(tag), int(status), a)
+            else:
+                self.results.append((int(tag), int(status), a))
+
+        self._cb = _INGEST_CB(cb)           # keep alive for the handle's lifetime
+        h = _vp()
+        _check(L.syncr_ingest_open(device, ctypes.byref(self.params), batch_bytes, depth, copy_threads,
+                                   self._cb, None, ctypes.byref(h)), "syncr_ingest_open")
+        self._h = h
+
+    def submit(self, data, tag: int) -> None:
+        a = _u8(data)
+        _check(library().syncr_ingest_submit(self._h, a.ctypes.data if a.size else None, a.size, tag),
+               "syncr_ingest_submit")
+
+    def submit_file(self, path, tag: int) -> None:
+        _check(library().syncr_ingest_submit_file(self._h, os.fsencode(path), tag), "syncr_ingest_submit_file")
+
+    def reserve(self, n: int) -> np.ndarray:
+        """Zero-copy: a writable view of n bytes of pinned staging; commit() after filling."""
+        p = _vp()
+        _check(library().syncr_ingest_reserve(self._h, n, ctypes.byref(p)), "syncr_ingest_reserve")
+        if not n:
+            return np.zeros(0, np.uint8)
+        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(n,))
+
+    def commit(self, tag: int) -> None:
+        _check(library().syncr_ingest_commit(self._h, tag), "syncr_ingest_commit")
+
+    def flush(self) -> None:
+        _check(library().syncr_ingest_flush(self._h), "syncr_ingest_flush")
+
+    def stats(self) -> dict:
+        st = (ctypes.c_uint64 * 4)()
+        _check(library().syncr_ingest_stats(self._h, st), "syncr_ingest_stats")
+        return {"files": st[0], "bytes": st[1], "batches": st[2], "chunks": st[3]}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            library().syncr_ingest_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _split(cuts: np.ndarray, counts: np.ndarray) -> list[np.ndarray]:
