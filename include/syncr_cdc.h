@@ -125,6 +125,23 @@ int32_t syncr_cdc_chunk_batch_device(syncr_cdc *h, const uint8_t *d_bytes, uint6
                                      uint32_t nfiles, syncr_cut *out, uint64_t cap,
                                      uint64_t *per_file_count, uint64_t *n_out, void *stream);
 
+/* --- wire / on-disk text of chunk lists ---------------------------------------
+ * Byte-identical with what the reference emits for a ChunkInfo list
+ * (hash = util::hash_to_base64, base64 URL_SAFE with padding, src/util.rs:62-64):
+ *   SYNCR_FMT_LIST_LINES  LIST reply, one line per chunk (src/protocol/v3_server.rs:146-182:
+ *                         serde_json::to_string(&json!({"typ","off","len","hsh"})) + "\n";
+ *                         serde_json's default Map is a BTreeMap, so keys come sorted):
+ *                         {"hsh":"<b64>","len":<size>,"off":<offset>,"typ":"C"}\n
+ *   SYNCR_FMT_HASHCHUNKS  the "ch" array of a profile FileData (HashChunk's Serialize,
+ *                         src/types.rs:117-129, through json5::to_string at
+ *                         src/sync_impl/mod.rs:1167-1172): [{"h":"<b64>","of":<offset>,"sz":<size>},...]
+ * Writes at most cap bytes (no terminating NUL); *len_out = bytes needed;
+ * SYNCR_CDC_ERANGE if cap is too small. */
+#define SYNCR_FMT_LIST_LINES 1
+#define SYNCR_FMT_HASHCHUNKS 2
+int32_t syncr_cdc_format_chunks(const syncr_chunk_info *chunks, uint64_t n, int32_t format, char *out,
+                                uint64_t cap, uint64_t *len_out);
+
 /* --- batched ingest pipeline (a whole directory walk) ------------------------
  * Replaces the serial per-file loop of traverse_and_stream
  * (src/protocol/file_operations.rs:544-715, which awaits compute_file_chunks per

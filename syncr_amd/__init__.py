@@ -24,7 +24,7 @@ import numpy as np
 
 __all__ = [
     "CHUNK_BITS", "MAX_CHUNK_SIZE_FACTOR", "MAX_CHUNK_SIZE", "TOKIO_READ_CAP",
-    "ChunkInfo", "Chunker", "Ingest", "SyncrCdcError", "compute_file_chunks", "chunk_data",
+    "ChunkInfo", "Chunker", "Ingest", "SyncrCdcError", "format_chunks", "compute_file_chunks", "chunk_data",
     "library", "library_path", "EXPORTED_SYMBOLS",
 ]
 
@@ -50,12 +50,15 @@ EXPORTED_SYMBOLS = (
     "syncr_cdc_last_stats", "syncr_cdc_get_info",
     "syncr_cdc_chunk_host_hashed", "syncr_cdc_chunk_batch_host_hashed", "syncr_cdc_launch_hashed",
     "syncr_cdc_fetch_hashed", "syncr_cdc_kernel_times_ex",
+    "syncr_cdc_format_chunks",
     "syncr_ingest_open", "syncr_ingest_submit", "syncr_ingest_submit_file", "syncr_ingest_reserve",
     "syncr_ingest_commit", "syncr_ingest_flush", "syncr_ingest_stats", "syncr_ingest_close",
 )
 
 ABI_VERSION = 2
 E_RANGE = -34
+FMT_LIST_LINES = 1      # LIST reply "C" lines (src/protocol/v3_server.rs:146-182)
+FMT_HASHCHUNKS = 2      # profile FileData "ch" array (src/types.rs:117-129)
 
 
 class SyncrCdcError(RuntimeError):
@@ -127,6 +130,7 @@ def library():
             "syncr_cdc_launch_hashed": ([_vp, _vp, _vp], _i32),
             "syncr_cdc_fetch_hashed": ([_vp, _vp, _u64, _vp, _pu64], _i32),
             "syncr_cdc_kernel_times_ex": ([_vp, ctypes.POINTER(ctypes.c_double), _u32, _pu64], _i32),
+            "syncr_cdc_format_chunks": ([_vp, _u64, _i32, _vp, _u64, _pu64], _i32),
             "syncr_ingest_open": ([_i32, ctypes.POINTER(Params), _u64, _u32, _u32, _INGEST_CB, _vp,
                                    ctypes.POINTER(_vp)], _i32),
             "syncr_ingest_submit": ([_vp, _vp, _u64, _u64], _i32),
@@ -350,6 +354,20 @@ class DeviceBuffer:
         if self.ptr:
             library().syncr_cdc_device_free(self._c.handle, self.ptr)
             self.ptr = 0
+
+
+def format_chunks(chunks: np.ndarray, fmt: int = FMT_LIST_LINES) -> bytes:
+    """Reference wire/on-disk text of a ChunkInfo list (CHUNK_INFO_DTYPE array):
+    LIST reply lines or the profile's HashChunk array (syncr_cdc_format_chunks)."""
+    a = np.ascontiguousarray(chunks, dtype=CHUNK_INFO_DTYPE)
+    n = ctypes.c_uint64(0)
+    rc = library().syncr_cdc_format_chunks(a.ctypes.data if a.size else None, a.size, fmt, None, 0, ctypes.byref(n))
+    if rc not in (0, E_RANGE):
+        _check(rc, "syncr_cdc_format_chunks")
+    buf = ctypes.create_string_buffer(max(int(n.value), 1))
+    _check(library().syncr_cdc_format_chunks(a.ctypes.data if a.size else None, a.size, fmt, buf, n.value,
+                                             ctypes.byref(n)), "syncr_cdc_format_chunks")
+    return buf.raw[: int(n.value)]
 
 
 class Ingest:

@@ -796,3 +796,79 @@ extern "C" int32_t syncr_cdc_get_info(const syncr_cdc *h, uint64_t *info8) {
     info8[7] = SYNCR_CDC_ABI_VERSION;
     return SYNCR_CDC_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Wire / on-disk text of chunk lists (include/syncr_cdc.h, SYNCR_FMT_*).
+// ---------------------------------------------------------------------------
+namespace {
+
+// base64 URL_SAFE with padding (base64 0.22 general_purpose::URL_SAFE,
+// util::hash_to_base64, src/util.rs:62-64): 32 bytes -> 44 chars
+void b64url32(const uint8_t h[32], char out[44]) {
+    static const char A[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+    int o = 0;
+    for (int i = 0; i < 30; i += 3) {
+        const uint32_t v = (uint32_t)h[i] << 16 | (uint32_t)h[i + 1] << 8 | h[i + 2];
+        out[o++] = A[v >> 18];
+        out[o++] = A[(v >> 12) & 63];
+        out[o++] = A[(v >> 6) & 63];
+        out[o++] = A[v & 63];
+    }
+    const uint32_t v = (uint32_t)h[30] << 16 | (uint32_t)h[31] << 8;
+    out[o++] = A[v >> 18];
+    out[o++] = A[(v >> 12) & 63];
+    out[o++] = A[(v >> 6) & 63];
+    out[o++] = '=';
+}
+
+struct Sink {
+    char *out;
+    uint64_t cap, n = 0;
+    void put(const char *s, size_t k) {
+        if (n + k <= cap && out) memcpy(out + n, s, k);
+        n += k;
+    }
+    void str(const char *s) { put(s, strlen(s)); }
+    void u64(uint64_t v) {
+        char b[24];
+        int k = 0;
+        do { b[k++] = (char)('0' + v % 10); v /= 10; } while (v);
+        char r[24];
+        for (int i = 0; i < k; i++) r[i] = b[k - 1 - i];
+        put(r, (size_t)k);
+    }
+};
+
+}  // namespace
+
+extern "C" int32_t syncr_cdc_format_chunks(const syncr_chunk_info *c, uint64_t n, int32_t format, char *out,
+                                           uint64_t cap, uint64_t *len_out) {
+    if ((n && !c) || (format != SYNCR_FMT_LIST_LINES && format != SYNCR_FMT_HASHCHUNKS)) return SYNCR_CDC_EINVAL;
+    Sink s{out, out ? cap : 0};
+    char h[44];
+    if (format == SYNCR_FMT_HASHCHUNKS) s.put("[", 1);
+    for (uint64_t i = 0; i < n; i++) {
+        b64url32(c[i].hash, h);
+        if (format == SYNCR_FMT_LIST_LINES) {            // v3_server.rs:148-153, BTreeMap key order
+            s.str("{\"hsh\":\"");
+            s.put(h, 44);
+            s.str("\",\"len\":");
+            s.u64(c[i].len);
+            s.str(",\"off\":");
+            s.u64(c[i].offset);
+            s.str(",\"typ\":\"C\"}\n");
+        } else {                                         // types.rs:122-127, field order h, of, sz
+            if (i) s.put(",", 1);
+            s.str("{\"h\":\"");
+            s.put(h, 44);
+            s.str("\",\"of\":");
+            s.u64(c[i].offset);
+            s.str(",\"sz\":");
+            s.u64(c[i].len);
+            s.put("}", 1);
+        }
+    }
+    if (format == SYNCR_FMT_HASHCHUNKS) s.put("]", 1);
+    if (len_out) *len_out = s.n;
+    return s.n > s.cap ? SYNCR_CDC_ERANGE : SYNCR_CDC_OK;
+}
