@@ -10,7 +10,7 @@
 // left-balanced binary tree of PARENT compressions; the last compression of
 // the root gets the ROOT flag.  Leaves are independent; a lane TASK is
 // LPL = B3_LANE_LEAVES consecutive leaves (contiguous bytes):
-//   b3_items_kernel  one wave per file: a chunk of T <= 64 tasks goes to packed
+//   b3_items_kernel  one block per 256 files: a chunk of T <= 64 tasks goes to packed
 //                    class c = ceil(log2 T) (64 >> c chunks share a wave, each
 //                    in an aligned run of 2^c lanes); a bigger chunk becomes
 //                    ceil(T / 64) group items plus a tree entry;
@@ -184,53 +184,82 @@ __device__ __forceinline__ uint32_t ceil_log2(uint32_t t) { return t <= 1 ? 0u :
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// One wave per file, lanes over its cuts: packed chunks are appended to their
-// class list; big chunks get group items (slot << 24 | group) and a tree
-// entry {slot, first item}.  A file whose cuts overflowed its output slots is
-// skipped (the host re-launches).
+// One block per 256 files: the block's cuts form one flat list (a block scan
+// of the per-file counts), so every thread has work whatever the file sizes.
+// Packed chunks are appended to their class list; big chunks get group items
+// (slot << 24 | group, contiguous per chunk) and a tree entry {slot, first
+// item}.  Slots are handed out by LDS atomics in two passes (count, then
+// place) so the global counters see one atomic per list per block.  A file
+// whose cuts overflowed its output slots is skipped (the host re-launches).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (i >= T.nfiles) return;
-    const uint64_t n = T.counts[i];
-    if (n > T.cut_cap[i]) return;
-    const uint64_t cb = T.cut_base[i];
-    for (uint64_t k0 = 0; k0 < n; k0 += 64) {
-        const uint64_t k = k0 + (uint64_t)lane;
-        const uint64_t slot = cb + k;
-        uint32_t ng = 0;
-        if (k < n) {
-            const uint32_t t = chunk_tasks(T.cuts[slot].len);
-            if (t <= 64) {
-                const uint32_t c = ceil_log2(t);
-                const uint64_t idx = atomicAdd((unsigned long long *)&H.ctr[B3C_PK0 + c], 1ull);
-                if (idx < H.packed_cap) H.packed[c * H.packed_cap + idx] = slot;
+    constexpr int NL = B3_CLASSES + 2;                   // lists: classes, group items, trees
+    constexpr int LIST_ITEMS = B3_CLASSES, LIST_TREES = B3_CLASSES + 1;
+    __shared__ uint32_t cnt[NL];
+    __shared__ uint64_t gbase[NL];
+    __shared__ uint32_t foff[257];                       // exclusive prefix of cut counts
+    __shared__ uint64_t fbase[256];                      // cut_base of the block's files
+    __shared__ uint32_t wsum[4];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t i = blockIdx.x * 256 + t;
+    uint32_t nc = 0;
+    if (i < T.nfiles) {
+        const uint64_t n = T.counts[i];
+        if (n <= T.cut_cap[i]) nc = (uint32_t)n;
+        fbase[t] = T.cut_base[i];
+    }
+    if (t < NL) cnt[t] = 0;
+    const uint32_t incl = wave_incl_scan_u32(nc, (int)lane);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t k = 0; k < w; ++k) before += wsum[k];
+    foff[t + 1] = before + incl;
+    if (t == 0) foff[0] = 0;
+    __syncthreads();
+    const uint32_t total = foff[256];
+    auto visit = [&](bool place) {
+        for (uint32_t q = t; q < total; q += 256) {
+            uint32_t lo = 0, hi = 256;                   // last f with foff[f] <= q
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (foff[mid] <= q) lo = mid; else hi = mid;
+            }
+            const uint64_t slot = fbase[lo] + (q - foff[lo]);
+            const uint32_t tk = chunk_tasks(T.cuts[slot].len);
+            if (tk <= 64) {
+                const uint32_t c = ceil_log2(tk);
+                const uint32_t li = atomicAdd(&cnt[c], 1u);
+                if (place) {
+                    const uint64_t idx = gbase[c] + li;
+                    if (idx < H.packed_cap) H.packed[c * H.packed_cap + idx] = slot;
+                }
             } else {
-                ng = (t + 63) / 64;
+                const uint32_t ng = (tk + 63) / 64;
+                const uint32_t li = atomicAdd(&cnt[LIST_ITEMS], ng);
+                const uint32_t lt = atomicAdd(&cnt[LIST_TREES], 1u);
+                if (place) {
+                    const uint64_t first = gbase[LIST_ITEMS] + li;
+                    if (first + ng <= H.items_cap) {
+                        for (uint32_t g = 0; g < ng; ++g) H.items[first + g] = (slot << 24) | g;
+                    } else {
+                        atomicOr((unsigned long long *)&H.ctr[B3C_FLAGS], 1ull);
+                    }
+                    const uint64_t ti = gbase[LIST_TREES] + lt;
+                    if (ti < H.trees_cap) H.trees[ti] = make_ulonglong2(slot, first);
+                }
             }
         }
-        if (!__ballot(ng != 0)) continue;
-        const uint32_t incl = wave_incl_scan_u32(ng, lane);
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        uint64_t base = 0;
-        if (lane == 0) base = atomicAdd((unsigned long long *)&H.ctr[B3C_ITEMS], (unsigned long long)tot);
-        base = bcast64(base);
-        const uint64_t first = base + (incl - ng);
-        if (base + tot <= H.items_cap) {
-            for (uint32_t g = 0; g < ng; ++g) H.items[first + g] = (slot << 24) | g;
-        } else if (lane == 0) {
-            atomicOr((unsigned long long *)&H.ctr[B3C_FLAGS], 1ull);
-        }
-        const unsigned long long multi = __ballot(ng != 0);
-        uint64_t tb = 0;
-        if (lane == 0) tb = atomicAdd((unsigned long long *)&H.ctr[B3C_TREES], (unsigned long long)__popcll(multi));
-        tb = bcast64(tb);
-        if (ng) {
-            const uint64_t idx = tb + (uint64_t)__popcll(multi & ((1ull << lane) - 1ull));
-            if (idx < H.trees_cap) H.trees[idx] = make_ulonglong2(slot, first);
-        }
+    };
+    visit(false);                                        // pass 1: count per list
+    __syncthreads();
+    if (t < NL) {
+        const uint32_t gi = t < B3_CLASSES ? B3C_PK0 + t : (t == LIST_ITEMS ? B3C_ITEMS : B3C_TREES);
+        gbase[t] = cnt[t] ? atomicAdd((unsigned long long *)&H.ctr[gi], (unsigned long long)cnt[t]) : 0ull;
+        cnt[t] = 0;
     }
+    __syncthreads();
+    visit(true);                                         // pass 2: place
 }
 
 // ---------------------------------------------------------------------------
@@ -408,14 +437,15 @@ __global__ __launch_bounds__(256) void b3_tree_kernel(Tables T, HashTables H) {
                     x[4] = c.x; x[5] = c.y; x[6] = c.z; x[7] = c.w;
                 }
                 wave_merge(x, min(64u, n - b * 64), n <= 64, lane);
-                __threadfence();                 // reads of this batch before the in-place write
+                // reads of this batch before the in-place write (one wave: CU-local ordering)
+                if (n > 64) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
                 if (lane == 0) {
                     uint32_t *dst = n <= 64 ? H.hashes + slot * 8 : nodes + b * 8;
                     *(uint4 *)dst = make_uint4(x[0], x[1], x[2], x[3]);
                     *(uint4 *)(dst + 4) = make_uint4(x[4], x[5], x[6], x[7]);
                 }
             }
-            __threadfence();                     // this level's nodes visible to every lane
+            if (n > 64) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // level visible to the wave
             n = nb;
         }
     }
@@ -437,7 +467,7 @@ hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const Hash
     hipError_t e = hipMemsetAsync(ht.ctr, 0, B3C_WORDS * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     if (!t.nfiles) return hipSuccess;
-    hipLaunchKernelGGL(b3_items_kernel, dim3((t.nfiles + 3) / 4), dim3(256), 0, s, t, ht);
+    hipLaunchKernelGGL(b3_items_kernel, dim3((t.nfiles + 255) / 256), dim3(256), 0, s, t, ht);
     switch (ht.ablate * 2 + (ht.nt ? 1 : 0)) {
         case 0: launch_leaf<false, 0>(device, d, t, ht, s); break;
         case 1: launch_leaf<true, 0>(device, d, t, ht, s); break;

@@ -26,6 +26,8 @@ def counters(path):
         name = r["Kernel_Name"].split("(")[0].replace("void ", "")
         if "cdc_scan_kernel" in name:
             name = "cdc::cdc_scan_kernel"
+        if "b3_leaf_kernel" in name:
+            name = "cdc::b3_leaf_kernel"
         agg[(name, r["Counter_Name"])].append(float(r["Counter_Value"]))
     return agg
 
@@ -61,6 +63,9 @@ def main(tag, src=None):
         "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halves wide streaming reads)",
         "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/prof.sh {tag}",
         "other_kernels": {kk[0]: sum(v) / len(v) for kk, v in {**f, **w}.items() if kk[0] != k},
+        "per_kernel_hbm_bytes": {
+            kk[0]: int(2 * 1024 * sum(v) / len(v) + 1024 * (sum(w[(kk[0], "WRITE_SIZE")]) / max(len(w[(kk[0], "WRITE_SIZE")]), 1)))
+            for kk, v in f.items() if kk[1] == "FETCH_SIZE"},
     }
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
