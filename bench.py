@@ -46,6 +46,9 @@ def workload(name: str, world: int):
         one = zipf_sizes()
         desc = ("SURVEY §8d config 3: 10 000 Zipf(1.5) files, 4 KiB-128 MiB, 9.73 GiB per GPU; "
                 "N GPUs chunk N x 10 000 files (distinct seeds) LPT-sharded per file (config 4)")
+    elif name == "big1":
+        one = np.full(1, 128 * M, np.uint64)
+        desc = "diagnostic: one 128 MiB file (the longest resolve walk of zipf10k)"
     elif name == "uniform1k":
         one = np.full(1024, M, np.uint64)
         desc = "SURVEY §8d config 2: 1024 x 1 MiB files per GPU, LPT-sharded per file"
@@ -183,7 +186,7 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k"])
+    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "big1"])
     ap.add_argument("--mode", default="production", choices=["production", "ideal"])
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -75,6 +75,9 @@ struct syncr_cdc {
     uint32_t b3_ablate = 0, b3_nt = 0;
     uint64_t items_cap = 0, trees_cap = 0;
     DevBuf hctr, items, trees, gcv, hashes, packed;
+    // read-boundary grid (Tables::gpos...): production semantics only
+    uint32_t ngrid = 0;
+    DevBuf gpos, gend, gfix, gbase;
 
     // launch
     bool launched = false;
@@ -167,6 +170,11 @@ Tables make_tables(syncr_cdc *h) {
     t.cand_cap = h->cand_cap;
     t.cuts = h->cuts.as<DevCut>();
     t.counts = h->counts.as<uint64_t>();
+    t.ngrid = h->ngrid;
+    t.gpos = h->gpos.as<uint64_t>();
+    t.gend = h->gend.as<uint64_t>();
+    t.gfix = h->gfix.as<uint8_t>();
+    t.gbase = h->gbase.as<uint64_t>();
     return t;
 }
 
@@ -374,7 +382,7 @@ void syncr_cdc_close(syncr_cdc *h) {
                       &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
                       &h->dense_cnt, &h->dense_bits, &h->super_off, &h->cand, &h->cuts,
                       &h->counts, &h->stage, &h->hctr, &h->items, &h->trees, &h->gcv,
-                      &h->hashes, &h->packed};
+                      &h->hashes, &h->packed, &h->gpos, &h->gend, &h->gfix, &h->gbase};
     for (DevBuf *b : bufs) b->release();
     (void)hipStreamDestroy(h->stream);
     delete h;
@@ -451,6 +459,33 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         }
         rc = upload_cut_tables(h);
         if (rc) return rc;
+        // read-boundary grid points k * read_cap of every file (production only)
+        h->ngrid = 0;
+        if (h->params.read_cap && nfiles) {
+            const uint64_t cap = h->params.read_cap;
+            std::vector<uint64_t> gbase(nfiles), gpos, gend;
+            uint64_t acc = 0;
+            for (uint32_t i = 0; i < nfiles; i++) {
+                gbase[i] = acc;
+                const uint64_t nk = (file_len[i] + cap - 1) / cap;
+                for (uint64_t k = 0; k < nk; k++) {
+                    gpos.push_back(file_off[i] + k * cap);
+                    gend.push_back(file_off[i] + file_len[i]);
+                }
+                acc += nk;
+            }
+            if (acc > 0xffffffffull) return SYNCR_CDC_EINVAL;
+            h->ngrid = (uint32_t)acc;
+            CHECK_HIP(h->gbase.ensure(nfiles * 8ull));
+            CHECK_HIP(h->gpos.ensure(std::max<uint64_t>(acc, 1) * 8));
+            CHECK_HIP(h->gend.ensure(std::max<uint64_t>(acc, 1) * 8));
+            CHECK_HIP(h->gfix.ensure(std::max<uint64_t>(acc, 1)));
+            CHECK_HIP(hipMemcpy(h->gbase.p, gbase.data(), nfiles * 8ull, hipMemcpyHostToDevice));
+            if (acc) {
+                CHECK_HIP(hipMemcpy(h->gpos.p, gpos.data(), acc * 8, hipMemcpyHostToDevice));
+                CHECK_HIP(hipMemcpy(h->gend.p, gend.data(), acc * 8, hipMemcpyHostToDevice));
+            }
+        }
         h->planned = true;
         return SYNCR_CDC_OK;
     } catch (const std::bad_alloc &) {

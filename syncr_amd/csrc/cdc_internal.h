@@ -100,6 +100,15 @@ struct Tables {
     uint64_t cand_cap;
     DevCut *cuts;                  // [sum cut_cap]
     uint64_t *counts;              // [nfiles]
+    // read-boundary grid (production semantics): while the reference's buffer
+    // is not saturated its reads end at multiples of read_cap from the file
+    // start, so cuts forced there start chunks at those offsets; their head
+    // hits are precomputed by cdc_fix_kernel instead of rolled by the resolve
+    uint32_t ngrid;
+    const uint64_t *gpos;          // [ngrid] batch offset of grid point (file start + k * read_cap)
+    const uint64_t *gend;          // [ngrid] batch offset of that file's end
+    uint8_t *gfix;                 // [ngrid] first chunk-local hit in [p, p+63): offset + 1, 0 = none
+    const uint64_t *gbase;         // [nfiles] first grid index of each file
 };
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------

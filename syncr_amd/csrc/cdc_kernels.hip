@@ -805,15 +805,26 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
 }
 
 // Head fix-up of every candidate e (first chunk-local hit in [e+1, e+63]),
-// one thread per candidate, so the resolve walk never waits on byte loads.
+// one thread per candidate, so the resolve walk never waits on byte loads;
+// then the head hit of every read-boundary grid point (first chunk-local hit
+// in [p, min(p+63, file end)), stored as offset + 1).
 __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict__ data, KParams P,
                                                       Tables T) {
     const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
     const uint64_t n = total < T.cand_cap ? total : T.cand_cap;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        const uint64_t e = T.cand[i] & CAND_POS_MASK;
-        const uint32_t fix = head_fix_global(data, T.span, e, P.mask);
-        T.cand[i] = e | ((uint64_t)fix << 48) | CAND_KNOWN;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n + T.ngrid; i += (uint64_t)gridDim.x * 256) {
+        if (i < n) {
+            const uint64_t e = T.cand[i] & CAND_POS_MASK;
+            const uint32_t fix = head_fix_global(data, T.span, e, P.mask);
+            T.cand[i] = e | ((uint64_t)fix << 48) | CAND_KNOWN;
+        } else {
+            const uint64_t g = i - n;
+            const uint64_t p = T.gpos[g];
+            // head_fix_global(p - 1) scans [p, p+63) with the window reset at p
+            const uint64_t end = T.gend[g];
+            uint32_t f = head_fix_global(data, end, p - 1, P.mask);
+            T.gfix[g] = (uint8_t)f;
+        }
     }
 }
 
@@ -941,6 +952,193 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t k) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// The walk of one file, in file-relative offsets of type Off (uint32_t for
+// files below 4 GiB: every comparison and min stays in the scalar unit, which
+// has no 64-bit unsigned compare).  Per window lane: wr = candidate position
+// relative to the file (below the file -> 0, at/after its end or none -> OMAX;
+// monotone, so the window stays sorted), wk = head fix-up | known << 8.
+// Cuts are gathered into two VGPRs (lane k = k-th cut of a batch of 64) and
+// stored 64 at a time.
+template <typename Off>
+__device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, const KParams &P,
+                                             const Tables &T, uint32_t i, uint64_t F, uint64_t g0, int lane) {
+    constexpr Off OMAX = (Off)~(Off)0;
+    DevCut *out = T.cuts + T.cut_base[i];
+    const uint64_t cap = T.cut_cap[i];
+    const Off Fo = (Off)F;
+    const Off MAX = (Off)min<uint64_t>(P.max_chunk, (uint64_t)OMAX);
+    const Off CAP = P.read_cap ? (Off)min<uint64_t>(P.read_cap, (uint64_t)OMAX) : OMAX;
+    const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
+    const uint64_t ncand = min(total, T.cand_cap);
+    uint64_t wb = F ? T.super_off[(uint32_t)((g0 / T.tile) >> 6)] : 0;   // the file's 64-tile group
+    Off wr = OMAX;
+    uint32_t wk = 0, nx = 64;
+    auto load_window = [&]() {
+        const uint64_t c = wb + (uint64_t)lane < ncand ? T.cand[wb + lane] : NONE;
+        wr = OMAX;
+        wk = 0;
+        if (c != NONE) {
+            const uint64_t p = c & CAND_POS_MASK;
+            wr = p < g0 ? (Off)0 : (p - g0 >= F ? OMAX : (Off)(p - g0));
+            wk = (uint32_t)((c >> 48) & 0xffu) | ((c & CAND_KNOWN) ? 0x100u : 0u);
+        }
+        // nx: window index of the first candidate >= this lane's + 64, where the
+        // search resumes after a cut at it with no head hit (64 = past the window)
+        const Off key = wr == OMAX ? OMAX : (Off)(wr + 64);
+        uint32_t idx = 0;
+#pragma unroll
+        for (uint32_t st = 32; st >= 1; st >>= 1) {
+            Off pv;
+            if constexpr (sizeof(Off) == 4) {
+                pv = (Off)__shfl((int)wr, (int)(idx + st - 1));
+            } else {
+                const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)wr, (int)(idx + st - 1));
+                const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)wr >> 32), (int)(idx + st - 1));
+                pv = (Off)(((uint64_t)hi << 32) | lo);
+            }
+            if (pv < key) idx += st;
+        }
+        nx = idx;
+    };
+    auto rl = [&](Off v, uint32_t k) -> Off {                // readlane of an Off
+        if constexpr (sizeof(Off) == 4) {
+            return (Off)__builtin_amdgcn_readlane((int)v, (int)k);
+        } else {
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), (int)k);
+            return (Off)(((uint64_t)hi << 32) | lo);
+        }
+    };
+    load_window();
+    // head hits at this file's read-boundary grid points (lane k: k * read_cap)
+    const uint64_t CAPv = P.read_cap;
+    const bool grid = T.ngrid && CAPv && F;
+    uint64_t gb = 0;
+    uint32_t gf = 0;
+    if (grid) {
+        gb = T.gbase[i];
+        if ((uint64_t)lane * CAPv < F) gf = T.gfix[gb + lane];
+    }
+    // gathered cuts: lane k of (bo, bl) = cut (cnt & ~63) + k
+    Off bo = 0;
+    uint32_t bl = 0;
+    Off cnt = 0;             // cuts so far (< F + 1, so Off is wide enough)
+    auto flush = [&](uint32_t n) {
+        const uint64_t k = (uint64_t)(cnt - n) + (uint64_t)lane;   // cnt already counts these n cuts
+        if ((uint32_t)lane < n && k < cap) {
+            DevCut d;
+            d.offset = (uint64_t)bo;
+            d.len = bl;
+            d.file = i;
+            out[k] = d;
+        }
+    };
+    Off R = min(min(Fo, MAX), CAP);                          // first read (file_operations.rs:738)
+    Off s = 0;
+    int head = 2;            // 1: fix known, 2: unknown (head scan / grid; also at the file start)
+    uint32_t fix = 0;
+    int jlast = -1;          // window index of the candidate the last cut was made at
+    while (s < R) {                                          // :747
+        const Off lim = R;                                   // :749-752
+        Off e = OMAX;
+        bool known = false;
+        uint32_t cfix = 0;
+        const Off from = s + 63;                             // stream G applies from here
+        bool done = false;
+        if (head == 1 && fix == 0 && jlast >= 0) {           // chained candidate: one table hop
+            const uint32_t jn = (uint32_t)__builtin_amdgcn_readlane((int)nx, jlast);
+            if (jn < 64) {
+                const Off c = rl(wr, jn);
+                // trusted only if it moves forward: after a candidate overflow the
+                // (discarded, re-run) launch sees unwritten, unsorted entries and
+                // the walk must still terminate; the ballot search always does
+                if (c >= from) {
+                    jlast = -1;
+                    if (c < lim) {
+                        const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)wk, (int)jn);
+                        e = c;
+                        known = (k & 0x100u) != 0;
+                        cfix = k & 0xffu;
+                        jlast = (int)jn;
+                    }
+                    done = true;
+                }
+            }
+        }
+        if (!done) {
+            jlast = -1;
+            Off hh = OMAX;
+            if (head == 1) {
+                if (fix) hh = s - 1 + fix;
+            } else {
+                bool tab = false;
+                if (grid) {                                  // a read-boundary grid point: precomputed
+                    const uint64_t k = (uint64_t)s / CAPv;
+                    if (k * CAPv == (uint64_t)s) {
+                        const uint32_t f = k < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)gf, (int)k)
+                                                  : (uint32_t)T.gfix[gb + k];
+                        if (f) hh = s + (Off)(f - 1);
+                        tab = true;
+                    }
+                }
+                if (!tab) {                                  // wave head scan of [s, min(s+63, lim))
+                    const uint32_t n = (uint32_t)min<uint64_t>(63ull, (uint64_t)(lim - s));
+                    const uint32_t x = (uint32_t)lane < n ? data[g0 + (uint64_t)s + lane] : 0u;
+                    const uint32_t S = wave_incl_scan(x, lane);
+                    const uint32_t W = wave_incl_scan(S, lane);
+                    const unsigned long long m = __ballot((uint32_t)lane < n && hit_exact(S, W, P.mask));
+                    if (m) hh = s + (Off)__builtin_ctzll(m);
+                }
+            }
+            if (hh != OMAX && hh < lim) e = hh;
+            if (e == OMAX && from < lim) {
+                for (;;) {
+                    const unsigned long long m = __ballot(wr >= from);
+                    if (m) {
+                        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                        const Off c = rl(wr, j);
+                        if (c < lim) {
+                            const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)wk, (int)j);
+                            e = c;
+                            known = (k & 0x100u) != 0;
+                            cfix = k & 0xffu;
+                            jlast = (int)j;
+                        }
+                        break;
+                    }
+                    if (wb + 64 >= ncand) break;             // whole window below `from`: slide
+                    wb += 64;
+                    load_window();
+                }
+            }
+        }
+        Off cut;                                             // :754-755
+        if (e != OMAX) { cut = e + 1; head = known ? 1 : 2; fix = cfix; }
+        else { cut = lim; head = 2; }
+        const uint32_t slot = (uint32_t)cnt & 63u;
+        if ((uint32_t)lane == slot) {                        // gather: lane `slot` keeps this cut
+            bo = s;
+            bl = (uint32_t)(cut - s);
+        }
+        ++cnt;
+        if (__builtin_expect(slot == 63u, 0)) flush(64);
+        s = cut;                                             // :771
+        // :776, kept in the scalar unit (hipcc otherwise fuses the mins into a
+        // VALU v_min3 plus a readfirstlane round trip on this serial path)
+        Off rd = MAX - (R - s);
+        rd = min(rd, CAP);
+        if constexpr (sizeof(Off) == 4) asm volatile("" : "+s"(rd));
+        rd = min(rd, (Off)(Fo - R));
+        R += rd;
+    }
+    if (cnt & 63u) flush((uint32_t)(cnt & 63u));
+    if (lane == 0) {
+        T.counts[i] = (uint64_t)cnt;
+        if ((uint64_t)cnt > cap) atomicOr(&T.ctr[CTR_FLAGS], FLAG_CUT_OVERFLOW);
+    }
+}
+
+// One wave per file; files below 4 GiB walk in 32-bit offsets.
 __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__restrict__ data,
                                                                KParams P, Tables T) {
     const int lane = threadIdx.x & 63;
@@ -948,85 +1146,10 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
     if (kf >= T.nfiles) return;
     const uint32_t i = T.order[kf];
     const uint64_t F = T.flen[i], g0 = T.foff[i];
-    DevCut *out = T.cuts + T.cut_base[i];
-    const uint32_t cap = T.cut_cap[i];
-    const uint64_t MAX = P.max_chunk;
-    const uint64_t CAP = P.read_cap ? P.read_cap : ~0ull;
-    const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
-    const uint64_t ncand = min(total, T.cand_cap);
-    // candidate window: wv = cand[wb + lane] (NONE past the end)
-    uint64_t wb = 0;
-    if (F) {
-        const uint32_t w = (uint32_t)((g0 / T.tile) >> 6);
-        wb = T.super_off[w];                               // first candidate of the file's 64-tile group
-    }
-    uint64_t wv = wb + lane < ncand ? T.cand[wb + lane] : NONE;
-    uint64_t cnt = 0;
-    uint64_t R = min(min(F, MAX), CAP);                   // first read (file_operations.rs:738)
-    uint64_t s = 0;
-    int head = 2;            // 1: fix known, 2: unknown (head scan; also at the file start)
-    uint32_t fix = 0;
-    while (s < R) {                                       // :747
-        const uint64_t lim = R;                           // :749-752
-        uint64_t e = NONE;
-        bool known = false;
-        uint32_t cfix = 0;
-        const uint64_t from = s + 63;                     // stream G applies from here
-        {
-            uint64_t hh = NONE;
-            if (head == 1) {
-                if (fix) hh = s - 1 + fix;
-            } else {                                      // wave head scan of [s, min(s+63, lim))
-                const uint32_t n = (uint32_t)min<uint64_t>(63ull, lim - s);
-                const uint32_t x = (uint32_t)lane < n ? data[g0 + s + lane] : 0u;
-                const uint32_t S = wave_incl_scan(x, lane);
-                const uint32_t W = wave_incl_scan(S, lane);
-                const unsigned long long m = __ballot((uint32_t)lane < n && hit_exact(S, W, P.mask));
-                if (m) hh = s + (uint64_t)__builtin_ctzll(m);
-            }
-            if (hh != NONE && hh < lim) e = hh;
-        }
-        if (e == NONE && from < lim) {
-            const uint64_t a = g0 + from, b = g0 + lim;
-            for (;;) {
-                const unsigned long long m = __ballot(wv != NONE && (wv & CAND_POS_MASK) >= a);
-                if (m) {
-                    const uint64_t c = readlane64(wv, (uint32_t)__builtin_ctzll(m));
-                    if ((c & CAND_POS_MASK) < b) {
-                        e = (c & CAND_POS_MASK) - g0;
-                        known = (c & CAND_KNOWN) != 0;
-                        cfix = (uint32_t)(c >> 48) & 0xffu;
-                    }
-                    break;
-                }
-                // whole window below a: slide (positions are sorted)
-                const uint64_t last = readlane64(wv, 63);
-                if (last == NONE || wb + 64 >= ncand) break;
-                wb += 64;
-                wv = wb + lane < ncand ? T.cand[wb + lane] : NONE;
-            }
-        }
-        uint64_t cut;                                     // :754-755
-        if (e != NONE) { cut = e + 1; head = known ? 1 : 2; fix = cfix; }
-        else { cut = lim; head = 2; }
-        if (lane == 0 && cnt < cap) {
-            DevCut d;
-            d.offset = s;
-            d.len = (uint32_t)(cut - s);
-            d.file = i;
-            out[cnt] = d;
-        }
-        ++cnt;
-        s = cut;                                          // :771
-        uint64_t rd = MAX - (R - s);                      // :776
-        rd = min(rd, CAP);
-        rd = min(rd, F - R);
-        R += rd;
-    }
-    if (lane == 0) {
-        T.counts[i] = cnt;
-        if (cnt > cap) atomicOr(&T.ctr[CTR_FLAGS], FLAG_CUT_OVERFLOW);
-    }
+    if (F <= 0xFFFFFF00ull)
+        resolve_walk<uint32_t>(data, P, T, i, F, g0, lane);
+    else
+        resolve_walk<uint64_t>(data, P, T, i, F, g0, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1217,7 +1340,7 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
     hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
     hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4), dim3(256), 0, s, t);
     {
-        const uint64_t want = (t.cand_cap + 255) / 256;
+        const uint64_t want = (t.cand_cap + t.ngrid + 255) / 256;
         const uint32_t blocks = (uint32_t)(want < 2048 ? (want ? want : 1) : 2048);
         hipLaunchKernelGGL(cdc_fix_kernel, dim3(blocks), dim3(256), 0, s, d, p, t);
     }
