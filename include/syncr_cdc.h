@@ -38,6 +38,7 @@ extern "C" {
 #define SYNCR_CDC_ENODEV (-19) /* no such HIP device / HIP runtime unavailable   */
 #define SYNCR_CDC_EIO (-5)     /* HIP runtime error while running                 */
 #define SYNCR_CDC_ESTATE (-71) /* call out of order (e.g. launch before plan)    */
+#define SYNCR_CDC_ENOENT (-2)  /* chunk cache: no valid entry                     */
 
 /* Chunker parameters.  Defaults mirror src/chunking.rs:7-13 and the production
  * read path of file_operations.rs:737-776. */
@@ -171,6 +172,27 @@ int32_t syncr_ingest_flush(syncr_ingest *g);
 /* [files, bytes, batches, chunks] so far */
 int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4);
 void syncr_ingest_close(syncr_ingest *g);
+
+/* --- chunk cache (skip re-chunking unchanged files) ---------------------------
+ * Restates ChildCache (src/cache.rs:138-260): one entry per key (file path) with
+ * the file's mtime, size and ChunkInfo list; valid when mtime (cache.rs:167-179)
+ * and size both match.  Persistent in an append-only log at `path` (NULL = in
+ * memory only); a torn tail is dropped on open.  get: 0 on a hit,
+ * SYNCR_CDC_ENOENT on a miss, SYNCR_CDC_ERANGE (n_out = needed) if cap is short.
+ * Attached to an ingest pipeline, submit_file serves unchanged files from it and
+ * stores every freshly chunked file in it. */
+typedef struct syncr_cache syncr_cache;
+int32_t syncr_cache_open(const char *path, syncr_cache **out);
+int32_t syncr_cache_get(syncr_cache *c, const char *key, uint32_t mtime, uint64_t size, syncr_chunk_info *out,
+                        uint64_t cap, uint64_t *n_out);
+int32_t syncr_cache_put(syncr_cache *c, const char *key, uint32_t mtime, uint64_t size,
+                        const syncr_chunk_info *chunks, uint64_t n);
+int32_t syncr_cache_sync(syncr_cache *c);
+/* [hits, misses, puts, entries] */
+int32_t syncr_cache_stats(syncr_cache *c, uint64_t *stats4);
+void syncr_cache_close(syncr_cache *c);
+int32_t syncr_ingest_set_cache(syncr_ingest *g, syncr_cache *c);
+int32_t syncr_ingest_cache_hits(const syncr_ingest *g, uint64_t *hits);
 
 /* --- device memory / stream / timing helpers (hosts without a GPU framework) -- */
 int32_t syncr_cdc_device_alloc(syncr_cdc *h, uint64_t bytes, void **d_ptr);

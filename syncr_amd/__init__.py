@@ -24,7 +24,7 @@ import numpy as np
 
 __all__ = [
     "CHUNK_BITS", "MAX_CHUNK_SIZE_FACTOR", "MAX_CHUNK_SIZE", "TOKIO_READ_CAP",
-    "ChunkInfo", "Chunker", "Ingest", "SyncrCdcError", "format_chunks", "compute_file_chunks", "chunk_data",
+    "ChunkInfo", "Chunker", "ChunkCache", "Ingest", "SyncrCdcError", "format_chunks", "compute_file_chunks", "chunk_data",
     "library", "library_path", "EXPORTED_SYMBOLS",
 ]
 
@@ -53,10 +53,13 @@ EXPORTED_SYMBOLS = (
     "syncr_cdc_format_chunks",
     "syncr_ingest_open", "syncr_ingest_submit", "syncr_ingest_submit_file", "syncr_ingest_reserve",
     "syncr_ingest_commit", "syncr_ingest_flush", "syncr_ingest_stats", "syncr_ingest_close",
+    "syncr_cache_open", "syncr_cache_get", "syncr_cache_put", "syncr_cache_sync", "syncr_cache_stats",
+    "syncr_cache_close", "syncr_ingest_set_cache", "syncr_ingest_cache_hits",
 )
 
 ABI_VERSION = 2
 E_RANGE = -34
+E_NOENT = -2
 FMT_LIST_LINES = 1      # LIST reply "C" lines (src/protocol/v3_server.rs:146-182)
 FMT_HASHCHUNKS = 2      # profile FileData "ch" array (src/types.rs:117-129)
 
@@ -140,6 +143,14 @@ def library():
             "syncr_ingest_flush": ([_vp], _i32),
             "syncr_ingest_stats": ([_vp, _pu64], _i32),
             "syncr_ingest_close": ([_vp], None),
+            "syncr_cache_open": ([ctypes.c_char_p, ctypes.POINTER(_vp)], _i32),
+            "syncr_cache_get": ([_vp, ctypes.c_char_p, _u32, _u64, _vp, _u64, _pu64], _i32),
+            "syncr_cache_put": ([_vp, ctypes.c_char_p, _u32, _u64, _vp, _u64], _i32),
+            "syncr_cache_sync": ([_vp], _i32),
+            "syncr_cache_stats": ([_vp, _pu64], _i32),
+            "syncr_cache_close": ([_vp], None),
+            "syncr_ingest_set_cache": ([_vp, _vp], _i32),
+            "syncr_ingest_cache_hits": ([_vp, _pu64], _i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -370,6 +381,68 @@ def format_chunks(chunks: np.ndarray, fmt: int = FMT_LIST_LINES) -> bytes:
     return buf.raw[: int(n.value)]
 
 
+class ChunkCache:
+    """Persistent chunk cache (syncr_cache_*), the reference's ChildCache
+    (src/cache.rs:138-260): per key (file path) the file's mtime, size and
+    ChunkInfo list; valid when mtime (cache.rs:175) and size match.  Host code:
+    works without a GPU."""
+
+    def __init__(self, path: Optional[str] = None):
+        h = _vp()
+        _check(library().syncr_cache_open(os.fsencode(path) if path else None, ctypes.byref(h)), "syncr_cache_open")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def get(self, key: str, mtime: int, size: int) -> Optional[np.ndarray]:
+        L = library()
+        n = ctypes.c_uint64(0)
+        k = os.fsencode(key)
+        rc = L.syncr_cache_get(self._h, k, mtime, size, None, 0, ctypes.byref(n))
+        if rc == E_NOENT:
+            return None
+        if rc == 0:                          # a hit with no chunks (an empty file)
+            return np.zeros(0, CHUNK_INFO_DTYPE)
+        if rc != E_RANGE:
+            _check(rc, "syncr_cache_get")
+        out = np.zeros(max(int(n.value), 1), CHUNK_INFO_DTYPE)
+        _check(L.syncr_cache_get(self._h, k, mtime, size, out.ctypes.data, out.size, ctypes.byref(n)),
+               "syncr_cache_get")
+        return out[: int(n.value)]
+
+    def put(self, key: str, mtime: int, size: int, chunks: np.ndarray) -> None:
+        a = np.ascontiguousarray(chunks, dtype=CHUNK_INFO_DTYPE)
+        _check(library().syncr_cache_put(self._h, os.fsencode(key), mtime, size, a.ctypes.data if a.size else None,
+                                         a.size), "syncr_cache_put")
+
+    def sync(self) -> None:
+        _check(library().syncr_cache_sync(self._h), "syncr_cache_sync")
+
+    def stats(self) -> dict:
+        st = (ctypes.c_uint64 * 4)()
+        _check(library().syncr_cache_stats(self._h, st), "syncr_cache_stats")
+        return {"hits": st[0], "misses": st[1], "puts": st[2], "entries": st[3]}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            library().syncr_cache_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Ingest:
     """Batched ingest pipeline (syncr_ingest_*): the directory walk of
     traverse_and_stream (file_operations.rs:544-715) without its serial
@@ -380,7 +453,7 @@ class Ingest:
 
     def __init__(self, chunk_bits: int = CHUNK_BITS, max_chunk: int = MAX_CHUNK_SIZE,
                  read_cap: int = TOKIO_READ_CAP, device: int = 0, batch_bytes: int = 256 << 20,
-                 depth: int = 3, copy_threads: int = 8, on_file=None):
+                 depth: int = 3, copy_threads: int = 8, on_file=None, cache: Optional["ChunkCache"] = None):
         L = library()
         self.params = Params(chunk_bits, 0, max_chunk, read_cap)
         self.results: list[tuple[int, int, np.ndarray]] = []
@@ -400,6 +473,9 @@ class Ingest:
         _check(L.syncr_ingest_open(device, ctypes.byref(self.params), batch_bytes, depth, copy_threads,
                                    self._cb, None, ctypes.byref(h)), "syncr_ingest_open")
         self._h = h
+        self._cache = cache                  # keep alive while attached
+        if cache is not None:
+            _check(L.syncr_ingest_set_cache(h, cache.handle), "syncr_ingest_set_cache")
 
     def submit(self, data, tag: int) -> None:
         a = _u8(data)
@@ -426,7 +502,9 @@ class Ingest:
     def stats(self) -> dict:
         st = (ctypes.c_uint64 * 4)()
         _check(library().syncr_ingest_stats(self._h, st), "syncr_ingest_stats")
-        return {"files": st[0], "bytes": st[1], "batches": st[2], "chunks": st[3]}
+        hits = ctypes.c_uint64(0)
+        _check(library().syncr_ingest_cache_hits(self._h, ctypes.byref(hits)), "syncr_ingest_cache_hits")
+        return {"files": st[0], "bytes": st[1], "batches": st[2], "chunks": st[3], "cache_hits": hits.value}
 
     def close(self) -> None:
         if getattr(self, "_h", None):

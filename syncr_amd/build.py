@@ -10,7 +10,8 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libsyncr_cdc.so")
 SOURCES = [os.path.join(CSRC, "cdc_kernels.hip"), os.path.join(CSRC, "b3_kernels.hip"),
-           os.path.join(CSRC, "cdc_api.cpp"), os.path.join(CSRC, "ingest.cpp")]
+           os.path.join(CSRC, "cdc_api.cpp"), os.path.join(CSRC, "ingest.cpp"),
+           os.path.join(CSRC, "cache.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, "cdc_internal.h"), os.path.join(ROOT, "include", "syncr_cdc.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SYNCR_CDC_ARCH", "gfx950")

@@ -299,6 +299,7 @@ const char *syncr_cdc_strerror(int32_t code) {
         case SYNCR_CDC_ENODEV: return "no HIP device";
         case SYNCR_CDC_EIO: return "HIP runtime error";
         case SYNCR_CDC_ESTATE: return "call out of order";
+        case SYNCR_CDC_ENOENT: return "no such entry";
         default: return "unknown error";
     }
 }

@@ -23,6 +23,7 @@
 #include <functional>
 #include <mutex>
 #include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -110,6 +111,14 @@ struct Slot {
     uint64_t cap = 0, used = 0;
     std::vector<uint64_t> off, len, tag;
     std::vector<int32_t> status;
+    // chunk cache: per file, the key to store the result under ("" = none) and
+    // its (mtime, size); a cache hit carries its chunks in cbuf[cstart, +ccount)
+    std::vector<std::string> key;
+    std::vector<uint32_t> mtime;
+    std::vector<uint64_t> fsize;
+    std::vector<uint8_t> hit;
+    std::vector<uint64_t> cstart, ccount;
+    std::vector<syncr_chunk_info> cbuf;
     bool inflight = false;
     std::vector<syncr_chunk_info> out;
     std::vector<uint64_t> counts;
@@ -133,6 +142,8 @@ struct syncr_ingest {
     uint64_t reserved_len = 0;
     uint64_t stats[4] = {0, 0, 0, 0};   // files, bytes, batches, chunks
     int32_t error = 0;                  // sticky engine error
+    syncr_cache *cache = nullptr;       // optional (syncr_ingest_set_cache)
+    uint64_t cache_hits = 0;
 };
 
 namespace {
@@ -195,9 +206,19 @@ int32_t complete(syncr_ingest *g, Slot &s) {
     }
     uint64_t o = 0;
     for (uint32_t i = 0; i < nf; i++) {
-        const uint64_t c = s.status[i] ? 0 : s.counts[i];
-        for (uint64_t k = 0; k < c; k++) s.out[o + k].file = 0;   // one file per callback
-        if (g->cb) g->cb(g->ctx, s.tag[i], s.status[i], c ? s.out.data() + o : nullptr, c);
+        const syncr_chunk_info *ci;
+        uint64_t c;
+        if (s.hit[i]) {                                       // served by the chunk cache
+            c = s.ccount[i];
+            ci = c ? s.cbuf.data() + s.cstart[i] : nullptr;
+        } else {
+            c = s.status[i] ? 0 : s.counts[i];
+            for (uint64_t k = 0; k < c; k++) s.out[o + k].file = 0;   // one file per callback
+            ci = c ? s.out.data() + o : nullptr;
+            if (g->cache && !s.status[i] && !s.key[i].empty())
+                (void)syncr_cache_put(g->cache, s.key[i].c_str(), s.mtime[i], s.fsize[i], ci, c);
+        }
+        if (g->cb) g->cb(g->ctx, s.tag[i], s.status[i], ci, c);
         o += s.counts[i];
         g->stats[3] += c;
     }
@@ -205,6 +226,13 @@ int32_t complete(syncr_ingest *g, Slot &s) {
     s.len.clear();
     s.tag.clear();
     s.status.clear();
+    s.key.clear();
+    s.mtime.clear();
+    s.fsize.clear();
+    s.hit.clear();
+    s.cstart.clear();
+    s.ccount.clear();
+    s.cbuf.clear();
     s.used = 0;
     return SYNCR_CDC_OK;
 }
@@ -238,11 +266,18 @@ int32_t room(syncr_ingest *g, uint64_t len) {
     return SYNCR_CDC_OK;
 }
 
-void record(Slot &s, uint64_t len, uint64_t tag, int32_t status) {
+void record(Slot &s, uint64_t len, uint64_t tag, int32_t status, const char *key = nullptr,
+            uint32_t mtime = 0, uint64_t fsize = 0) {
     s.off.push_back(s.used);
     s.len.push_back(status ? 0 : len);
     s.tag.push_back(tag);
     s.status.push_back(status);
+    s.key.emplace_back(key ? key : "");
+    s.mtime.push_back(mtime);
+    s.fsize.push_back(fsize);
+    s.hit.push_back(0);
+    s.cstart.push_back(0);
+    s.ccount.push_back(0);
     if (!status) s.used += len;
 }
 
@@ -330,6 +365,30 @@ int32_t syncr_ingest_submit_file(syncr_ingest *g, const char *path, uint64_t tag
         return SYNCR_CDC_OK;
     }
     const uint64_t len = (uint64_t)st.st_size;
+    const uint32_t mt = (uint32_t)st.st_mtime;                // meta.mtime() as u32 (file_operations.rs:615)
+    if (g->cache) {                                           // unchanged file: cached ChunkInfo list
+        uint64_t n = 0;
+        std::vector<syncr_chunk_info> tmp;
+        int32_t rc = syncr_cache_get(g->cache, path, mt, len, nullptr, 0, &n);   // OK here: no chunks
+        if (rc == SYNCR_CDC_ERANGE) {
+            tmp.resize(n);
+            rc = syncr_cache_get(g->cache, path, mt, len, tmp.data(), n, &n);
+        }
+        if (rc == SYNCR_CDC_OK) {
+            close(fd);
+            rc = room(g, 0);
+            if (rc) return rc;
+            Slot &s = g->slots[g->cur];
+            record(s, 0, tag, 0);
+            s.hit.back() = 1;
+            s.cstart.back() = s.cbuf.size();
+            s.ccount.back() = n;
+            s.cbuf.insert(s.cbuf.end(), tmp.begin(), tmp.end());
+            g->stats[0]++;
+            g->cache_hits++;
+            return SYNCR_CDC_OK;
+        }
+    }
     uint8_t *dst = nullptr;
     int32_t rc = syncr_ingest_reserve(g, len, &dst);
     if (rc) {
@@ -369,10 +428,16 @@ int32_t syncr_ingest_submit_file(syncr_ingest *g, const char *path, uint64_t tag
     if (err) {                                       // file_operations.rs:740-743: empty list
         record(g->slots[g->cur], 0, tag, -err);
     } else {
-        record(g->slots[g->cur], len, tag, 0);
+        record(g->slots[g->cur], len, tag, 0, g->cache ? path : nullptr, mt, len);
         g->stats[1] += len;
     }
     g->stats[0]++;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_ingest_set_cache(syncr_ingest *g, syncr_cache *c) {
+    if (!g) return SYNCR_CDC_EINVAL;
+    g->cache = c;
     return SYNCR_CDC_OK;
 }
 
@@ -395,6 +460,12 @@ int32_t syncr_ingest_flush(syncr_ingest *g) {
 int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4) {
     if (!g || !stats4) return SYNCR_CDC_EINVAL;
     for (int k = 0; k < 4; k++) stats4[k] = g->stats[k];
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_ingest_cache_hits(const syncr_ingest *g, uint64_t *hits) {
+    if (!g || !hits) return SYNCR_CDC_EINVAL;
+    *hits = g->cache_hits;
     return SYNCR_CDC_OK;
 }
 

@@ -23,7 +23,7 @@ def lib():
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(syncr_(?:cdc|ingest)_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(syncr_(?:cdc|ingest|cache)_\w+)\s*\(", src)))
 
 
 def test_header_matches_python_binding():
@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(lib):
     import syncr_amd
     out = subprocess.run(["nm", "-D", "--defined-only", syncr_amd.library_path],
                          capture_output=True, text=True, check=True).stdout
-    exported = set(re.findall(r"\bT (syncr_(?:cdc|ingest)_\w+)", out))
+    exported = set(re.findall(r"\bT (syncr_(?:cdc|ingest|cache)_\w+)", out))
     missing = [s for s in declared_functions() if s not in exported]
     assert not missing, missing
     for s in declared_functions():

@@ -98,3 +98,46 @@ def test_flush_is_repeatable():
         g.flush()
         res = g.results
     check(res, files)
+
+
+def test_chunk_cache_skips_unchanged_files(tmp_path):
+    """src/cache.rs:183-203 wired into the walk: a second pass over unchanged
+    files is served from the cache (identical ChunkInfo lists); a modified file
+    (new mtime) is re-chunked; the cache persists across handles."""
+    import os
+    files = corpus(12, 13, 3 * M)
+    paths = []
+    for i, f in enumerate(files):
+        p = tmp_path / f"f{i}.bin"
+        p.write_bytes(f.tobytes())
+        paths.append(str(p))
+    cpath = str(tmp_path / "chunks.cache")
+
+    def run(cache):
+        res = []
+        with syncr_amd.Ingest(batch_bytes=4 * M, depth=2, cache=cache,
+                              on_file=lambda t, s, a: res.append((t, s, a))) as g:
+            for i, p in enumerate(paths):
+                g.submit_file(p, i)
+            g.flush()
+            return res, g.stats()
+
+    with syncr_amd.ChunkCache(cpath) as c:
+        first, st1 = run(c)
+        assert st1["cache_hits"] == 0
+        check(first, files)
+        second, st2 = run(c)
+        assert st2["cache_hits"] == len(files) and st2["bytes"] == 0
+        for (t1, s1, a1), (t2, s2, a2) in zip(first, second):
+            assert t1 == t2 and s1 == s2 and np.array_equal(a1, a2)
+    # modify one file (content and mtime): only it is re-chunked
+    new = O.xorshift_bytes(777, 2 * M + 5)
+    with open(paths[4], "wb") as fh:
+        fh.write(new.tobytes())
+    st = os.stat(paths[4])
+    os.utime(paths[4], (st.st_atime, st.st_mtime + 10))
+    files[4] = new
+    with syncr_amd.ChunkCache(cpath) as c:                   # reopened from disk
+        third, st3 = run(c)
+    assert st3["cache_hits"] == len(files) - 1
+    check(third, files)
