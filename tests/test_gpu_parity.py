@@ -295,3 +295,66 @@ def test_resolve_variants_agree(kat_cases):
     finally:
         for ch in lanes.values():
             ch.close()
+
+
+def test_dedup_corpus_full_size():
+    """SURVEY §8d config 5 at its full BASELINE size: 1000 variants of one 32 MiB
+    random base, each with one 1-256 byte edit (50 % overwrite, 25 % insert,
+    25 % delete) = ~32 GiB, device-resident, chunked AND hashed: every cut and
+    every BLAKE3 bit-exact vs the oracle; boundary stability vs the base."""
+    rng = np.random.default_rng(20251212)
+    base = O.xorshift_bytes(31337, 32 * M)
+    plan = []
+    for _ in range(1000):
+        pos = int(rng.integers(0, base.size))
+        ln = int(rng.integers(1, 257))
+        kind = ("overwrite", "overwrite", "insert", "delete")[int(rng.integers(0, 4))]
+        ins = rng.integers(0, 256, ln, dtype=np.uint8)
+        size = base.size + (ln if kind == "insert" else (-min(ln, base.size - pos) if kind == "delete" else 0))
+        plan.append((kind, pos, ln, ins, size))
+    lens = np.array([p[4] for p in plan], np.uint64)
+    offs = np.zeros_like(lens)
+    offs[1:] = np.cumsum(lens)[:-1]
+    total = int(lens.sum())
+    buf = np.empty(total, np.uint8)
+    edits = []
+    for (kind, pos, ln, ins, size), o in zip(plan, offs.tolist()):
+        f = buf[o:o + size]
+        if kind == "overwrite":
+            f[:] = base
+            k = max(0, min(ln, base.size - pos))
+            f[pos:pos + k] = ins[:k]
+            edits.append((pos, 0))
+        elif kind == "insert":
+            f[:pos] = base[:pos]
+            f[pos:pos + ln] = ins
+            f[pos + ln:] = base[pos:]
+            edits.append((pos, ln))
+        else:
+            d = min(ln, base.size - pos)
+            f[:pos] = base[:pos]
+            f[pos:] = base[pos + d:]
+            edits.append((pos, -d))
+    with syncr_amd.Chunker() as ch:
+        dev = syncr_amd.DeviceBuffer(ch, total)
+        try:
+            dev.upload(buf)
+            ch.plan(offs, lens, total)
+            ch.launch(dev.ptr, hashed=True)
+            got = ch.fetch(hashed=True)
+        finally:
+            dev.free()
+    ref = O.chunk_batch(buf, offs, lens, nthreads=16)
+    base_cuts = set(O.chunk_production(base).tolist())
+    kept, starts, sizes = [], [], []
+    for i in range(lens.size):
+        e = ends_of(got[i])
+        assert e == ref[i].tolist(), i
+        starts.append(got[i]["offset"].astype(np.uint64) + offs[i])
+        sizes.append(got[i]["len"].astype(np.uint64))
+        pos, delta = edits[i]
+        adj = {x - delta if x > pos else x for x in e}
+        kept.append(len(adj & base_cuts) / len(base_cuts))
+    want = O.blake3_batch(buf, np.concatenate(starts), np.concatenate(sizes), nthreads=16)
+    assert np.array_equal(np.concatenate([g["hash"] for g in got]), want)
+    assert np.median(kept) >= 0.9
