@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--file-gib", type=float, default=2.0)
     ap.add_argument("--check-files", type=int, default=200)
+    ap.add_argument("--no-fill", action="store_true",
+                    help="diagnostic: reserve/commit without writing the bytes (pipeline ceiling without the "
+                         "host copy; results are not checked)")
     args = ap.parse_args()
 
     sizes, idx, _ = bench.workload("zipf10k", 1)
@@ -69,12 +72,19 @@ def main():
             counts["files"] = counts["chunks"] = 0
             t0 = time.perf_counter()
             for i, f in enumerate(files):
-                g.submit(f, i)
+                if args.no_fill:
+                    g.reserve(f.size)
+                    g.commit(i)
+                else:
+                    g.submit(f, i)
             g.flush()
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
         out.update({"bytes_mode_s": round(best, 4), "bytes_mode_GiBps": round(span / best / 2**30, 2),
-                    "chunks": counts["chunks"]})
+                    "chunks": counts["chunks"], "no_fill": args.no_fill})
+        if args.no_fill:
+            print(json.dumps(out), flush=True)
+            return
         st = g.stats()
         out["batches_per_pass"] = st["batches"] // args.reps
 
