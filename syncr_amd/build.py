@@ -12,7 +12,7 @@ LIB = os.path.join(PKG, "libsyncr_cdc.so")
 SOURCES = [os.path.join(CSRC, "cdc_kernels.hip"), os.path.join(CSRC, "b3_kernels.hip"),
            os.path.join(CSRC, "cdc_api.cpp"), os.path.join(CSRC, "ingest.cpp"),
            os.path.join(CSRC, "cache.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, "cdc_internal.h"), os.path.join(ROOT, "include", "syncr_cdc.h")]
+DEPS = SOURCES + [os.path.join(CSRC, "cdc_internal.h"), os.path.join(CSRC, "lds_dma.h"), os.path.join(ROOT, "include", "syncr_cdc.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SYNCR_CDC_ARCH", "gfx950")
 

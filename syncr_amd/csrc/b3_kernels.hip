@@ -140,17 +140,22 @@ __device__ __forceinline__ void load_block(const uint8_t *__restrict__ data, uin
             m[4 * i] = v.x; m[4 * i + 1] = v.y; m[4 * i + 2] = v.z; m[4 * i + 3] = v.w;
         }
     } else {                                   // the batch's last bytes: guarded byte loads
+        // one 32-bit limit (no per-byte 64-bit compares: this rare path sets
+        // the kernel's peak register count); the bytes past it are zero
+        const uint32_t lim = (uint32_t)min<uint64_t>(valid, span > p ? span - p : 0ull);
+        const uint8_t *src = data + p;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             uint32_t w = 0;
-            for (int b = 0; b < 4; ++b) {
-                const uint64_t a = p + 4 * k + b;
-                if (a < span && (uint32_t)(4 * k + b) < valid) w |= (uint32_t)data[a] << (8 * b);
-            }
+            for (int b = 0; b < 4; ++b)
+                if ((uint32_t)(4 * k + b) < lim) w |= (uint32_t)src[4 * k + b] << (8 * b);
             m[k] = w;
         }
+        return;
     }
-    if (valid < 64) {
+    // only a task's last block can be partial: a wave-uniform branch keeps the
+    // compiler from if-converting the masking into the full-block path
+    if (__builtin_expect(__ballot(valid < 64) != 0ull, 0)) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int c = (int)valid - 4 * k;
@@ -186,9 +191,11 @@ __device__ __forceinline__ uint32_t ceil_log2(uint32_t t) { return t <= 1 ? 0u :
 // ---------------------------------------------------------------------------
 // One block per 256 files: the block's cuts form one flat list (a block scan
 // of the per-file counts), so every thread has work whatever the file sizes.
-// Packed chunks are appended to their class list; big chunks get group items
-// (slot << 24 | group, contiguous per chunk) and a tree entry {slot, first
-// item}.  Slots are handed out by LDS atomics in two passes (count, then
+// Packed chunks are appended to their class list; a big chunk gets its group
+// items (slot << 24 | group, contiguous per chunk) and a tree entry {slot,
+// first item}.  When its task count T is not a multiple of 64 the last item
+// is a placeholder (B3_TAIL set; skipped by the group loop) and the T % 64
+// tail tasks are a unit in the class list of their size (B3_TAIL | item).  Slots are handed out by LDS atomics in two passes (count, then
 // place) so the global counters see one atomic per list per block.  A file
 // whose cuts overflowed its output slots is skipped (the host re-launches).
 // ---------------------------------------------------------------------------
@@ -234,14 +241,21 @@ __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
                     const uint64_t idx = gbase[c] + li;
                     if (idx < H.packed_cap) H.packed[c * H.packed_cap + idx] = slot;
                 }
-            } else {
-                const uint32_t ng = (tk + 63) / 64;
+            } else {                                     // big chunk: full group items + tail unit
+                const uint32_t tail = tk % 64, ng = tk / 64 + (tail ? 1u : 0u);
                 const uint32_t li = atomicAdd(&cnt[LIST_ITEMS], ng);
                 const uint32_t lt = atomicAdd(&cnt[LIST_TREES], 1u);
+                const uint32_t c = ceil_log2(tail);
+                const uint32_t lp = tail ? atomicAdd(&cnt[c], 1u) : 0u;
                 if (place) {
                     const uint64_t first = gbase[LIST_ITEMS] + li;
                     if (first + ng <= H.items_cap) {
-                        for (uint32_t g = 0; g < ng; ++g) H.items[first + g] = (slot << 24) | g;
+                        for (uint32_t g = 0; g < ng; ++g)   // the tail's entry is a placeholder
+                            H.items[first + g] = (slot << 24) | g | (tail && g + 1 == ng ? B3_TAIL : 0ull);
+                        if (tail) {
+                            const uint64_t idx = gbase[c] + lp;
+                            if (idx < H.packed_cap) H.packed[c * H.packed_cap + idx] = B3_TAIL | (first + ng - 1);
+                        }
                     } else {
                         atomicOr((unsigned long long *)&H.ctr[B3C_FLAGS], 1ull);
                     }
@@ -288,23 +302,25 @@ __global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict_
         bool valid;
         uint64_t slot = 0;
         uint32_t k;              // task index within the chunk
-        uint32_t km, mm;         // merge index / node count of this lane's chunk in this wave
-        uint32_t dmax;           // merge levels: lanes per chunk in this wave (uniform)
-        bool root;               // this wave finishes the chunk's tree
-        uint64_t out_item = 0;
-        if (w < nbig) {                                          // group item of a big chunk
+        uint32_t km, mm;         // merge index / node count of this lane's unit in this wave
+        uint32_t dmax;           // merge levels: lanes per unit in this wave (uniform)
+        bool root;               // this unit is the whole chunk (its merge gets ROOT)
+        const bool group = w < nbig;                             // uniform
+        uint64_t out_item = w;                                   // group item / tail: its gcv slot
+        bool tail = false;
+        uint32_t k0 = 0;                                         // first task of this unit
+        if (group) {                                             // 64 tasks of a big chunk
             const uint64_t code = H.items[w];
+            if (code & B3_TAIL) continue;                        // placeholder: hashed as a packed unit
             slot = code >> 24;
-            const uint32_t g = (uint32_t)code & 0xffffffu;
-            k = g * 64 + (uint32_t)lane;
+            k0 = ((uint32_t)code & 0xffffffu) * 64;
+            k = k0 + (uint32_t)lane;
             km = (uint32_t)lane;
-            const uint32_t t = chunk_tasks(T.cuts[slot].len);
-            mm = min(64u, t - g * 64);
+            mm = 64;
             valid = true;
             dmax = 64;
-            root = false;                                        // t > 64: b3_tree_kernel finishes
-            out_item = w;
-        } else {                                                 // packed chunks
+            root = false;                                        // b3_tree_kernel finishes
+        } else {                                                 // packed units
             uint64_t r = w - nbig;
             int c = B3_CLASSES - 1;
             for (; c > 0; --c) {                                 // uniform
@@ -316,10 +332,21 @@ __global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict_
             k = (uint32_t)lane & ((1u << c) - 1u);
             km = k;
             valid = idx < npk[c];
-            if (valid) slot = H.packed[c * H.packed_cap + idx];
+            if (valid) {
+                const uint64_t code = H.packed[c * H.packed_cap + idx];
+                tail = (code & B3_TAIL) != 0;
+                if (tail) {                                      // T % 64 tail tasks of a big chunk
+                    out_item = code & ~B3_TAIL;
+                    const uint64_t ic = H.items[out_item] & ~B3_TAIL;
+                    slot = ic >> 24;
+                    k0 = ((uint32_t)ic & 0xffffffu) * 64;
+                } else {
+                    slot = code;
+                }
+            }
             mm = 0;
             dmax = 1u << c;
-            root = true;
+            root = !tail;
         }
         uint32_t len = 0;
         uint64_t cstart = 0;
@@ -327,7 +354,10 @@ __global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict_
             const DevCut cu = T.cuts[slot];
             len = cu.len;
             cstart = T.foff[cu.file] + cu.offset;                // batch offset of the chunk
-            if (w >= nbig) mm = chunk_tasks(len);
+            if (!group) {
+                k += k0;
+                mm = chunk_tasks(len) - k0;
+            }
         }
         const uint32_t nleaves = chunk_leaves(len);
         const uint32_t j0 = k * LPL;

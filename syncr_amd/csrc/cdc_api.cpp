@@ -186,8 +186,9 @@ int32_t upload_cut_tables(syncr_cdc *h) {
         acc += h->h_cut_cap[i];
     }
     h->total_cut_cap = acc;
-    // BLAKE3 items: a chunk of len bytes is ceil(leaves / B3_GROUP_LEAVES) items,
-    // so a file needs at most ceil(F / group bytes) + (its cuts) of them
+    // BLAKE3 items: a chunk of len bytes is ceil(leaves / B3_GROUP_LEAVES) items
+    // (the last may be a tail placeholder), so a file needs at most
+    // ceil(F / group bytes) + (its cuts) of them
     const uint64_t gbytes = 1024ull * B3_GROUP_LEAVES;
     uint64_t icap = 0;
     for (uint32_t i = 0; i < h->nfiles; i++) icap += (h->h_flen[i] + gbytes - 1) / gbytes + h->h_cut_cap[i];

@@ -113,23 +113,26 @@ struct Tables {
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------
 // A lane TASK is B3_LANE_LEAVES consecutive 1 KiB leaves of one chunk.  A chunk
-// of T <= 64 tasks is PACKED: class c = ceil(log2 T), 64 >> c such chunks per
-// wave, each in an aligned run of 2^c lanes.  A chunk of T > 64 tasks is split
-// into GROUP items of 64 tasks (one wave each) merged by b3_tree_kernel.
+// of T <= 64 tasks is PACKED: class c = ceil(log2 T), 64 >> c such units per
+// wave, each in an aligned run of 2^c lanes.  A chunk of T > 64 tasks (a BIG
+// chunk) is floor(T / 64) GROUP items of 64 tasks (one wave each) plus, when
+// T % 64 != 0, a TAIL unit of the last T % 64 tasks packed like a small chunk;
+// b3_tree_kernel merges the items' and the tail's subtree CVs.
 constexpr uint32_t B3_LANE_LEAVES = 4;                      // 1 KiB leaves per lane task
 constexpr uint32_t B3_GROUP_LEAVES = 64 * B3_LANE_LEAVES;   // leaves per group item (one wave)
 constexpr int B3_CLASSES = 7;                               // packed classes: <= 1, 2, 4, ..., 64 tasks
+constexpr uint64_t B3_TAIL = 1ull << 63;                  // packed entry: tail unit
 enum { B3C_ITEMS = 0, B3C_TREES = 1, B3C_NEXT = 2, B3C_FLAGS = 3, B3C_PK0 = 4, B3C_WORDS = 4 + B3_CLASSES };
 
 struct HashTables {
     uint64_t *ctr;                 // [B3C_WORDS] (zeroed per hashed launch)
-    uint64_t *items;               // [items_cap] slot << 24 | group (group items of big chunks)
+    uint64_t *items;               // [items_cap] slot << 24 | group (| B3_TAIL: tail placeholder)
     uint64_t items_cap;
-    uint64_t *packed;              // [B3_CLASSES * packed_cap] chunk slots by packed class
-    uint64_t packed_cap;
-    ulonglong2 *trees;             // [trees_cap] {slot, first item} of multi-item chunks
+    uint64_t *packed;              // [B3_CLASSES * packed_cap] by packed class: a chunk slot, or
+    uint64_t packed_cap;           //   B3_TAIL | its placeholder item for a big chunk's tail unit
+    ulonglong2 *trees;             // [trees_cap] {slot, first item} of big chunks
     uint64_t trees_cap;
-    uint32_t *gcv;                 // [items_cap * 8] item chaining values
+    uint32_t *gcv;                 // [items_cap * 8] subtree CV of each item (or tail placeholder)
     uint32_t *hashes;              // [sum cut_cap * 8] BLAKE3 of each cut slot
     uint32_t ablate;               // timing-only (SYNCR_B3_ABLATE): 1 = loads only, 2 = no loads
     uint32_t nt;                   // 1: non-temporal chunk loads (SYNCR_B3_NT)

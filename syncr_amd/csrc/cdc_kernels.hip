@@ -15,6 +15,7 @@
 //   gather), then cdc_resolve_kernel walks compute_file_chunks' loop for each
 //   file (one lane per file) applying MAX_CHUNK_SIZE and the tokio read cap.
 #include "cdc_internal.h"
+#include "lds_dma.h"
 
 namespace cdc {
 
@@ -55,11 +56,6 @@ __device__ __forceinline__ uint32_t min3_lo16(uint32_t a, uint32_t b, uint32_t c
     return __builtin_elementwise_min(__builtin_elementwise_min(x, y), z);
 }
 
-// LDS byte address of a generic pointer into dynamic shared memory.
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
-}
-
 // Scalar (s_load) read of wave-uniform, kernel-invariant metadata.  A vector
 // load here would be waited with vmcnt(0), draining the in-flight tile DMA.
 __device__ __forceinline__ uint64_t sload_u64(const void *p) {
@@ -71,39 +67,6 @@ __device__ __forceinline__ uint64_t sload_u64(const void *p) {
     uint64_t v;
     asm volatile("s_nop 4\n\ts_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(u) : "memory");
     return v;
-}
-
-template <int N> __device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// 16 B per lane, HBM -> LDS (M0 = wave-uniform LDS base; lane l lands at +16*l).
-// Written as inline asm so hipcc does not drain it with vmcnt(0) before the
-// ds_reads of the OTHER buffer; completion is tracked by hand (wait_vmcnt).
-template <bool NT>
-__device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds) {
-    uint32_t keep;
-    if constexpr (NT)
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %2\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, off nt\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(gsrc), "s"(lds)
-            : "memory");
-    else
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %2\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, off\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(gsrc), "s"(lds)
-            : "memory");
 }
 
 // ---------------------------------------------------------------------------
