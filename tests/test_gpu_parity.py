@@ -218,6 +218,34 @@ def test_zipf_corpus_full_size(chunkers):
 
 
 @pytest.mark.slow
+def test_single_file_over_4gib(chunkers):
+    """One 5 GiB file (the reference's offsets are u64: file_operations.rs:721-788):
+    the resolve walk's 64-bit path, cut offsets past 2^32 and the hash kernels'
+    64-bit chunk starts, in both modes, vs the oracle; hashes vs the BLAKE3 oracle."""
+    n = 5 << 30
+    lens = np.array([n], np.uint64)
+    offs = np.zeros(1, np.uint64)
+    for cap in (2 << 20, 0):
+        ch = chunkers(20, 16 << 20, cap)
+        buf = syncr_amd.DeviceBuffer(ch, n)
+        try:
+            buf.gen_corpus(offs, lens)
+            ch.plan(offs, lens, n)
+            ch.launch(buf.ptr, hashed=True)
+            res = ch.fetch(hashed=True)[0]
+            host = buf.download(n)
+        finally:
+            buf.free()
+        ref = O.chunk_batch(host, offs, lens, read_cap=cap,
+                            mode=O.MODE_PRODUCTION if cap else O.MODE_IDEAL)[0]
+        assert ends_of(res) == ref.tolist()
+        assert int(res["offset"][-1]) > (1 << 32)
+        want = O.blake3_batch(host, res["offset"].astype(np.uint64), res["len"].astype(np.uint64), nthreads=8)
+        assert np.array_equal(res["hash"], want)
+        del host
+
+
+@pytest.mark.slow
 def test_dedup_corpus(chunkers):
     """SURVEY §8d config 5 (scaled to 200 variants of a 32 MiB base): bit-exact
     and boundary-stable (most base cuts survive a small edit, shift-adjusted)."""
