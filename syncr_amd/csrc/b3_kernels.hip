@@ -26,6 +26,7 @@
 // Compute bound: 7 rounds x 8 G x 12 integer ops per 64-byte block
 // (~10.5 VALU ops per byte); the 1 byte/byte HBM read is not the limit.
 #include "cdc_internal.h"
+#include "lds_dma.h"
 
 namespace cdc {
 
@@ -277,15 +278,136 @@ __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
 }
 
 // ---------------------------------------------------------------------------
+// Cooperative block loader (COOP): the wave steps through block index t in
+// lockstep (t < wave max of the tasks' block counts).  Block t+1 of all 64
+// tasks is fetched by four global_load_lds_dwordx4: instruction i moves one
+// 16-byte piece of each of tasks 16i..16i+15, so every instruction reads 16
+// contiguous 64-byte runs instead of 64 scattered 16-byte pieces.  Task q's
+// block lands at slot + 64 q with its pieces rotated by (q >> 2) & 3, which
+// makes the owner's four ds_read_b128 bank-conflict free.  Bytes past the
+// chunk (a task's last block) are zeroed by the owner; pieces that would read
+// past the batch end are not DMA'd but loaded byte by byte by the owner.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <bool NT, int ABLATE>
+__device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ data, uint64_t span, uint32_t stage,
+                                                 uint32_t *stage_ptr, int lane, bool act, uint64_t tp,
+                                                 uint32_t nbytes, uint32_t nblk, uint32_t nl, uint32_t nleaves,
+                                                 uint32_t j0, bool task_root, uint32_t x[8]) {
+    // leaf CVs are folded as they complete (left-balanced pairing of <= 4
+    // leaves): x = leaf 0, then node(0,1); y = leaf 2, then node(2,3)
+    uint32_t y[8];
+    // piece at task byte ps (multiple of 16) is DMA'd iff ps < plim: inside the
+    // chunk's task and 16 bytes inside the batch
+    const uint32_t plim = act ? (uint32_t)min<uint64_t>(nbytes, span >= tp + 16 ? span - tp - 15 : 0ull) : 0u;
+    uint32_t tmax = nblk;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tmax = max(tmax, (uint32_t)__shfl_xor((int)tmax, o));
+    tmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)tmax);
+    // the piece sources are re-derived from the owners' registers at every
+    // issue (ds_bpermute): holding four 64-bit sources and limits across the
+    // compression cost 5 -> 4 waves/SIMD
+    auto issue = [&](uint32_t t) {
+        // opaque copies: keep the shuffles here instead of hoisted out of the loop
+        uint32_t tl = (uint32_t)tp, th = (uint32_t)(tp >> 32), pl = plim;
+        asm volatile("" : "+v"(tl), "+v"(th), "+v"(pl));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = 16 * i + (lane >> 2);
+            const uint32_t pc = ((uint32_t)lane & 3u) ^ (((uint32_t)q >> 2) & 3u);   // piece this lane moves
+            const uint32_t ps = t * 64u + pc * 16u;
+            const uint32_t l = (uint32_t)__shfl((int)pl, q);
+            const uint64_t src = ((uint64_t)(uint32_t)__shfl((int)th, q) << 32) | (uint32_t)__shfl((int)tl, q);
+            if (ps < l) dma16<NT>(data + src + ps, stage + (uint32_t)i * 1024u);
+        }
+    };
+    const uint32_t rot = ((uint32_t)lane >> 2) & 3u;
+    uint8_t *mine = (uint8_t *)stage_ptr + lane * 64;
+    if (ABLATE != 2 && tmax) issue(0);
+#pragma unroll
+    for (uint32_t jj = 0; jj < B3_LANE_LEAVES; ++jj) {
+        if (16 * jj < tmax) {                                    // uniform
+            uint32_t cv[8];
+            set_iv(cv);
+            const uint32_t lbu = min(16u, tmax - 16 * jj);             // uniform blocks of this leaf
+            const uint32_t lb = nblk > 16 * jj ? min(16u, nblk - 16 * jj) : 0u;   // this lane's
+            for (uint32_t b = 0; b < lbu; ++b) {
+                const uint32_t t = 16 * jj + b;
+                const uint32_t off = t * 64;
+                const uint32_t vb = nbytes > off ? min(64u, nbytes - off) : 0u;
+                uint32_t m[16];
+                if constexpr (ABLATE == 2) {               // timing only: no loads
+    #pragma unroll
+                    for (int q = 0; q < 16; ++q) m[q] = (uint32_t)lane * 0x9E3779B9u + q + off;
+                } else {
+                    wait_vmcnt<0>();                                    // block t has landed
+                    // bytes of my block that are past the chunk or were not DMA'd
+                    const uint32_t dma_end = plim > off ? min(64u, (plim - off + 15u) & ~15u) : 0u;
+                    const uint32_t fix = min(vb, dma_end);
+                    if (__builtin_expect(__ballot(b < lb && fix < 64u) != 0ull, 0)) {
+                        if (b < lb) {
+    #pragma unroll 1
+                            for (uint32_t q = fix; q < 64u; ++q) {
+                                const uint8_t v = q < vb ? data[tp + off + q] : (uint8_t)0;
+                                mine[(((q >> 4) ^ rot) << 4) | (q & 15u)] = v;
+                            }
+                        }
+                    }
+    #pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint4 v = *(const uint4 *)(mine + ((((uint32_t)i) ^ rot) << 4));
+                        m[4 * i] = v.x; m[4 * i + 1] = v.y; m[4 * i + 2] = v.z; m[4 * i + 3] = v.w;
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // slot free for block t+1
+                    if (t + 1 < tmax) issue(t + 1);
+                }
+                if (b < lb) {
+                    uint32_t fl = (b == 0 ? B3_START : 0u) | (b + 1 == lb ? B3_END : 0u);
+                    if (b + 1 == lb && nleaves == 1) fl |= B3_ROOT;
+                    if constexpr (ABLATE == 1) {           // timing only: loads, no compression
+    #pragma unroll
+                        for (int q = 0; q < 8; ++q) cv[q] ^= m[q] + m[q + 8] + fl;
+                    } else {
+                        compress(cv, m, j0 + jj, vb, fl);
+                    }
+                }
+            }
+            if (jj < nl) {
+                if (jj == 0) {
+    #pragma unroll
+                    for (int q = 0; q < 8; ++q) x[q] = cv[q];
+                } else if (jj == 1) {
+                    parent(x, cv, (task_root && nl == 2) ? B3_ROOT : 0u);
+                } else if (jj == 2) {
+    #pragma unroll
+                    for (int q = 0; q < 8; ++q) y[q] = cv[q];
+                } else {
+                    parent(y, cv, 0u);
+                }
+            }
+        }
+    }
+    if (nl > 2) parent(x, y, task_root ? B3_ROOT : 0u);
+}
+
+// ---------------------------------------------------------------------------
 // Persistent waves pull wave items: the group items of big chunks first, then
 // the packed classes 6..0.  Per lane: a chunk slot, its task k (leaves
 // LPL*k .. LPL*k+LPL-1) and the merge geometry of that chunk within the wave.
 // ---------------------------------------------------------------------------
-template <bool NT, int ABLATE>
-__global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict__ data, Tables T,
-                                                      HashTables H) {
+template <bool NT, int ABLATE, bool COOP>
+__device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, const Tables &T,
+                                             const HashTables &H) {
     constexpr uint32_t LPL = B3_LANE_LEAVES;
     const int lane = threadIdx.x & 63;
+    // COOP: per-wave staging slot for the cooperative block loader (4 KiB)
+    __shared__ __attribute__((aligned(16))) uint32_t stage_mem[COOP ? 4 * 1024 : 1];
+    uint32_t *stage_ptr = stage_mem + (COOP ? (threadIdx.x >> 6) * 1024 : 0);
+    const uint32_t stage = (uint32_t)__builtin_amdgcn_readfirstlane(lds_addr(stage_ptr));
     const uint64_t nbig = min(H.ctr[B3C_ITEMS], H.items_cap);
     uint64_t npk[B3_CLASSES], total = nbig;
 #pragma unroll
@@ -366,64 +488,67 @@ __global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict_
         const uint32_t nbytes = act ? (uint32_t)min<uint64_t>(1024ull * LPL, len - lane_off) : 0u;
         const uint32_t nblk = act ? (nbytes ? (nbytes + 63) >> 6 : 1u) : 0u;
         const uint32_t nl = (nblk + 15) >> 4;                    // leaves of this task
-        uint32_t lc[LPL][8];                                     // leaf CVs
-        // block t of the task (t < nblk) is at task offset 64*t; the next
-        // block's loads are issued before the current block is compressed
-        auto fetch = [&](uint32_t t, uint32_t m[16]) {
-            const uint32_t off = t * 64;
-            const uint32_t vb = nbytes > off ? min(64u, nbytes - off) : 0u;
-            if constexpr (ABLATE == 2) {               // timing only: no loads
-#pragma unroll
-                for (int q = 0; q < 16; ++q) m[q] = (uint32_t)lane * 0x9E3779B9u + q + off;
-            } else {
-                load_block<NT>(data, T.span, cstart + lane_off + off, vb, m);
-            }
-        };
-        uint32_t m[16];
-        if (nblk) fetch(0, m);
-#pragma unroll
-        for (uint32_t jj = 0; jj < LPL; ++jj) {
-            if (jj >= nl) continue;
-            uint32_t cv[8];
-            set_iv(cv);
-            const uint32_t tb = jj * 16;
-            const uint32_t lb = min(16u, nblk - tb);               // blocks of this leaf
-            for (uint32_t b = 0; b < lb; ++b) {
-                const uint32_t t = tb + b;
-                uint32_t mn[16];
-                const bool more = t + 1 < nblk;
-                if (more) fetch(t + 1, mn);
+        const bool task_root = root && mm == 1;                  // the task is the whole chunk
+        uint32_t x[8];
+        if constexpr (COOP) {
+            leaf_blocks_coop<NT, ABLATE>(data, T.span, stage, stage_ptr, lane, act, cstart + lane_off, nbytes,
+                                         nblk, nl, nleaves, j0, task_root, x);
+        } else {
+            uint32_t lc[LPL][8];                                 // leaf CVs
+            // block t of the task (t < nblk) is at task offset 64*t; the next
+            // block's loads are issued before the current block is compressed
+            auto fetch = [&](uint32_t t, uint32_t m[16]) {
                 const uint32_t off = t * 64;
                 const uint32_t vb = nbytes > off ? min(64u, nbytes - off) : 0u;
-                uint32_t fl = (b == 0 ? B3_START : 0u) | (b + 1 == lb ? B3_END : 0u);
-                if (b + 1 == lb && nleaves == 1) fl |= B3_ROOT;
-                if constexpr (ABLATE == 1) {           // timing only: loads, no compression
+                if constexpr (ABLATE == 2) {               // timing only: no loads
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) cv[q] ^= m[q] + m[q + 8] + fl;
+                    for (int q = 0; q < 16; ++q) m[q] = (uint32_t)lane * 0x9E3779B9u + q + off;
                 } else {
-                    compress(cv, m, j0 + jj, vb, fl);
+                    load_block<NT>(data, T.span, cstart + lane_off + off, vb, m);
                 }
-                if (more) {
+            };
+            uint32_t m[16];
+            if (nblk) fetch(0, m);
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) m[q] = mn[q];
+            for (uint32_t jj = 0; jj < LPL; ++jj) {
+                if (jj >= nl) continue;
+                uint32_t cv[8];
+                set_iv(cv);
+                const uint32_t tb = jj * 16;
+                const uint32_t lb = min(16u, nblk - tb);               // blocks of this leaf
+                for (uint32_t b = 0; b < lb; ++b) {
+                    const uint32_t t = tb + b;
+                    uint32_t mn[16];
+                    const bool more = t + 1 < nblk;
+                    if (more) fetch(t + 1, mn);
+                    const uint32_t off = t * 64;
+                    const uint32_t vb = nbytes > off ? min(64u, nbytes - off) : 0u;
+                    uint32_t fl = (b == 0 ? B3_START : 0u) | (b + 1 == lb ? B3_END : 0u);
+                    if (b + 1 == lb && nleaves == 1) fl |= B3_ROOT;
+                    if constexpr (ABLATE == 1) {           // timing only: loads, no compression
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) cv[q] ^= m[q] + m[q + 8] + fl;
+                    } else {
+                        compress(cv, m, j0 + jj, vb, fl);
+                    }
+                    if (more) {
+#pragma unroll
+                        for (int q = 0; q < 16; ++q) m[q] = mn[q];
+                    }
                 }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) lc[jj][q] = cv[q];
             }
+            // fold the task's leaves (left-balanced level pairing); ROOT when the
+            // task is the whole chunk.
 #pragma unroll
-            for (int q = 0; q < 8; ++q) lc[jj][q] = cv[q];
+            for (uint32_t d = 1; d < LPL; d <<= 1)
+#pragma unroll
+                for (uint32_t i = 0; i + d < LPL; i += 2 * d)
+                    if (i + d < nl) parent(lc[i], lc[i + d], (task_root && nl <= 2 * d) ? B3_ROOT : 0u);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) x[q] = lc[0][q];
         }
-        // fold the task's leaves (left-balanced level pairing); ROOT when the
-        // task is the whole chunk.  (A cooperative variant -- 4 lanes load one
-        // task's 64 contiguous bytes, LDS transpose -- cut the load-only time
-        // 4.5 -> 3.6 ms but cost a wave per SIMD and was slower overall.)
-        const bool task_root = root && mm == 1;
-#pragma unroll
-        for (uint32_t d = 1; d < LPL; d <<= 1)
-#pragma unroll
-            for (uint32_t i = 0; i + d < LPL; i += 2 * d)
-                if (i + d < nl) parent(lc[i], lc[i + d], (task_root && nl <= 2 * d) ? B3_ROOT : 0u);
-        uint32_t x[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) x[q] = lc[0][q];
         // merge the tasks of each chunk (runs of 2^c lanes, or the 64 lanes of a group)
 #pragma unroll
         for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -481,16 +606,34 @@ __global__ __launch_bounds__(256) void b3_tree_kernel(Tables T, HashTables H) {
     }
 }
 
-template <bool NT, int AB>
+template <bool NT, int ABLATE, bool COOP>
+__global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict__ data, Tables T, HashTables H) {
+    b3_leaf_body<NT, ABLATE, COOP>(data, T, H);
+}
+
+template <bool NT, int AB, bool CO>
 static void launch_leaf(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
         cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)&b3_leaf_kernel<NT, AB>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)&b3_leaf_kernel<NT, AB, CO>, 256, 0) !=
             hipSuccess ||
         per <= 0)
         per = 1;
-    hipLaunchKernelGGL((b3_leaf_kernel<NT, AB>), dim3((uint32_t)(cus * per)), dim3(256), 0, s, d, t, ht);
+    hipLaunchKernelGGL((b3_leaf_kernel<NT, AB, CO>), dim3((uint32_t)(cus * per)), dim3(256), 0, s, d, t, ht);
+}
+
+template <bool CO>
+static hipError_t launch_leaf_v(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
+    switch (ht.ablate * 2 + (ht.nt ? 1 : 0)) {
+        case 0: launch_leaf<false, 0, CO>(device, d, t, ht, s); break;
+        case 1: launch_leaf<true, 0, CO>(device, d, t, ht, s); break;
+        case 2: launch_leaf<false, 1, CO>(device, d, t, ht, s); break;
+        case 3: launch_leaf<true, 1, CO>(device, d, t, ht, s); break;
+        case 4: case 5: launch_leaf<true, 2, CO>(device, d, t, ht, s); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
@@ -498,14 +641,8 @@ hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const Hash
     if (e != hipSuccess) return e;
     if (!t.nfiles) return hipSuccess;
     hipLaunchKernelGGL(b3_items_kernel, dim3((t.nfiles + 255) / 256), dim3(256), 0, s, t, ht);
-    switch (ht.ablate * 2 + (ht.nt ? 1 : 0)) {
-        case 0: launch_leaf<false, 0>(device, d, t, ht, s); break;
-        case 1: launch_leaf<true, 0>(device, d, t, ht, s); break;
-        case 2: launch_leaf<false, 1>(device, d, t, ht, s); break;
-        case 3: launch_leaf<true, 1>(device, d, t, ht, s); break;
-        case 4: case 5: launch_leaf<true, 2>(device, d, t, ht, s); break;
-        default: return hipErrorInvalidValue;
-    }
+    e = ht.coop ? launch_leaf_v<true>(device, d, t, ht, s) : launch_leaf_v<false>(device, d, t, ht, s);
+    if (e != hipSuccess) return e;
     const uint64_t want = (ht.trees_cap + 3) / 4;
     const uint32_t blocks = (uint32_t)(want < 4096 ? (want ? want : 1) : 4096);
     hipLaunchKernelGGL(b3_tree_kernel, dim3(blocks), dim3(256), 0, s, t, ht);

@@ -72,7 +72,7 @@ struct syncr_cdc {
         dense_list, dense_cnt, dense_bits, super_off, cand, cuts, counts;
     // BLAKE3 of every chunk (launch_hashed)
     bool hash_on = false;
-    uint32_t b3_ablate = 0, b3_nt = 0;
+    uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 1;
     uint64_t items_cap = 0, trees_cap = 0;
     DevBuf hctr, items, trees, gcv, hashes, packed;
     // read-boundary grid (Tables::gpos...): production semantics only
@@ -223,6 +223,7 @@ HashTables make_hash_tables(syncr_cdc *h) {
     t.packed_cap = std::max<uint64_t>(h->total_cut_cap, 1);
     t.ablate = h->b3_ablate;
     t.nt = h->b3_nt;
+    t.coop = h->b3_coop;
     return t;
 }
 
@@ -343,6 +344,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *rs = getenv("SYNCR_CDC_RESOLVE")) h->kp.resolve_lane = strcmp(rs, "lane") == 0;
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
     if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
+    if (const char *ld = getenv("SYNCR_B3_LOAD")) h->b3_coop = strcmp(ld, "plain") != 0;   // A/B only
     // scan variant (timing / A-B only; every variant is exact)
     if (const char *k = getenv("SYNCR_CDC_SCAN")) {
         if (strcmp(k, "valu") == 0) h->geom = ScanGeom{SCAN_VALU, DEFAULT_RUN, 0};
