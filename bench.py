@@ -234,12 +234,17 @@ def main(argv=None):
     run_steps(1, args.warmup)
     d.barrier()
     ch.synchronize()
-    ch.set_timing(True)                       # HIP events around each kernel, same stream
+    ch.set_timing(True, scan_only=True)       # HIP events around the scan kernel, on its stream
     t0 = time.perf_counter()
     run_steps(1, args.steps)                  # the timed region: one batch in flight
     dt = time.perf_counter() - t0
     d.barrier()
     kms, nl = ch.kernel_times()
+    ch.set_timing(False)
+    # diagnostics outside the timed region: every phase bracketed by events
+    ch.set_timing(True)
+    run_steps(1, min(args.steps, 5))
+    pms, pn = ch.kernel_times()
     ch.set_timing(False)
 
     pipelined = None
@@ -279,8 +284,8 @@ def main(argv=None):
         "traffic": (int(tr["hbm_bytes_per_launch"]) if tr else None),
         "kernel": engine_info["scan_kernel"], "kernel_ms": round(scan_ms, 4),
         "algorithmic_bytes_per_launch": span,
-        "dense_ms": round(kms[1] / max(nl, 1), 4), "resolve_ms": round(kms[2] / max(nl, 1), 4),
-        "hash_ms": round(kms[3] / max(nl, 1), 4) if args.hashed else None,
+        "dense_ms": round(pms[1] / max(pn, 1), 4), "resolve_ms": round(pms[2] / max(pn, 1), 4),
+        "hash_ms": round(pms[3] / max(pn, 1), 4) if args.hashed else None,
         "traffic_source": (tr.get("source") if tr else None),
     }
     cpu = None

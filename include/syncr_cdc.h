@@ -210,9 +210,11 @@ void *syncr_cdc_stream(syncr_cdc *h);
 int32_t syncr_cdc_gen_corpus(syncr_cdc *h, uint8_t *d_bytes, const uint64_t *file_off,
                              const uint64_t *file_len, const uint64_t *file_index,
                              uint32_t nfiles, uint64_t first_index, void *stream);
-/* Per-kernel timing: when enabled, every launch brackets its kernels with HIP
- * events on the launch stream; kernel_times returns the summed milliseconds of
- * [scan, dense, resolve] since the last reset and the number of launches. */
+/* Per-kernel timing: enable = 1 brackets every phase of each launch with HIP
+ * events on the launch stream (kernel_times: summed ms of [scan, dense +
+ * compaction, resolve] since the last reset, and the number of launches);
+ * enable = 2 records only the two events around the scan kernel (each event
+ * costs a few microseconds of queue idle); 0 disables. */
 int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable);
 int32_t syncr_cdc_kernel_times(syncr_cdc *h, double *ms3, uint64_t *launches);
 /* The same for up to 4 phases: [scan, dense+compaction, resolve, hash]. */

@@ -294,8 +294,10 @@ class Chunker:
         _check(fn(self._h, out.ctypes.data, out.size, counts.ctypes.data, ctypes.byref(n)), "syncr_cdc_fetch")
         return _split(out[: int(n.value)], counts[:nf])
 
-    def set_timing(self, on: bool) -> None:
-        _check(library().syncr_cdc_set_timing(self._h, 1 if on else 0), "syncr_cdc_set_timing")
+    def set_timing(self, on: bool, scan_only: bool = False) -> None:
+        """HIP events around each launch's kernels; scan_only: only around the scan."""
+        mode = (2 if scan_only else 1) if on else 0
+        _check(library().syncr_cdc_set_timing(self._h, mode), "syncr_cdc_set_timing")
 
     def kernel_times(self) -> tuple[list[float], int]:
         """Summed ms of [scan, dense+compaction, resolve, hash] since set_timing(True)."""

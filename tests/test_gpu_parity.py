@@ -295,6 +295,12 @@ def test_kernel_timing_api(chunkers):
         ms, n = ch.kernel_times()
         ch.set_timing(False)
         assert n == 3 and ms[0] > 0 and ms[2] > 0
+        ch.set_timing(True, scan_only=True)          # two events per launch, around the scan
+        for _ in range(2):
+            ch.launch(buf.ptr)
+        ms2, n2 = ch.kernel_times()
+        ch.set_timing(False)
+        assert n2 == 2 and ms2[0] > 0 and ms2[1] == ms2[2] == ms2[3] == 0
         ch.fetch()
         st = ch.last_stats()
         assert st["tiles"] >= data_len // (144 * 128) and st["flags"] == 0
