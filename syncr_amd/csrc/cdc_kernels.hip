@@ -231,31 +231,6 @@ __device__ __forceinline__ void rewalk_dirty(const KParams &P, int lane, uint32_
     }
 }
 
-// First chunk-local hit in [e+1, e+63] from global memory.  Bytes are loaded
-// 16 at a time (one chunk's loads in flight) to bound the register footprint
-// of the scan kernels that inline it; it runs once per recorded edge.
-__device__ __forceinline__ uint32_t head_fix_global(const uint8_t *data, uint64_t span, uint64_t e,
-                                                    uint32_t mask) {
-    uint32_t S = 0, W = 0;
-#pragma unroll 1
-    for (int k0 = 0; k0 < 64; k0 += 16) {
-        uint32_t x[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint64_t q = e + 1 + (uint64_t)(k0 + k);
-            x[k] = (k0 + k < 63 && q < span) ? data[q] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            S += x[k];
-            W += S;
-            const uint64_t q = e + 1 + (uint64_t)(k0 + k);
-            if (k0 + k < 63 && q < span && hit_exact(S, W, mask)) return (uint32_t)(k0 + k) + 1;
-        }
-    }
-    return 0;
-}
-
 // Publish this tile's candidates (sorted, with head fix-ups) or mark it dense.
 __device__ __forceinline__ void publish_tile(const uint8_t *__restrict__ data, const KParams &P,
                                              const Tables &T, uint32_t tile, int64_t t0,
@@ -771,6 +746,43 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
 // one thread per candidate, so the resolve walk never waits on byte loads;
 // then the head hit of every read-boundary grid point (first chunk-local hit
 // in [p, min(p+63, file end)), stored as offset + 1).
+// First chunk-local hit in [e+1, e+63] (as k = hit - e; 0 = none) for a chunk
+// starting at e+1, from global memory.  The window's bytes are fetched in one
+// round: four unaligned 16-byte loads (gfx950 global loads are
+// unaligned-capable) when the 64 bytes after e lie inside the batch.  Bytes at
+// or past `lim` are outside the file: no hit there.
+__device__ __forceinline__ uint32_t head_fix_fast(const uint8_t *__restrict__ data, uint64_t span, uint64_t lim,
+                                                  uint64_t e, uint32_t mask) {
+    const uint64_t a = e + 1;
+    uint32_t w[16];
+    if (a + 64 <= span) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint4 v;
+            __builtin_memcpy(&v, data + a + 16 * i, 16);
+            w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            uint32_t x = 0;
+            for (int b = 0; b < 4; ++b)
+                if (a + 4 * i + b < span) x |= (uint32_t)data[a + 4 * i + b] << (8 * b);
+            w[i] = x;
+        }
+    }
+    const uint32_t n = lim > a ? (uint32_t)min<uint64_t>(63ull, lim - a) : 0u;
+    uint32_t S = 0, W = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 63; ++k) {
+        const uint32_t x = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+        S += x;
+        W += S;
+        if (k < n && hit_exact(S, W, mask)) return k + 1;
+    }
+    return 0;
+}
+
 __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict__ data, KParams P,
                                                       Tables T) {
     const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
@@ -778,14 +790,14 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n + T.ngrid; i += (uint64_t)gridDim.x * 256) {
         if (i < n) {
             const uint64_t e = T.cand[i] & CAND_POS_MASK;
-            const uint32_t fix = head_fix_global(data, T.span, e, P.mask);
+            const uint32_t fix = head_fix_fast(data, T.span, T.span, e, P.mask);
             T.cand[i] = e | ((uint64_t)fix << 48) | CAND_KNOWN;
         } else {
             const uint64_t g = i - n;
             const uint64_t p = T.gpos[g];
-            // head_fix_global(p - 1) scans [p, p+63) with the window reset at p
+            // head_fix_fast(p - 1) scans [p, p+63) with the window reset at p
             const uint64_t end = T.gend[g];
-            uint32_t f = head_fix_global(data, end, p - 1, P.mask);
+            uint32_t f = head_fix_fast(data, T.span, end, p - 1, P.mask);
             T.gfix[g] = (uint8_t)f;
         }
     }
