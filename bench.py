@@ -190,6 +190,8 @@ def main(argv=None):
     ap.add_argument("--mode", default="production", choices=["production", "ideal"])
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-read-probe", action="store_true",
+                    help="skip the streaming-read microbenchmark reported as roofline.measured_read_peak")
     ap.add_argument("--pipeline-depth", type=int, default=2,
                     help="after the timed region, also time K steps with this many batches in flight "
                          "(each slot its own engine handle, HIP stream and copy of the corpus, like the "
@@ -288,6 +290,19 @@ def main(argv=None):
         "hash_ms": round(pms[3] / max(pn, 1), 4) if args.hashed else None,
         "traffic_source": (tr.get("source") if tr else None),
     }
+    if not args.no_read_probe and span >= 16:
+        # measured streaming-read ceiling over the same resident bytes:
+        # a read-only kernel, best pass of `reps`, both load policies
+        probe = {}
+        for nt in (True, False):
+            best, mean = ch.read_probe(dbuf.ptr, span, reps=10, nt=nt)
+            probe["nt" if nt else "plain"] = {"best_gbs": round(span / (best / 1e3) / 1e9, 1),
+                                              "mean_gbs": round(span / (mean / 1e3) / 1e9, 1)}
+        peak_meas = max(v["best_gbs"] for v in probe.values())
+        roofline["measured_read_peak"] = peak_meas
+        roofline["frac_of_measured"] = round(achieved / peak_meas, 4) if peak_meas else None
+        roofline["read_probe"] = dict(probe, kernel="cdc_read_probe_kernel (syncr_cdc_read_probe), 10 passes "
+                                                    "over the corpus buffer, 16 B loads, no writes")
     cpu = None
     if d.rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(ch, dbuf, offs, lens, cuts, args.cpu_sample_gib, hashed=args.hashed)

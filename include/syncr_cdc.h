@@ -210,6 +210,12 @@ void *syncr_cdc_stream(syncr_cdc *h);
 int32_t syncr_cdc_gen_corpus(syncr_cdc *h, uint8_t *d_bytes, const uint64_t *file_off,
                              const uint64_t *file_len, const uint64_t *file_index,
                              uint32_t nfiles, uint64_t first_index, void *stream);
+/* Streaming-read probe (roofline denominator): reads
+ * [d_bytes, d_bytes + bytes) once per pass with 16-byte loads (nt != 0: the
+ * non-temporal policy the scan uses), writes nothing, `reps` timed passes on
+ * the handle's stream after one warm-up.  ms2 = [best, mean] ms per pass. */
+int32_t syncr_cdc_read_probe(syncr_cdc *h, const uint8_t *d_bytes, uint64_t bytes, uint32_t reps,
+                             int32_t nt, double *ms2);
 /* Per-kernel timing: enable = 1 brackets every phase of each launch with HIP
  * events on the launch stream (kernel_times: summed ms of [scan, dense +
  * compaction, resolve] since the last reset, and the number of launches);

@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "syncr_cdc_fetch", "syncr_cdc_chunk_batch_device", "syncr_cdc_device_alloc",
     "syncr_cdc_device_free", "syncr_cdc_host_alloc_pinned", "syncr_cdc_host_free_pinned",
     "syncr_cdc_memcpy_h2d", "syncr_cdc_memcpy_d2h", "syncr_cdc_synchronize", "syncr_cdc_stream",
-    "syncr_cdc_gen_corpus", "syncr_cdc_set_timing", "syncr_cdc_kernel_times",
+    "syncr_cdc_gen_corpus", "syncr_cdc_read_probe", "syncr_cdc_set_timing", "syncr_cdc_kernel_times",
     "syncr_cdc_last_stats", "syncr_cdc_get_info",
     "syncr_cdc_chunk_host_hashed", "syncr_cdc_chunk_batch_host_hashed", "syncr_cdc_launch_hashed",
     "syncr_cdc_fetch_hashed", "syncr_cdc_kernel_times_ex",
@@ -124,6 +124,7 @@ def library():
             "syncr_cdc_synchronize": ([_vp], _i32),
             "syncr_cdc_stream": ([_vp], _vp),
             "syncr_cdc_gen_corpus": ([_vp, _vp, _vp, _vp, _vp, _u32, _u64, _vp], _i32),
+            "syncr_cdc_read_probe": ([_vp, _vp, _u64, _u32, _i32, ctypes.POINTER(ctypes.c_double)], _i32),
             "syncr_cdc_set_timing": ([_vp, _i32], _i32),
             "syncr_cdc_kernel_times": ([_vp, ctypes.POINTER(ctypes.c_double), _pu64], _i32),
             "syncr_cdc_last_stats": ([_vp, _pu64], _i32),
@@ -305,6 +306,13 @@ class Chunker:
         n = ctypes.c_uint64(0)
         _check(library().syncr_cdc_kernel_times_ex(self._h, ms, 4, ctypes.byref(n)), "syncr_cdc_kernel_times_ex")
         return [ms[0], ms[1], ms[2], ms[3]], int(n.value)
+
+    def read_probe(self, d_ptr: int, nbytes: int, reps: int = 10, nt: bool = True) -> tuple[float, float]:
+        """Streaming-read microbenchmark over device bytes: (best, mean) ms per pass."""
+        ms = (ctypes.c_double * 2)()
+        _check(library().syncr_cdc_read_probe(self._h, d_ptr, nbytes, reps, 1 if nt else 0, ms),
+               "syncr_cdc_read_probe")
+        return ms[0], ms[1]
 
     def last_stats(self) -> dict:
         st = (ctypes.c_uint64 * 4)()

@@ -789,6 +789,44 @@ int32_t syncr_cdc_gen_corpus(syncr_cdc *h, uint8_t *d_bytes, const uint64_t *fil
     }
 }
 
+int32_t syncr_cdc_read_probe(syncr_cdc *h, const uint8_t *d_bytes, uint64_t bytes, uint32_t reps,
+                             int32_t nt, double *ms2) {
+    if (!h || !d_bytes || !ms2 || !reps || bytes < 16) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus <= 0)
+        cus = 256;
+    const uint64_t blocks_needed = (bytes / 16 + 4095) / 4096;     // 64 KiB per block step
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(blocks_needed, (uint64_t)cus * 8);
+    DevBuf sink;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e = hipSuccess;
+    double best = 1e30, sum = 0;
+    do {
+        if ((e = sink.ensure((size_t)grid * 4)) != hipSuccess) break;
+        if ((e = hipEventCreate(&e0)) != hipSuccess) break;
+        if ((e = hipEventCreate(&e1)) != hipSuccess) break;
+        if ((e = launch_read_probe(d_bytes, bytes, nt != 0, grid, sink.as<uint32_t>(), h->stream)) != hipSuccess) break;
+        for (uint32_t r = 0; r < reps && e == hipSuccess; ++r) {
+            if ((e = hipEventRecord(e0, h->stream)) != hipSuccess) break;
+            if ((e = launch_read_probe(d_bytes, bytes, nt != 0, grid, sink.as<uint32_t>(), h->stream)) != hipSuccess) break;
+            if ((e = hipEventRecord(e1, h->stream)) != hipSuccess) break;
+            if ((e = hipEventSynchronize(e1)) != hipSuccess) break;
+            float f = 0;
+            if ((e = hipEventElapsedTime(&f, e0, e1)) != hipSuccess) break;
+            best = std::min(best, (double)f);
+            sum += f;
+        }
+    } while (0);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    sink.release();
+    if (e != hipSuccess) return hip_err(e);
+    ms2[0] = best;
+    ms2[1] = sum / reps;
+    return SYNCR_CDC_OK;
+}
+
 int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable) {
     if (!h) return SYNCR_CDC_EINVAL;
     (void)hipSetDevice(h->device);

@@ -153,6 +153,8 @@ hipError_t launch_resolve(const uint8_t *d_bytes, const KParams &p, const Tables
 hipError_t launch_gen(uint8_t *d_base, const uint64_t *d_foff, const uint64_t *d_flen,
                       const uint64_t *d_findex, const uint64_t *d_seg_prefix, uint32_t nfiles,
                       uint64_t nseg, uint64_t first_index, const uint64_t *d_jump, hipStream_t s);
+hipError_t launch_read_probe(const uint8_t *d_bytes, uint64_t bytes, bool nt, uint32_t grid, uint32_t *sink,
+                             hipStream_t s);
 hipError_t launch_hash(int device, const uint8_t *d_bytes, const Tables &t, const HashTables &ht,
                        hipStream_t s);
 constexpr int GEN_SEG = 4096;     // bytes generated per thread

@@ -1183,6 +1183,55 @@ __global__ __launch_bounds__(256) void cdc_gen_kernel(uint8_t *__restrict__ base
 }
 
 // ---------------------------------------------------------------------------
+// Streaming-read probe (roofline denominator): the best rate this
+// part reaches reading bytes once, with nothing else to do.  Each lane keeps
+// UNR 16-byte loads in flight per iteration (grid-stride over 64 KiB blocks so
+// a workgroup's loads are contiguous); the XOR of everything read is stored
+// only if it equals an impossible sentinel, so the loads cannot be dropped and
+// nothing is written.  NT selects the non-temporal policy (as the scan uses).
+// ---------------------------------------------------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__global__ __launch_bounds__(256) void cdc_read_probe_kernel(const u32x4 *__restrict__ src, uint64_t nvec,
+                                                             uint32_t *__restrict__ sink) {
+    constexpr int UNR = 16;                               // 256 lanes x 16 x 16 B = 64 KiB per block step
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    const uint64_t step = (uint64_t)gridDim.x * 256 * UNR;
+    for (uint64_t b = (uint64_t)blockIdx.x * 256 * UNR; b < nvec; b += step) {
+        u32x4 v[UNR];
+        if (b + 256 * UNR <= nvec) {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const u32x4 *p = src + b + u * 256 + threadIdx.x;
+                if constexpr (NT) v[u] = __builtin_nontemporal_load(p); else v[u] = *p;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const uint64_t k = b + u * 256 + threadIdx.x;
+                v[u] = k < nvec ? src[k] : u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) acc ^= v[u];
+    }
+    const uint32_t r = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (r == 0x5EC7E7u && acc.x == 0xC0FFEEu && acc.y == 0xFACADEu) sink[blockIdx.x] = r;
+}
+
+hipError_t launch_read_probe(const uint8_t *d, uint64_t bytes, bool nt, uint32_t grid, uint32_t *sink,
+                             hipStream_t s) {
+    const uint64_t nvec = bytes / 16;
+    if (!nvec) return hipSuccess;
+    if (nt)
+        hipLaunchKernelGGL(cdc_read_probe_kernel<true>, dim3(grid), dim3(256), 0, s, (const u32x4 *)d, nvec, sink);
+    else
+        hipLaunchKernelGGL(cdc_read_probe_kernel<false>, dim3(grid), dim3(256), 0, s, (const u32x4 *)d, nvec, sink);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 static bool valu_run_ok(int run) { return run == 48 || run == 80 || run == 112 || run == 144 || run == 176; }
 static bool mfma_nb_ok(int nb) { return nb == 4 || nb == 6 || nb == 8 || nb == 10 || nb == 12; }
 

@@ -392,3 +392,23 @@ def test_dedup_corpus_full_size():
     want = O.blake3_batch(buf, np.concatenate(starts), np.concatenate(sizes), nthreads=16)
     assert np.array_equal(np.concatenate([g["hash"] for g in got]), want)
     assert np.median(kept) >= 0.9
+
+
+def test_read_probe_reports_a_plausible_rate():
+    """The streaming-read probe (bench.py's measured roofline denominator) runs
+    over a resident buffer, writes nothing and reports best <= mean."""
+    with syncr_amd.Chunker(device=0) as ch:
+        n = 256 * M + 48                                  # ragged tail: not a multiple of a block step
+        buf = syncr_amd.DeviceBuffer(ch, n)
+        try:
+            buf.gen_corpus(np.array([0], np.uint64), np.array([n], np.uint64))
+            before = buf.download(4096)
+            for nt in (True, False):
+                best, mean = ch.read_probe(buf.ptr, n, reps=3, nt=nt)
+                assert 0 < best <= mean
+                assert 100.0 < n / (best / 1e3) / 1e9 < 20000.0          # GB/s
+            assert np.array_equal(buf.download(4096), before)
+            with pytest.raises(syncr_amd.SyncrCdcError):
+                ch.read_probe(buf.ptr, 0, reps=1)
+        finally:
+            buf.free()
