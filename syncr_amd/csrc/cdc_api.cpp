@@ -345,7 +345,10 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     h->kp = make_kparams(prm);
     if (const char *a = getenv("SYNCR_CDC_ABLATE")) h->kp.ablate = (uint32_t)atoi(a);  // timing-only
     if (const char *nt = getenv("SYNCR_CDC_NT")) h->kp.nt = (uint32_t)atoi(nt);
-    if (const char *rs = getenv("SYNCR_CDC_RESOLVE")) h->kp.resolve_lane = strcmp(rs, "lane") == 0;
+    if (const char *rs = getenv("SYNCR_CDC_RESOLVE")) {
+        h->kp.resolve_lane = strcmp(rs, "lane") == 0;
+        h->kp.resolve_noburst = strcmp(rs, "noburst") == 0;
+    }
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
     if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
     if (const char *ld = getenv("SYNCR_B3_LOAD")) h->b3_coop = strcmp(ld, "plain") != 0;   // A/B only

@@ -66,6 +66,7 @@ struct KParams {
     uint32_t ablate;   // timing-only diagnostics (SYNCR_CDC_ABLATE): 1 = no rolling, 2 = no DMA, 3 = 1 with nt
     uint32_t nt;       // 1: non-temporal tile loads (SYNCR_CDC_NT=1)
     uint32_t resolve_lane;  // 1: lane-per-file resolve (SYNCR_CDC_RESOLVE=lane); 0: wave-per-file
+    uint32_t resolve_noburst;  // 1: no burst of chained hops in the wave resolve (SYNCR_CDC_RESOLVE=noburst, A/B)
 };
 
 struct DevCut {        // == syncr_cut

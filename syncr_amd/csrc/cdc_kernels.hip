@@ -994,13 +994,15 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
         gb = T.gbase[i];
         if ((uint64_t)lane * CAPv < F) gf = T.gfix[gb + lane];
     }
-    // gathered cuts: lane k of (bo, bl) = cut (cnt & ~63) + k
+    // gathered cuts: lane k of (bo, bl) = cut (cnt & ~63) + k, valid from slot bstart
+    // (the slots below it were written directly by a burst, see below)
     Off bo = 0;
     uint32_t bl = 0;
     Off cnt = 0;             // cuts so far (< F + 1, so Off is wide enough)
+    uint32_t bstart = 0;
     auto flush = [&](uint32_t n) {
         const uint64_t k = (uint64_t)(cnt - n) + (uint64_t)lane;   // cnt already counts these n cuts
-        if ((uint32_t)lane < n && k < cap) {
+        if ((uint32_t)lane >= bstart && (uint32_t)lane < n && k < cap) {
             DevCut d;
             d.offset = (uint64_t)bo;
             d.len = bl;
@@ -1014,6 +1016,61 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
     uint32_t fix = 0;
     int jlast = -1;          // window index of the candidate the last cut was made at
     while (s < R) {                                          // :747
+        if constexpr (sizeof(Off) == 4) {
+            // Burst of chained hops: while every cut lands on a window candidate
+            // with no head hit after it (fix 0), the next cut is the candidate
+            // nx[] names, if it lies below the read limit.  Those iterations of
+            // the loop below reduce to this scalar chain; the cuts are marked in
+            // a lane mask and written in parallel afterwards (one lane per cut).
+            if (head == 1 && fix == 0 && jlast >= 0 && !P.resolve_noburst) {
+                uint64_t mk = 0;
+                const Off s0 = s, n0 = cnt;
+                for (;;) {
+                    const uint32_t jn = (uint32_t)__builtin_amdgcn_readlane((int)nx, jlast);
+                    if (jn >= 64) break;
+                    const Off c = rl(wr, jn);
+                    if (c < s + 63 || c >= R) break;                 // general iteration decides
+                    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)wk, (int)jn);
+                    mk |= 1ull << jn;
+                    ++cnt;
+                    s = c + 1;                                       // cut = edge + 1 (:754-755, :771)
+                    Off rd = MAX - (R - s);                          // :776
+                    rd = min(rd, CAP);
+                    asm volatile("" : "+s"(rd));
+                    rd = min(rd, (Off)(Fo - R));
+                    R += rd;
+                    jlast = (int)jn;
+                    head = (k & 0x100u) ? 1 : 2;
+                    fix = k & 0xffu;
+                    if (head != 1 || fix != 0 || s >= R) break;
+                }
+                if (mk) {
+                    const uint32_t pend = (uint32_t)n0 & 63u;        // gathered cuts before the burst
+                    if (pend > bstart) {
+                        const Off keep = cnt;
+                        cnt = n0;
+                        flush(pend);
+                        cnt = keep;
+                    }
+                    const uint64_t below = (lane ? (~0ull >> (64 - lane)) : 0ull) & mk;
+                    const uint32_t pl = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
+                    const Off pw = (Off)__shfl((int)wr, (int)pl);
+                    if ((mk >> lane) & 1ull) {
+                        const Off st = below ? pw + 1 : s0;
+                        const uint64_t idx = (uint64_t)n0 + (uint64_t)__builtin_popcountll(below);
+                        if (idx < cap) {
+                            DevCut d;
+                            d.offset = (uint64_t)st;
+                            d.len = (uint32_t)(wr + 1 - st);
+                            d.file = i;
+                            out[idx] = d;
+                        }
+                    }
+                    bstart = (uint32_t)cnt & 63u;
+                }
+                if (s >= R) break;
+            }
+        }
         const Off lim = R;                                   // :749-752
         Off e = OMAX;
         bool known = false;
@@ -1096,7 +1153,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
             bl = (uint32_t)(cut - s);
         }
         ++cnt;
-        if (__builtin_expect(slot == 63u, 0)) flush(64);
+        if (__builtin_expect(slot == 63u, 0)) { flush(64); bstart = 0; }
         s = cut;                                             // :771
         // :776, kept in the scalar unit (hipcc otherwise fuses the mins into a
         // VALU v_min3 plus a readfirstlane round trip on this serial path)
