@@ -655,9 +655,7 @@ __global__ __launch_bounds__(1024) void cdc_prefix_kernel(Tables T) {
     const uint32_t n = T.nwords, t = threadIdx.x;
     const int lane = t & 63, wv = t >> 6;
     uint64_t carry = 0;
-    for (uint32_t base = 0; base < n; base += 4096) {
-        const uint32_t i0 = base + 4 * t;
-        uint32_t c[4];
+    auto load4 = [&](uint32_t i0, uint32_t (&c)[4]) {
         if (i0 + 3 < n && (n & 3) == 0) {
             const uint4 v = *(const uint4 *)(T.super_cnt + i0);
             c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
@@ -665,6 +663,13 @@ __global__ __launch_bounds__(1024) void cdc_prefix_kernel(Tables T) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) c[k] = i0 + k < n ? T.super_cnt[i0 + k] : 0u;
         }
+    };
+    uint32_t nxt[4];
+    load4(4 * t, nxt);                                    // pass 0; pass p+1 is loaded during pass p
+    for (uint32_t base = 0; base < n; base += 4096) {
+        const uint32_t i0 = base + 4 * t;
+        uint32_t c[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
+        if (base + 4096 < n) load4(i0 + 4096, nxt);
         const uint64_t mine = (uint64_t)c[0] + c[1] + c[2] + c[3];
         const uint64_t incl = wave_incl_scan64(mine, lane);
         if (lane == 63) wsum[wv] = incl;
@@ -948,8 +953,14 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
     uint64_t wb = F ? T.super_off[(uint32_t)((g0 / T.tile) >> 6)] : 0;   // the file's 64-tile group
     Off wr = OMAX;
     uint32_t wk = 0, nx = 64;
+    // the window after the current one is loaded ahead (a slide then costs no
+    // dependent HBM round trip on this serial walk)
+    auto fetch = [&](uint64_t b) -> uint64_t {
+        return b + (uint64_t)lane < ncand ? T.cand[b + lane] : NONE;
+    };
+    uint64_t pf_cur = fetch(wb), pf_next = fetch(wb + 64);
     auto load_window = [&]() {
-        const uint64_t c = wb + (uint64_t)lane < ncand ? T.cand[wb + lane] : NONE;
+        const uint64_t c = pf_cur;
         wr = OMAX;
         wk = 0;
         if (c != NONE) {
@@ -1140,6 +1151,8 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     }
                     if (wb + 64 >= ncand) break;             // whole window below `from`: slide
                     wb += 64;
+                    pf_cur = pf_next;
+                    pf_next = fetch(wb + 64);
                     load_window();
                 }
             }
