@@ -1036,26 +1036,32 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
             if (head == 1 && fix == 0 && jlast >= 0 && !P.resolve_noburst) {
                 uint64_t mk = 0;
                 const Off s0 = s, n0 = cnt;
+                // nxv: the chain continues past a cut at lane j only if j's
+                // fix-up is known and zero; otherwise 64 ends the burst there
+                const uint32_t nxv = (wk & 0x1ffu) == 0x100u ? nx : 64u;
+                int j = jlast;
                 for (;;) {
-                    const uint32_t jn = (uint32_t)__builtin_amdgcn_readlane((int)nx, jlast);
+                    const uint32_t jn = (uint32_t)__builtin_amdgcn_readlane((int)nxv, j);
                     if (jn >= 64) break;
                     const Off c = rl(wr, jn);
+                    // c < s + 63: never for a sorted window; keeps the walk moving
+                    // forward after a candidate overflow (see the chained hop below)
                     if (c < s + 63 || c >= R) break;                 // general iteration decides
-                    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)wk, (int)jn);
                     mk |= 1ull << jn;
-                    ++cnt;
                     s = c + 1;                                       // cut = edge + 1 (:754-755, :771)
                     Off rd = MAX - (R - s);                          // :776
                     rd = min(rd, CAP);
                     asm volatile("" : "+s"(rd));
                     rd = min(rd, (Off)(Fo - R));
                     R += rd;
-                    jlast = (int)jn;
-                    head = (k & 0x100u) ? 1 : 2;
-                    fix = k & 0xffu;
-                    if (head != 1 || fix != 0 || s >= R) break;
+                    j = (int)jn;
                 }
                 if (mk) {
+                    cnt += (Off)__builtin_popcountll(mk);
+                    jlast = j;
+                    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)wk, j);
+                    head = (k & 0x100u) ? 1 : 2;
+                    fix = k & 0xffu;
                     const uint32_t pend = (uint32_t)n0 & 63u;        // gathered cuts before the burst
                     if (pend > bstart) {
                         const Off keep = cnt;
