@@ -105,8 +105,14 @@ def load_traffic(workload_name: str, span: int, run_bytes: int):
     """HBM bytes per scan launch from the committed rocprofv3 PMC summary of
     the same workload, span and scan geometry (profiles/*_pmc_traffic.json)."""
     import glob
+    import re
+
+    def version(path):            # r01_v11h_pmc_traffic.json -> (1, 11): latest round/version last
+        m = re.search(r"r(\d+)(?:_v(\d+))?", os.path.basename(path))
+        return (int(m.group(1)), int(m.group(2) or 0)) if m else (0, 0)
+
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), key=version):
         try:
             d = json.load(open(p))
         except Exception:
