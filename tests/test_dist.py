@@ -64,3 +64,26 @@ def test_gloo_world2_reductions():
     assert [r[1] for r in res] == [1024, 1024]
     assert all(r[2] == 2048 * (1 << 20) for r in res)           # sum over ranks
     assert all(r[3] == 2.0 for r in res)                         # max over ranks
+
+
+def test_load_traffic_takes_latest_version(tmp_path, monkeypatch):
+    """bench.py's roofline.traffic comes from the newest matching PMC summary:
+    r01_v11 must win over r01_v9 (numeric, not lexicographic, order), and a
+    summary for another span or scan geometry is never used."""
+    import json
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+
+    def put(tag, span, run, hbm):
+        (prof / f"{tag}_pmc_traffic.json").write_text(json.dumps(
+            {"workload": "zipf10k", "span": span, "run_bytes": run, "hbm_bytes_per_launch": hbm,
+             "source": tag}))
+
+    put("r01_v9", 1000, 144, 1)
+    put("r01_v11", 1000, 144, 2)
+    put("r01_v12", 2000, 144, 3)          # other span
+    put("r01_v13", 1000, 112, 4)          # other scan geometry
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    t = bench.load_traffic("zipf10k", 1000, 144)
+    assert t["source"] == "r01_v11" and t["hbm_bytes_per_launch"] == 2
+    assert bench.load_traffic("uniform1k", 1000, 144) is None
