@@ -412,3 +412,19 @@ def test_read_probe_reports_a_plausible_rate():
                 ch.read_probe(buf.ptr, 0, reps=1)
         finally:
             buf.free()
+
+
+@pytest.mark.parametrize("bits,mx,cap", [(12, 16 << 20, 2 << 20), (16, 1 << 20, 70000), (14, 40000, 0),
+                                         (10, 3000, 1000)])
+def test_long_resolve_chains(chunkers, bits, mx, cap):
+    """One 48 MiB file cut into thousands of chunks: the wave resolve walks
+    hundreds of 64-candidate windows, its chained-hop bursts end on every
+    kind of break (window end, read limit R, max-chunk cut, head hit), and
+    the cuts a burst writes directly interleave with the gathered ones."""
+    rng = np.random.default_rng(bits * 1000 + cap)
+    data = rng.integers(0, 256, 48 * M, dtype=np.uint8)
+    data[5 * M: 5 * M + 300000] = 7                       # a low-entropy stretch: max-chunk cuts
+    ch = chunkers(bits, mx, cap)
+    cuts = ch.cut_array(data)
+    assert ends_of(cuts) == oracle_ends(data, bits, mx, cap)
+    check_contiguous(cuts, data.size, mx)
