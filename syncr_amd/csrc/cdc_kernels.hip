@@ -361,12 +361,40 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
     uint32_t *dcount = wcount + 1;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
     const uint32_t stride = gridDim.x;
+    // MODE bit 3 (DYN, the product; SYNCR_CDC_ABLATE=4 = static stride): dynamic groups of DG tiles.  Group k covers tiles
+    // (k / G) * G * DG + (k % G) + i * G, i < DG (G = grid): the waves still
+    // sweep the batch together as with the static stride, but a wave that
+    // runs faster takes more groups.  A wave's first group is its block
+    // index; later ones come from a counter (CTR_CANDS_HI is free until the
+    // prefix kernel writes it), grabbed at a group's first tile so the atomic
+    // completes under the roll.
+    constexpr bool DYN = (MODE & 8) != 0;
+    constexpr uint32_t DG = 16;           // A/B on zipf10k: 4 -> 2.07 ms (counter-bound), 16 -> 1.627, 32 -> 1.633, 64 -> 1.669, static 1.657
+    auto gbase = [&](uint32_t k) { return (k / stride) * stride * DG + (k % stride); };
     uint32_t tile = blockIdx.x;
     if (tile >= T.ntiles) return;
     const int64_t span = (int64_t)T.span;
     issue_tile<RUN, (MODE & 4) != 0>(data, T.span, tile, lds0, lane);
-    for (; tile < T.ntiles; tile += stride) {
-        const uint32_t next = tile + stride;
+    uint32_t gj = 0, pend = 0;
+    for (uint32_t next; tile < T.ntiles; tile = next) {
+        bool grabbed = false;
+        uint32_t gjn = 0;
+        if constexpr (DYN) {
+            if (gj + 1 < DG && tile + stride < T.ntiles) {
+                next = tile + stride;
+                gjn = gj + 1;
+            } else {
+                if (gj == 0) {                                       // group ends at its first tile (last round)
+                    if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
+                    grabbed = true;
+                }
+                wait_vmcnt<0>();                                     // the grab
+                next = gbase(stride + (uint32_t)__builtin_amdgcn_readfirstlane(pend));
+                gjn = 0;
+            }
+        } else {
+            next = tile + stride;
+        }
         const int64_t t0 = (int64_t)tile * TILE;
         if (lane == 0) { *wcount = 0u; *dcount = 0u; }
         wait_vmcnt<0>();                                             // this tile has landed
@@ -383,6 +411,10 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");           // runs are in registers
         if (next < T.ntiles && (MODE & 3) != 2) issue_tile<RUN, (MODE & 4) != 0>(data, T.span, next, lds0, lane);
+        if constexpr (DYN) {
+            if (gj == 0 && !grabbed && lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
+            gj = gjn;
+        }
         if constexpr ((MODE & 3) == 1) {                                   // diagnostics: staging only
 #pragma unroll
             for (int q = 0; q < NQ * 4; ++q) asm volatile("" ::"v"(A[q]), "v"(B[q]));
@@ -1319,7 +1351,7 @@ int scan_lds_bytes(ScanGeom g) {
     return g.kind == SCAN_VALU ? lds_wave_bytes(g.param) : mf_lds_bytes(g.param, (g.var & MFV_SINGLE) ? 1 : 2);
 }
 
-template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN, 4>; }
+template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN, 12>; }
 template <int NB> static const void *mfma_fn(int var) {
     switch (var & 3) {
         case 0: return (const void *)&cdc_scan_mfma_kernel<NB, 4, true>;
@@ -1368,10 +1400,12 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, ABL ? 2 : 0>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (ABL && p.ablate == 3u)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, ABL ? 5 : 0>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.nt)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 4>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (ABL && p.ablate == 4u)                                  // A/B: static stride (exact)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, ABL ? 4 : 12>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.nt)                                                   // product: nt loads + dynamic groups
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
     else
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 0>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 8>), dim3(grid), dim3(64), lds, s, d, p, t);
 }
 
 template <int NB, int V>
