@@ -369,7 +369,9 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
     // prefix kernel writes it), grabbed at a group's first tile so the atomic
     // completes under the roll.
     constexpr bool DYN = (MODE & 8) != 0;
-    constexpr uint32_t DG = 16;           // A/B on zipf10k: 4 -> 2.07 ms (counter-bound), 16 -> 1.627, 32 -> 1.633, 64 -> 1.669, static 1.657
+    // zipf10k A/B (same process): groups of 4 -> 2.07 ms (one counter serialises ~69 M grabs/s), 8 -> 1.601,
+    // 16 -> 1.635, 24 -> 1.651, 32 -> 1.633, 64 -> 1.669, static stride 1.657-1.694
+    constexpr uint32_t DG = 8;
     auto gbase = [&](uint32_t k) { return (k / stride) * stride * DG + (k % stride); };
     uint32_t tile = blockIdx.x;
     if (tile >= T.ntiles) return;
