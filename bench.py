@@ -12,7 +12,12 @@ LPT-sharded per file across ranks: fixed work per GPU ("weak" scaling), no
 data-path collective (files are independent).  torch.distributed
 (gloo) is used only for the barrier and the max-over-ranks of the step time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload zipf10k|uniform1k]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload zipf10k|uniform1k|dense|big1]
+
+`--gpus N` with N > 1 launches the N ranks itself (one process per GPU, before
+anything touches HIP) unless a launcher (torchrun) already set WORLD_SIZE, in
+which case WORLD_SIZE must equal N.  `--dry-run` does everything but touch a
+device: it prints the shard plan (files / bytes per rank, disjointness).
 """
 from __future__ import annotations
 
@@ -20,6 +25,8 @@ import argparse
 import heapq
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,12 +47,53 @@ def zipf_sizes(n: int = 10000, seed: int = 20251212) -> np.ndarray:
     return np.minimum(4096.0 * z, float(128 * M)).astype(np.uint64)
 
 
+# --workload dense: the zipf10k file table with adversarial contents in some
+# files (VERDICT r1 "What's missing" #4; the reference's own tests chunk
+# constant data, tests/chunking_test.rs:95-108, and 50 MiB of 'A',
+# tests/protocol_list_test.rs:360-378).  Kind per corpus index i:
+DENSE_PERIODIC, DENSE_CONSTANT = 5, 11          # i % 16 == 5: 64-byte period; i % 16 == 11: one byte value
+
+
+def dense_kind(i: int) -> int:
+    """0 random, 1 periodic (a 64-byte pattern that hits at bits 20 once per
+    period: a candidate every 64 bytes, 288 per scan tile = dense tiles), 2
+    constant byte (never hits: forced MAX / read-cap cuts only)."""
+    r = i % 16
+    return 1 if r == DENSE_PERIODIC else (2 if r == DENSE_CONSTANT else 0)
+
+
+def periodic_pattern(seed: int = 20251212) -> np.ndarray:
+    """64 bytes whose periodic extension hits the Bup edge test at chunk_bits
+    20 (S = sum of the window = 15 mod 16 and W = sum of (age+1)*byte = 0x17BF
+    mod 2^16, Appendix A) at the phase where the window is exactly the pattern
+    (age 0 = pattern[63]).  Built by fixing 62 random bytes and solving the last
+    two (weights 1 and 2) for the W target, then checking S."""
+    rng = np.random.default_rng(seed)
+    w = np.arange(64, 0, -1, dtype=np.int64)          # pattern[k] has age 63-k: weight 64-k
+    for _ in range(1 << 20):
+        p = rng.integers(0, 256, 64).astype(np.int64)
+        rest = int((w[:62] * p[:62]).sum())
+        t = (0x17BF - rest) % 65536                   # W = 0x17BF mod 2^16: (124992 + W) & 0xffff == 0xffff
+        for x1 in range(256):                          # pattern[62]: weight 2, pattern[63]: weight 1
+            x0 = t - 2 * x1
+            if 0 <= x0 < 256:
+                p[62], p[63] = x1, x0
+                S = int(p.sum())
+                if (1984 + S) % 16 == 15 and ((124992 + int((w * p).sum())) & 0xFFFF) == 0xFFFF:
+                    return p.astype(np.uint8)
+    raise RuntimeError("no periodic pattern found")
+
+
 def workload(name: str, world: int):
     """Global file table (sizes, corpus indices) for `world` GPUs."""
-    if name == "zipf10k":
+    if name in ("zipf10k", "dense"):
         one = zipf_sizes()
         desc = ("SURVEY §8d config 3: 10 000 Zipf(1.5) files, 4 KiB-128 MiB, 9.73 GiB per GPU; "
                 "N GPUs chunk N x 10 000 files (distinct seeds) LPT-sharded per file (config 4)")
+        if name == "dense":
+            desc = ("adversarial: the zipf10k file table; files i%16==5 are a 64-byte period that hits at "
+                    "chunk_bits 20 every 64 bytes (dense tiles, long serial resolve chains), files i%16==11 are "
+                    "one constant byte (no hits: MAX / read-cap cuts), the rest random")
     elif name == "big1":
         one = np.full(1, 128 * M, np.uint64)
         desc = "diagnostic: one 128 MiB file (the longest resolve walk of zipf10k)"
@@ -96,14 +144,54 @@ class Dist:
         self.pg.all_reduce(t, op={"max": self.pg.ReduceOp.MAX, "sum": self.pg.ReduceOp.SUM}[op])
         return float(t.item())
 
+    def gather(self, obj) -> list:
+        if not self.pg:
+            return [obj]
+        out = [None] * self.world
+        self.pg.all_gather_object(out, obj)
+        return out
+
     def close(self):
         if self.pg:
             self.pg.destroy_process_group()
 
 
-def load_traffic(workload_name: str, span: int, run_bytes: int):
-    """HBM bytes per scan launch from the committed rocprofv3 PMC summary of
-    the same workload, span and scan geometry (profiles/*_pmc_traffic.json)."""
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """One process per GPU, started here before anything touches HIP (the
+    parent never initialises a device).  Each child gets RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* like torchrun would set them; rank 0 prints the line.
+    A failing rank stops the others (by their exact PIDs)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def load_traffic(workload_name: str, span: int, run_bytes: int, kernel: str = "cdc::cdc_scan_kernel"):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    of the same workload, span and scan geometry (profiles/*_pmc_traffic.json)."""
     import glob
     import re
 
@@ -117,17 +205,39 @@ def load_traffic(workload_name: str, span: int, run_bytes: int):
             d = json.load(open(p))
         except Exception:
             continue
+        dk = d.get("kernel", "cdc::cdc_scan_kernel")     # the summary's main kernel
         if (d.get("workload") == workload_name and int(d.get("span", -1)) == span
-                and d.get("run_bytes") == run_bytes):
-            best = d
+                and d.get("run_bytes") == run_bytes
+                and (kernel == dk or kernel in d.get("per_kernel_hbm_bytes", {}))):
+            best = dict(d)
+            best["hbm_bytes_per_launch"] = (d["hbm_bytes_per_launch"] if kernel == dk
+                                            else d["per_kernel_hbm_bytes"][kernel])
     return best
 
 
-def cpu_baseline(chunker, dbuf, offs, lens, cuts, sample_gib: float, hashed: bool = False):
+def cpu_host() -> dict:
+    """The host the CPU baseline runs on (state core count and model)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    share = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_share": share,
+            "cpu_share_source": "OMP_NUM_THREADS (the GPU box's CPU share per GPU)" if omp else "sched_getaffinity"}
+
+
+def cpu_baseline(dbuf, offs, lens, cuts, hcuts, sample_gib: float):
     """Oracle (oracle/bup_oracle.c, the literal compute_file_chunks restatement)
-    timed on this host on a bounded sample of the same bytes.  Also checks the
-    GPU cuts of the sampled files against it.  hashed: the oracle also BLAKE3s
-    every chunk (oracle/blake3_oracle.c) and the GPU hashes are checked."""
+    timed on this host on a bounded sample of the same bytes, single thread (the
+    reference's serial per-file loop) and on every core of this job's CPU share.
+    Also the checker of the sample: the GPU cuts (and, when hcuts is given, the
+    GPU BLAKE3 of every chunk: oracle/blake3_oracle.c) must match it bit for bit."""
     from oracle import oracle as O
     take, tot = [], 0
     for i in range(lens.size):
@@ -141,6 +251,7 @@ def cpu_baseline(chunker, dbuf, offs, lens, cuts, sample_gib: float, hashed: boo
     host = dbuf.download(hi - lo, offset=lo)
     s_offs = (offs[take] - np.uint64(lo)).astype(np.uint64)
     s_lens = lens[take]
+
     def chunk_offsets(ref):
         o, n = [], []
         for j in range(take.size):
@@ -151,48 +262,84 @@ def cpu_baseline(chunker, dbuf, offs, lens, cuts, sample_gib: float, hashed: boo
         return (np.concatenate(o) if o else np.zeros(0, np.uint64),
                 np.concatenate(n) if n else np.zeros(0, np.uint64))
 
-    def run(nthreads):
-        r = O.chunk_batch(host, s_offs, s_lens, nthreads=nthreads)
-        hs = None
-        if hashed:
-            co, cn = chunk_offsets(r)
-            hs = O.blake3_batch(host, co, cn, nthreads=nthreads)
-        return r, hs
-
+    hw = cpu_host()
+    nthr = hw["cpu_share"]
     t = time.perf_counter()
-    ref, ref_h = run(1)
+    ref = O.chunk_batch(host, s_offs, s_lens, nthreads=1)
     dt1 = time.perf_counter() - t
-    nthr = min(16, os.cpu_count() or 1)
     t = time.perf_counter()
-    run(nthr)
+    O.chunk_batch(host, s_offs, s_lens, nthreads=nthr)
     dtn = time.perf_counter() - t
     mism = 0
-    k = 0
     for j, i in enumerate(take.tolist()):
         c = cuts[i]
         e = (c["offset"].astype(np.uint64) + c["len"].astype(np.uint64)).tolist()
-        bad = e != ref[j].tolist()
-        if hashed and not bad:
-            bad = not np.array_equal(c["hash"], ref_h[k:k + c.size])
-        k += c.size
-        mism += bad
+        mism += e != ref[j].tolist()
     gib = tot / 2**30
-    return {
+    out = {
         "value": round(gib / dt1, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
         "sample": f"first {take.size} files of rank 0's batch ({gib:.2f} GiB), production semantics, "
-                  f"oracle/bup_oracle.c literal compute_file_chunks loop (gcc -O3), "
-                  + ("plus oracle/blake3_oracle.c per chunk (portable C, no SIMD)" if hashed else "chunking only"),
-        "threads_value": round(gib / dtn, 4), "threads": nthr,
+                  f"oracle/bup_oracle.c literal compute_file_chunks loop (gcc -O3), chunking only; "
+                  f"`value` single thread (the reference chunks one file at a time, file_operations.rs:599-605), "
+                  f"`threads_value` one file per thread on `threads` threads",
+        "threads_value": round(gib / dtn, 4), "threads": nthr, **hw,
         "gpu_cuts_match_sample": mism == 0, "sample_files_mismatched": int(mism),
     }
+    if hcuts is not None:
+        co, cn = chunk_offsets(ref)
+        t = time.perf_counter()
+        ref_h = O.blake3_batch(host, co, cn, nthreads=nthr)
+        dth = time.perf_counter() - t
+        hm, k = 0, 0
+        for i in take.tolist():
+            c = hcuts[i]
+            hm += not np.array_equal(c["hash"], ref_h[k:k + c.size])
+            k += c.size
+        out["hashed_threads_value"] = round(gib / (dtn + dth), 4)
+        out["gpu_hashes_match_sample"] = hm == 0 and k == ref_h.shape[0]
+        out["sample_chunks_hashed"] = int(k)
+    return out
+
+
+def fill_dense(dbuf, offs, lens, idx):
+    """Overwrite the adversarial files of --workload dense (see dense_kind)."""
+    pat = periodic_pattern()
+    for j in range(lens.size):
+        k = dense_kind(int(idx[j]))
+        n = int(lens[j])
+        if k == 0 or n == 0:
+            continue
+        if k == 1:
+            a = np.resize(pat, n)
+        else:
+            a = np.full(n, int(idx[j]) & 0xFF, np.uint8)
+        dbuf.upload(a, offset=int(offs[j]))
+
+
+def dry_run(d: Dist, args) -> None:
+    sizes, idx, desc = workload(args.workload, d.world)
+    mine = lpt_shard(sizes, d.world)[d.rank]
+    plan = d.gather({"rank": d.rank, "files": mine.tolist()})
+    if d.rank == 0:
+        allf = np.concatenate([np.array(p["files"], np.int64) for p in plan]) if plan else np.zeros(0, np.int64)
+        loads = [int(sizes[np.array(p["files"], np.int64)].sum()) for p in plan]
+        print(json.dumps({
+            "dry_run": True, "n_gpus": d.world, "workload": args.workload,
+            "shards": [{"rank": p["rank"], "files": len(p["files"]), "bytes": l} for p, l in zip(plan, loads)],
+            "disjoint": bool(np.unique(allf).size == allf.size),
+            "covers_all": bool(np.array_equal(np.sort(allf), np.arange(sizes.size))),
+            "max_over_mean": round(max(loads) / (sum(loads) / len(loads)), 5) if loads and sum(loads) else None,
+            "launcher": os.environ.get("SYNCR_BENCH_LAUNCHER", "env"),
+        }), flush=True)
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "big1"])
+    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "dense", "big1"])
     ap.add_argument("--mode", default="production", choices=["production", "ideal"])
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -203,13 +350,29 @@ def main(argv=None):
                          "(each slot its own engine handle, HIP stream and copy of the corpus, like the "
                          "ingest pipeline's slots); reported as `pipelined`, 1 = skip")
     ap.add_argument("--hashed", action="store_true",
-                    help="also BLAKE3 every chunk on the GPU (SURVEY §8f next #1); reports the "
-                         "chunk+hash rate as its own metric, not the BASELINE metric")
+                    help="make the chunk+BLAKE3 rate the headline (profiling the hash kernels); by default "
+                         "it is reported in the `hashed` sub-object after the headline region")
+    ap.add_argument("--no-hashed", action="store_true", help="skip the `hashed` sub-object")
+    ap.add_argument("--dry-run", action="store_true", help="shard plan only, no device")
+    ap.add_argument("--dev-lib", action="store_true",
+                    help="tools/ only: run against libsyncr_cdc_dev.so (variants / ablations by env)")
     args = ap.parse_args(argv)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        os.environ["SYNCR_BENCH_LAUNCHER"] = "bench.py"
+        return spawn_ranks(args.gpus, argv)
     d = Dist()
     world = d.world
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        dry_run(d, args)
+        d.close()
+        return 0
+
     import syncr_amd
+    if args.dev_lib:
+        syncr_amd.use_dev_library()
     read_cap = syncr_amd.TOKIO_READ_CAP if args.mode == "production" else 0
     ch = syncr_amd.Chunker(syncr_amd.CHUNK_BITS, syncr_amd.MAX_CHUNK_SIZE, read_cap, device=d.local_rank)
 
@@ -228,18 +391,22 @@ def main(argv=None):
                                                  device=d.local_rank)
         b = syncr_amd.DeviceBuffer(h, span)   # own buffer: no slot reads another's bytes from cache
         b.gen_corpus(offs, lens, indices=idx)
+        if args.workload == "dense":
+            fill_dense(b, offs, lens, idx)
         h.plan(offs, lens, span)
         slots.append((h, b))
     ch, dbuf = slots[0]
+    head_hashed = args.hashed
 
-    def run_steps(nslots, steps):
+    def run_steps(nslots, steps, hashed=head_hashed):
         for k in range(steps):
             h, b = slots[k % nslots]
-            h.launch(b.ptr, hashed=args.hashed)
+            h.launch(b.ptr, hashed=hashed)
         for h, _ in slots[:nslots]:
             h.synchronize()
 
     run_steps(1, args.warmup)
+    ch.fetch(hashed=head_hashed)              # settles any capacity re-run before timing
     d.barrier()
     ch.synchronize()
     ch.set_timing(True, scan_only=True)       # HIP events around the scan kernel, on its stream
@@ -255,8 +422,16 @@ def main(argv=None):
     pms, pn = ch.kernel_times()
     ch.set_timing(False)
 
+    dt_max = d.reduce(dt, "max")
+    total_bytes = d.reduce(float(span), "sum")
+    step_s = dt_max / max(args.steps, 1)
+    value = total_bytes / step_s / 2**30
+
     pipelined = None
     if depth > 1:                             # the same K steps with `depth` batches in flight
+        for h, b in slots[1:]:                # settle capacity re-runs before timing
+            h.launch(b.ptr, hashed=head_hashed)
+            h.fetch(hashed=head_hashed)
         run_steps(depth, max(args.warmup, depth))
         d.barrier()
         t0 = time.perf_counter()
@@ -264,19 +439,15 @@ def main(argv=None):
         dtp = d.reduce(time.perf_counter() - t0, "max")
         d.barrier()
         stepp = dtp / max(args.steps, 1)
-        pipelined = {"depth": depth, "value": round(d.reduce(float(span), "sum") / stepp / 2**30, 3),
+        pipelined = {"depth": depth, "value": round(total_bytes / stepp / 2**30, 3),
                      "ms_per_step": round(stepp * 1e3, 4),
                      "note": "same workload and K; step k on slot k % depth, each slot its own handle, "
-                             "HIP stream and corpus copy; per-launch kernel times overlap here, so the "
-                             "roofline is taken from the one-in-flight timed region"}
+                             "HIP stream and corpus copy; a slot's scan waits for the previous slot's scan "
+                             "(scans fill the GPU), the compaction/resolve tails overlap the next scan; "
+                             "the roofline is taken from the one-in-flight timed region"}
 
-    dt_max = d.reduce(dt, "max")
-    total_bytes = d.reduce(float(span), "sum")
-    step_s = dt_max / max(args.steps, 1)
-    value = total_bytes / step_s / 2**30
-
-    cuts = ch.fetch(hashed=args.hashed)
-    slots_agree = all(all(np.array_equal(a, x) for a, x in zip(cuts, h.fetch(hashed=args.hashed)))
+    cuts = ch.fetch(hashed=head_hashed)
+    slots_agree = all(all(np.array_equal(a, x) for a, x in zip(cuts, h.fetch(hashed=head_hashed)))
                       for h, _ in slots[1:])
     stats = ch.last_stats()
     engine_info = ch.info()
@@ -293,7 +464,7 @@ def main(argv=None):
         "kernel": engine_info["scan_kernel"], "kernel_ms": round(scan_ms, 4),
         "algorithmic_bytes_per_launch": span,
         "dense_ms": round(pms[1] / max(pn, 1), 4), "resolve_ms": round(pms[2] / max(pn, 1), 4),
-        "hash_ms": round(pms[3] / max(pn, 1), 4) if args.hashed else None,
+        "hash_ms": round(pms[3] / max(pn, 1), 4) if head_hashed else None,
         "traffic_source": (tr.get("source") if tr else None),
     }
     if not args.no_read_probe and span >= 16:
@@ -309,24 +480,62 @@ def main(argv=None):
         roofline["frac_of_measured"] = round(achieved / peak_meas, 4) if peak_meas else None
         roofline["read_probe"] = dict(probe, kernel="cdc_read_probe_kernel (syncr_cdc_read_probe), 10 passes "
                                                     "over the corpus buffer, 16 B loads, no writes")
+
+    # complete ChunkInfo records (boundaries + BLAKE3 of every chunk, the
+    # hash_binary call at file_operations.rs:757): timed after the headline
+    # region, on the same corpus, one batch in flight
+    hashed = None
+    hcuts = None
+    if not args.no_hashed and not head_hashed:
+        run_steps(1, max(1, min(args.warmup, 3)), hashed=True)
+        ch.fetch(hashed=True)
+        d.barrier()
+        ch.synchronize()
+        t0 = time.perf_counter()
+        run_steps(1, args.steps, hashed=True)
+        dth = d.reduce(time.perf_counter() - t0, "max")
+        d.barrier()
+        ch.set_timing(True)
+        run_steps(1, min(args.steps, 5), hashed=True)
+        hms, hn = ch.kernel_times()
+        ch.set_timing(False)
+        hcuts = ch.fetch(hashed=True)
+        steph = dth / max(args.steps, 1)
+        hash_ms = hms[3] / max(hn, 1)
+        htr = load_traffic(args.workload, span, engine_info["run_bytes"], kernel="cdc::b3_leaf_kernel")
+        hashed = {
+            "metric": METRIC_HASHED, "value": round(total_bytes / steph / 2**30, 3), "unit": "GiB/s",
+            "ms_per_step": round(steph * 1e3, 4), "hash_ms": round(hash_ms, 4),
+            "scan_ms": round(hms[0] / max(hn, 1), 4),
+            "hash_rate_gbs": round(span / (hash_ms / 1e3) / 1e9, 1) if hash_ms > 0 else None,
+            "cuts_agree_with_headline": all(np.array_equal(a[f], x[f]) for a, x in zip(hcuts, cuts)
+                                            for f in ("offset", "len", "file")),
+            "leaf_traffic_over_algorithmic": (round(htr["hbm_bytes_per_launch"] / span, 4) if htr else None),
+            "leaf_traffic_source": (htr.get("source") if htr else None),
+            "sample_check": "cpu_baseline.gpu_hashes_match_sample (rank 0, N=1)",
+        }
+
     cpu = None
     if d.rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(ch, dbuf, offs, lens, cuts, args.cpu_sample_gib, hashed=args.hashed)
+        cpu = cpu_baseline(dbuf, offs, lens, cuts, hcuts, args.cpu_sample_gib)
     for h, b in slots:
         b.free()
         h.close()
 
     if d.rank == 0:
         out = {
-            "metric": METRIC_HASHED if args.hashed else METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+            "metric": METRIC_HASHED if head_hashed else METRIC, "value": round(value, 3), "unit": "GiB/s",
+            "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic: per-file xorshift64 corpus generated in HBM (SURVEY §8d seed rule)",
+            "data": "synthetic: per-file xorshift64 corpus generated in HBM (SURVEY §8d seed rule)"
+                    + ("; adversarial files uploaded from the host (dense_kind)" if args.workload == "dense" else ""),
             "config": {
                 "workload": f"{args.workload}: {desc}", "files_per_gpu": int(lens.size),
                 "bytes_per_gpu": span, "total_bytes": int(total_bytes), "chunk_bits": 20,
                 "max_chunk": syncr_amd.MAX_CHUNK_SIZE, "read_cap": read_cap, "mode": args.mode,
-                "parallelism": f"file-sharded x{world} (LPT), one HIP stream per GPU, no collective",
+                "parallelism": f"file-sharded x{world} (LPT), one process + HIP stream per GPU, no collective",
+                "launcher": os.environ.get("SYNCR_BENCH_LAUNCHER", "torchrun/env" if world > 1 else "none"),
                 "slots_agree_rank0": slots_agree,
                 "cuts_rank0": ncuts, "coverage_ok_rank0": covered,
                 "candidates_rank0": int(stats["candidates"]), "dense_tiles_rank0": int(stats["dense_tiles"]),
@@ -335,10 +544,17 @@ def main(argv=None):
             "roofline": roofline,
             "cpu_baseline": cpu,
             "pipelined": pipelined,
+            "hashed": hashed,
         }
+        if args.workload == "dense":
+            kinds = np.array([dense_kind(int(i)) for i in idx.tolist()])
+            out["config"]["adversarial_bytes_frac"] = {
+                "periodic64": round(float(lens[kinds == 1].sum()) / max(span, 1), 4),
+                "constant": round(float(lens[kinds == 2].sum()) / max(span, 1), 4)}
         print(json.dumps(out), flush=True)
     d.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

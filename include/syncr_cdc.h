@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SYNCR_CDC_ABI_VERSION 2
+#define SYNCR_CDC_ABI_VERSION 3
 
 /* error codes (negative errno values) */
 #define SYNCR_CDC_OK 0
@@ -39,12 +39,16 @@ extern "C" {
 #define SYNCR_CDC_EIO (-5)     /* HIP runtime error while running                 */
 #define SYNCR_CDC_ESTATE (-71) /* call out of order (e.g. launch before plan)    */
 #define SYNCR_CDC_ENOENT (-2)  /* chunk cache: no valid entry                     */
+#define SYNCR_CDC_EBUSY (-16)  /* chunk cache: the log is locked by another handle */
 
 /* Chunker parameters.  Defaults mirror src/chunking.rs:7-13 and the production
- * read path of file_operations.rs:737-776. */
+ * read path of file_operations.rs:737-776.  `flags` selects an exact
+ * alternative resolve (same cuts; for cross-checks only): */
+#define SYNCR_CDC_FLAG_RESOLVE_LANE 1u    /* one lane per file instead of one wave */
+#define SYNCR_CDC_FLAG_RESOLVE_NOBURST 2u /* wave resolve without the chained-hop burst */
 typedef struct syncr_cdc_params {
     uint32_t chunk_bits; /* CHUNK_BITS, 1..31 (default 20; reference validates 8..32) */
-    uint32_t flags;      /* reserved, must be 0                                       */
+    uint32_t flags;      /* 0, or SYNCR_CDC_FLAG_* (other bits: SYNCR_CDC_EINVAL)     */
     uint64_t max_chunk;  /* MAX_CHUNK_SIZE, 1..2^32-1 (default 16 MiB)                  */
     uint64_t read_cap;   /* bytes per tokio File::read (default 2 MiB); 0 = "ideal"
                             in-memory semantics of tests/chunking_test.rs:170-192       */
@@ -76,7 +80,12 @@ const char *syncr_cdc_strerror(int32_t code);
 void syncr_cdc_default_params(syncr_cdc_params *p);
 int32_t syncr_cdc_device_count(int32_t *n);
 
-/* Replaces Bup::new_with_chunk_bits: one handle per device, parameters fixed. */
+/* Replaces Bup::new_with_chunk_bits: one handle per device, parameters fixed.
+ * The library reads no environment variables: its results depend only on the
+ * parameters and the bytes.  Handles on one device order their scans: a
+ * launch's scan kernel starts after the scan most recently enqueued on that
+ * device by another handle (each scan fills the whole GPU), so several
+ * handles = several batches in flight with only their short tails overlapping. */
 int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **out);
 void syncr_cdc_close(syncr_cdc *h);
 int32_t syncr_cdc_get_params(const syncr_cdc *h, syncr_cdc_params *p);
@@ -151,16 +160,34 @@ int32_t syncr_cdc_format_chunks(const syncr_chunk_info *chunks, uint64_t n, int3
  * on its own stream while the next one fills (`depth` batches in flight).  Each
  * file's ChunkInfo list comes back through `cb`, in submission order, on the
  * thread that called submit / flush.  `status` is 0, or -errno for a file that
- * could not be opened or read (then n = 0: the reference's empty list,
- * file_operations.rs:727-744).  In callbacks chunk.file is 0.  A file larger than
- * batch_bytes gets a batch of its own.  copy_threads: host threads used for
- * large copies / reads into pinned memory (1 = the caller only). */
+ * could not be opened or read, following compute_file_chunks: when the open or
+ * the first read fails n = 0 (the reference's empty list,
+ * file_operations.rs:727-744); when a later read fails, the chunks the
+ * reference cuts before its loop breaks (:776-782).  A file that shrinks while
+ * being read is chunked at the length read (status 0).  In callbacks chunk.file
+ * is 0.  A file larger than batch_bytes gets a batch of its own.  copy_threads:
+ * host threads used for large copies / reads into pinned memory (1 = the caller
+ * only). */
 typedef struct syncr_ingest syncr_ingest;
 typedef void (*syncr_ingest_cb)(void *ctx, uint64_t tag, int32_t status, const syncr_chunk_info *chunks,
                                 uint64_t n);
 int32_t syncr_ingest_open(int32_t device, const syncr_cdc_params *p, uint64_t batch_bytes, uint32_t depth,
                           uint32_t copy_threads, syncr_ingest_cb cb, void *ctx, syncr_ingest **out);
-/* bytes already in memory (copied into the staging batch) */
+/* One pipeline over several devices of this process (the reference's host is
+ * one process, src/protocol/factory.rs:116-125): devices[k] is the HIP device
+ * of sub-pipeline k (a device may repeat: two sub-pipelines on one GPU).  Each
+ * sub-pipeline has its own `depth` staging batches, engine handles and streams,
+ * and its own worker thread, which reads / copies its files and runs its
+ * batches.  Each file goes whole to the sub-pipeline with the fewest bytes
+ * assigned so far (files are independent, file_operations.rs:721-788: the
+ * online form of LPT by size; no cross-device traffic).  Callbacks still arrive
+ * in submission order, on the thread that called submit / flush.  Every
+ * syncr_ingest_* call takes the returned handle; syncr_ingest_open is the
+ * one-device case (no worker thread). */
+int32_t syncr_ingest_open_multi(const int32_t *devices, uint32_t ndevices, const syncr_cdc_params *p,
+                                uint64_t batch_bytes, uint32_t depth, uint32_t copy_threads,
+                                syncr_ingest_cb cb, void *ctx, syncr_ingest **out);
+/* bytes already in memory (copied into the staging batch before returning) */
 int32_t syncr_ingest_submit(syncr_ingest *g, const uint8_t *data, uint64_t len, uint64_t tag);
 /* a file read with pread straight into pinned staging */
 int32_t syncr_ingest_submit_file(syncr_ingest *g, const char *path, uint64_t tag);
@@ -171,18 +198,30 @@ int32_t syncr_ingest_commit(syncr_ingest *g, uint64_t tag);
 int32_t syncr_ingest_flush(syncr_ingest *g);
 /* [files, bytes, batches, chunks] so far */
 int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4);
+/* per sub-pipeline k: stats[4k..4k+3] = [device, files, bytes, batches];
+ * SYNCR_CDC_ERANGE if n < 4 * ndevices */
+int32_t syncr_ingest_device_stats(const syncr_ingest *g, uint64_t *stats, uint32_t n);
 void syncr_ingest_close(syncr_ingest *g);
 
 /* --- chunk cache (skip re-chunking unchanged files) ---------------------------
  * Restates ChildCache (src/cache.rs:138-260): one entry per key (file path) with
  * the file's mtime, size and ChunkInfo list; valid when mtime (cache.rs:167-179)
- * and size both match.  Persistent in an append-only log at `path` (NULL = in
- * memory only); a torn tail is dropped on open.  get: 0 on a hit,
- * SYNCR_CDC_ENOENT on a miss, SYNCR_CDC_ERANGE (n_out = needed) if cap is short.
- * Attached to an ingest pipeline, submit_file serves unchanged files from it and
- * stores every freshly chunked file in it. */
+ * and size both match.  A cache holds chunk lists cut under ONE set of chunking
+ * parameters `p` (NULL = defaults; flags are ignored): the reference's are
+ * compile-time constants (src/chunking.rs:7-13), these are runtime values, so
+ * they are part of the cache's identity.  Persistent in an append-only log at
+ * `path` (NULL = in memory only) that records them in its header; opening a log
+ * written under other parameters gives SYNCR_CDC_EINVAL, a file that is not a
+ * cache log SYNCR_CDC_EIO, a log locked by another open handle SYNCR_CDC_EBUSY.
+ * An empty file (or one torn while its header was written) is a new cache; a
+ * torn tail is dropped on open; a failed append is rolled back and makes later
+ * puts fail with SYNCR_CDC_EIO.  get: 0 on a hit, SYNCR_CDC_ENOENT on a miss,
+ * SYNCR_CDC_ERANGE (n_out = needed) if cap is short.  Attached to an ingest
+ * pipeline (same parameters, else SYNCR_CDC_EINVAL), submit_file serves
+ * unchanged files from it and stores every freshly chunked file in it. */
 typedef struct syncr_cache syncr_cache;
-int32_t syncr_cache_open(const char *path, syncr_cache **out);
+int32_t syncr_cache_open(const char *path, const syncr_cdc_params *p, syncr_cache **out);
+int32_t syncr_cache_get_params(const syncr_cache *c, syncr_cdc_params *p);
 int32_t syncr_cache_get(syncr_cache *c, const char *key, uint32_t mtime, uint64_t size, syncr_chunk_info *out,
                         uint64_t cap, uint64_t *n_out);
 int32_t syncr_cache_put(syncr_cache *c, const char *key, uint32_t mtime, uint64_t size,

@@ -148,6 +148,41 @@ uint64_t orc_chunk_production(const uint8_t *file, uint64_t F, uint32_t bits,
     return sk.n;
 }
 
+/*
+ * compute_file_chunks over a file whose bytes from offset P on cannot be read:
+ * each read returns the bytes before P it asks for (a short read at P), and a
+ * non-empty read starting at P fails, which breaks the loop (:776-782) and drops
+ * whatever was buffered but not yet cut.  P = 0: the first read fails (:738-743),
+ * no chunks.  Checks the ingest pipeline's read_error_keep rule (ingest_logic.h).
+ */
+uint64_t orc_chunk_production_read_error(const uint8_t *file, uint64_t P, uint32_t bits,
+                                         uint64_t max_chunk, uint64_t read_cap,
+                                         uint64_t *ends, uint64_t ends_cap) {
+    sink_t sk = {ends, ends_cap, 0};
+    if (P == 0) return 0;
+    uint8_t *buf = (uint8_t *)malloc(max_chunk);
+    if (!buf) return UINT64_MAX;
+    uint64_t fpos = 0;
+    uint64_t n = emu_read(file, P, &fpos, buf, max_chunk, read_cap);
+    uint64_t offset = 0;
+    bup_t b;
+    while (n > 0) {
+        bup_init(&b, bits);
+        uint64_t endofs = max_chunk;
+        if (endofs > n) endofs = n;
+        uint64_t edge = bup_find_chunk_edge(&b, buf, endofs);
+        uint64_t count = edge ? edge : endofs;
+        sink_push(&sk, offset + count);
+        memmove(buf, buf + count, n - count);
+        offset += count;
+        n -= count;
+        if (max_chunk - n > 0 && fpos == P) break;       /* the read at P fails */
+        n += emu_read(file, P, &fpos, buf + n, max_chunk - n, read_cap);
+    }
+    free(buf);
+    return sk.n;
+}
+
 /* chunk_data (tests/chunking_test.rs:170-192): in-memory "ideal" semantics. */
 uint64_t orc_chunk_ideal(const uint8_t *data, uint64_t len, uint32_t bits,
                          uint64_t max_chunk, uint64_t *ends, uint64_t ends_cap) {

@@ -55,11 +55,16 @@ EXPORTED_SYMBOLS = (
     "syncr_ingest_commit", "syncr_ingest_flush", "syncr_ingest_stats", "syncr_ingest_close",
     "syncr_cache_open", "syncr_cache_get", "syncr_cache_put", "syncr_cache_sync", "syncr_cache_stats",
     "syncr_cache_close", "syncr_ingest_set_cache", "syncr_ingest_cache_hits",
+    "syncr_ingest_open_multi", "syncr_ingest_device_stats", "syncr_cache_get_params",
 )
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 E_RANGE = -34
 E_NOENT = -2
+E_BUSY = -16
+E_INVAL = -22
+FLAG_RESOLVE_LANE = 1       # exact alternative resolves (include/syncr_cdc.h SYNCR_CDC_FLAG_*)
+FLAG_RESOLVE_NOBURST = 2
 FMT_LIST_LINES = 1      # LIST reply "C" lines (src/protocol/v3_server.rs:146-182)
 FMT_HASHCHUNKS = 2      # profile FileData "ch" array (src/types.rs:117-129)
 
@@ -91,6 +96,17 @@ _vp, _u64, _u32, _i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctype
 _pu64 = ctypes.POINTER(ctypes.c_uint64)
 # syncr_ingest_cb(ctx, tag, status, const syncr_chunk_info *chunks, n)
 _INGEST_CB = ctypes.CFUNCTYPE(None, _vp, _u64, _i32, _vp, _u64)
+
+
+def use_dev_library() -> None:
+    """tools/ only: load libsyncr_cdc_dev.so (python -m syncr_amd.build --dev)
+    instead of the product library.  It adds scan variants and timing-only
+    ablations chosen by SYNCR_CDC_* / SYNCR_B3_* environment variables; the
+    product library reads no environment.  Must run before the first library()."""
+    global library_path
+    if _lib is not None:
+        raise RuntimeError("syncr_amd: library already loaded")
+    library_path = os.path.join(_PKG, "libsyncr_cdc_dev.so")
 
 
 def library():
@@ -144,7 +160,11 @@ def library():
             "syncr_ingest_flush": ([_vp], _i32),
             "syncr_ingest_stats": ([_vp, _pu64], _i32),
             "syncr_ingest_close": ([_vp], None),
-            "syncr_cache_open": ([ctypes.c_char_p, ctypes.POINTER(_vp)], _i32),
+            "syncr_cache_open": ([ctypes.c_char_p, ctypes.POINTER(Params), ctypes.POINTER(_vp)], _i32),
+            "syncr_cache_get_params": ([_vp, ctypes.POINTER(Params)], _i32),
+            "syncr_ingest_open_multi": ([ctypes.POINTER(_i32), _u32, ctypes.POINTER(Params), _u64, _u32, _u32,
+                                         _INGEST_CB, _vp, ctypes.POINTER(_vp)], _i32),
+            "syncr_ingest_device_stats": ([_vp, _pu64, _u32], _i32),
             "syncr_cache_get": ([_vp, ctypes.c_char_p, _u32, _u64, _vp, _u64, _pu64], _i32),
             "syncr_cache_put": ([_vp, ctypes.c_char_p, _u32, _u64, _vp, _u64], _i32),
             "syncr_cache_sync": ([_vp], _i32),
@@ -196,9 +216,9 @@ class Chunker:
     """One engine handle on one device (Bup::new_with_chunk_bits, fixed params)."""
 
     def __init__(self, chunk_bits: int = CHUNK_BITS, max_chunk: int = MAX_CHUNK_SIZE,
-                 read_cap: int = TOKIO_READ_CAP, device: int = 0):
+                 read_cap: int = TOKIO_READ_CAP, device: int = 0, flags: int = 0):
         L = library()
-        self.params = Params(chunk_bits, 0, max_chunk, read_cap)
+        self.params = Params(chunk_bits, flags, max_chunk, read_cap)
         h = _vp()
         _check(L.syncr_cdc_open(device, ctypes.byref(self.params), ctypes.byref(h)), "syncr_cdc_open")
         self._h = h
@@ -394,12 +414,16 @@ def format_chunks(chunks: np.ndarray, fmt: int = FMT_LIST_LINES) -> bytes:
 class ChunkCache:
     """Persistent chunk cache (syncr_cache_*), the reference's ChildCache
     (src/cache.rs:138-260): per key (file path) the file's mtime, size and
-    ChunkInfo list; valid when mtime (cache.rs:175) and size match.  Host code:
+    ChunkInfo list; valid when mtime (cache.rs:175) and size match.  Bound to
+    one set of chunking parameters (stored in the log header).  Host code:
     works without a GPU."""
 
-    def __init__(self, path: Optional[str] = None):
+    def __init__(self, path: Optional[str] = None, chunk_bits: int = CHUNK_BITS, max_chunk: int = MAX_CHUNK_SIZE,
+                 read_cap: int = TOKIO_READ_CAP):
         h = _vp()
-        _check(library().syncr_cache_open(os.fsencode(path) if path else None, ctypes.byref(h)), "syncr_cache_open")
+        self.params = Params(chunk_bits, 0, max_chunk, read_cap)
+        _check(library().syncr_cache_open(os.fsencode(path) if path else None, ctypes.byref(self.params),
+                                          ctypes.byref(h)), "syncr_cache_open")
         self._h = h
 
     @property
@@ -459,11 +483,14 @@ class Ingest:
     per-file await.  Files go into pinned staging batches; each sealed batch is
     chunked + hashed on the GPU while the next fills.  Results arrive in
     submission order as (tag, status, ChunkInfo structured array) through
-    `on_file`, or are collected in `.results` when no callback is given."""
+    `on_file`, or are collected in `.results` when no callback is given.
+    devices=[d0, d1, ...]: one sub-pipeline and worker thread per listed device
+    (syncr_ingest_open_multi), files assigned whole to the least-loaded one."""
 
     def __init__(self, chunk_bits: int = CHUNK_BITS, max_chunk: int = MAX_CHUNK_SIZE,
                  read_cap: int = TOKIO_READ_CAP, device: int = 0, batch_bytes: int = 256 << 20,
-                 depth: int = 3, copy_threads: int = 8, on_file=None, cache: Optional["ChunkCache"] = None):
+                 depth: int = 3, copy_threads: int = 8, on_file=None, cache: Optional["ChunkCache"] = None,
+                 devices: Optional[Sequence[int]] = None):
         L = library()
         self.params = Params(chunk_bits, 0, max_chunk, read_cap)
         self.results: list[tuple[int, int, np.ndarray]] = []
@@ -480,8 +507,15 @@ class Ingest:
 
         self._cb = _INGEST_CB(cb)           # keep alive for the handle's lifetime
         h = _vp()
-        _check(L.syncr_ingest_open(device, ctypes.byref(self.params), batch_bytes, depth, copy_threads,
-                                   self._cb, None, ctypes.byref(h)), "syncr_ingest_open")
+        if devices is None:
+            _check(L.syncr_ingest_open(device, ctypes.byref(self.params), batch_bytes, depth, copy_threads,
+                                       self._cb, None, ctypes.byref(h)), "syncr_ingest_open")
+            self.devices = [device]
+        else:
+            self.devices = [int(d) for d in devices]
+            arr = (_i32 * len(self.devices))(*self.devices)
+            _check(L.syncr_ingest_open_multi(arr, len(self.devices), ctypes.byref(self.params), batch_bytes, depth,
+                                             copy_threads, self._cb, None, ctypes.byref(h)), "syncr_ingest_open_multi")
         self._h = h
         self._cache = cache                  # keep alive while attached
         if cache is not None:
@@ -515,6 +549,14 @@ class Ingest:
         hits = ctypes.c_uint64(0)
         _check(library().syncr_ingest_cache_hits(self._h, ctypes.byref(hits)), "syncr_ingest_cache_hits")
         return {"files": st[0], "bytes": st[1], "batches": st[2], "chunks": st[3], "cache_hits": hits.value}
+
+    def device_stats(self) -> list[dict]:
+        """Per sub-pipeline: device, files, bytes, batches."""
+        n = 4 * len(self.devices)
+        st = (ctypes.c_uint64 * n)()
+        _check(library().syncr_ingest_device_stats(self._h, st, n), "syncr_ingest_device_stats")
+        return [{"device": st[4 * k], "files": st[4 * k + 1], "bytes": st[4 * k + 2], "batches": st[4 * k + 3]}
+                for k in range(len(self.devices))]
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -623,6 +623,9 @@ static void launch_leaf(int device, const uint8_t *d, const Tables &t, const Has
     hipLaunchKernelGGL((b3_leaf_kernel<NT, AB, CO>), dim3((uint32_t)(cus * per)), dim3(256), 0, s, d, t, ht);
 }
 
+#ifdef SYNCR_CDC_DEV
+// development library only: per-lane loads, non-temporal loads and the
+// timing-only ablations (loads only / no loads), selected by SYNCR_B3_* variables
 template <bool CO>
 static hipError_t launch_leaf_v(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
     switch (ht.ablate * 2 + (ht.nt ? 1 : 0)) {
@@ -635,14 +638,19 @@ static hipError_t launch_leaf_v(int device, const uint8_t *d, const Tables &t, c
     }
     return hipSuccess;
 }
+#endif
 
 hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
     hipError_t e = hipMemsetAsync(ht.ctr, 0, B3C_WORDS * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     if (!t.nfiles) return hipSuccess;
     hipLaunchKernelGGL(b3_items_kernel, dim3((t.nfiles + 255) / 256), dim3(256), 0, s, t, ht);
+#ifdef SYNCR_CDC_DEV
     e = ht.coop ? launch_leaf_v<true>(device, d, t, ht, s) : launch_leaf_v<false>(device, d, t, ht, s);
     if (e != hipSuccess) return e;
+#else
+    launch_leaf<false, 0, true>(device, d, t, ht, s);    // the one exact product instance
+#endif
     const uint64_t want = (ht.trees_cap + 3) / 4;
     const uint32_t blocks = (uint32_t)(want < 4096 ? (want ? want : 1) : 4096);
     hipLaunchKernelGGL(b3_tree_kernel, dim3(blocks), dim3(256), 0, s, t, ht);

@@ -7,6 +7,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -53,9 +55,11 @@ struct syncr_cdc {
     syncr_cdc_params params{};
     KParams kp{};
     hipStream_t stream = nullptr;
+    hipEvent_t scan_done = nullptr;     // recorded after each launch's scan (scan_order)
+    bool serial_scans = true;           // order scans of same-device handles (dev lib: SYNCR_CDC_SERIAL=0)
     // scan kernel and tile geometry: the packed-u16 VALU roll (north_star: integer
-    // work, no MFMA).  The MFMA Toeplitz variant is an opt-in experiment
-    // (SYNCR_CDC_SCAN=mfma).
+    // work, no MFMA).  Other geometries and the MFMA Toeplitz variant exist only
+    // in the development library.
     ScanGeom geom{SCAN_VALU, DEFAULT_RUN, 0};
     uint32_t scan_grid = 0;         // persistent scan grid (CUs x resident blocks)
 
@@ -114,7 +118,7 @@ int32_t hip_err(hipError_t e) {
 int32_t validate_params(const syncr_cdc_params *p) {
     if (!p) return SYNCR_CDC_EINVAL;
     if (p->chunk_bits < 1 || p->chunk_bits > 31) return SYNCR_CDC_EINVAL;
-    if (p->flags != 0) return SYNCR_CDC_EINVAL;
+    if (p->flags & ~(uint32_t)(SYNCR_CDC_FLAG_RESOLVE_LANE | SYNCR_CDC_FLAG_RESOLVE_NOBURST)) return SYNCR_CDC_EINVAL;
     if (p->max_chunk < 1 || p->max_chunk > 0xffffffffull) return SYNCR_CDC_EINVAL;
     return SYNCR_CDC_OK;
 }
@@ -131,7 +135,10 @@ KParams make_kparams(const syncr_cdc_params &p) {
     k.kmv = km | (km << 16);
     k.max_chunk = p.max_chunk;
     k.read_cap = p.read_cap;
-    k.nt = 1;              // tile bytes are read once: non-temporal loads (SYNCR_CDC_NT=0 to disable)
+    k.nt = 1;              // tile bytes are read once: non-temporal loads
+    // exact alternative resolves, for cross-checks (include/syncr_cdc.h)
+    k.resolve_lane = (p.flags & SYNCR_CDC_FLAG_RESOLVE_LANE) ? 1u : 0u;
+    k.resolve_noburst = (p.flags & SYNCR_CDC_FLAG_RESOLVE_NOBURST) ? 1u : 0u;
     return k;
 }
 
@@ -259,7 +266,30 @@ void drain_timing(syncr_cdc *h) {
     h->pending.clear();
 }
 
+// Scan ordering between handles of one device.  The scan is a persistent grid
+// sized to fill every CU (scan_grid = CUs x resident blocks), so two scans in
+// flight on two streams cannot co-reside: they contend for the same slots and
+// HBM, and the later one's waves start piecemeal as the earlier one's retire.
+// With several handles on one device (the ingest pipeline's slots, bench.py's
+// pipelined segment) each launch's scan therefore waits for the scan most
+// recently enqueued on that device by ANOTHER handle; only the short
+// compaction / fix-up / resolve / hash tail of one batch overlaps the next
+// batch's scan.  (Round-1 driver run: two unordered scans in flight made the
+// step 13 % slower than one, BENCH_r01.json `pipelined`.)
+struct ScanOrder {
+    std::mutex mu;
+    const syncr_cdc *owner = nullptr;   // handle whose scan was enqueued last
+    hipEvent_t ev = nullptr;            // its scan_done event
+};
+ScanOrder &scan_order(int device) {
+    static std::mutex reg_mu;
+    static std::map<int, ScanOrder> reg;   // std::map: node addresses are stable
+    std::lock_guard<std::mutex> g(reg_mu);
+    return reg[device];
+}
+
 int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
+    CHECK_HIP(hipSetDevice(h->device));
     KParams kp = h->kp;
     Tables t = make_tables(h);
     PendingTiming pt{};
@@ -269,9 +299,20 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
         for (int k = 0; k < pt.nev; k++) CHECK_HIP(hipEventCreate(&pt.ev[k]));
     }
     CHECK_HIP(hipMemsetAsync(h->zeroed.p, 0, zeroed_bytes(h), s));
+    ScanOrder &so = scan_order(h->device);
+    if (h->serial_scans) {
+        std::lock_guard<std::mutex> g(so.mu);        // held: the owner cannot close its event meanwhile
+        if (so.owner && so.owner != h) CHECK_HIP(hipStreamWaitEvent(s, so.ev, 0));
+    }
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[0], s));
     CHECK_HIP(launch_scan(h->geom, h->scan_grid, d_bytes, kp, t, s));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[1], s));
+    if (h->serial_scans) {
+        std::lock_guard<std::mutex> g(so.mu);
+        CHECK_HIP(hipEventRecord(h->scan_done, s));
+        so.owner = h;
+        so.ev = h->scan_done;
+    }
     // an event record costs ~6 us of queue idle: the scan-only mode records
     // just the two around the scan
     const bool phases = h->timing && !h->timing_scan_only;
@@ -306,6 +347,7 @@ const char *syncr_cdc_strerror(int32_t code) {
         case SYNCR_CDC_EIO: return "HIP runtime error";
         case SYNCR_CDC_ESTATE: return "call out of order";
         case SYNCR_CDC_ENOENT: return "no such entry";
+        case SYNCR_CDC_EBUSY: return "locked by another handle";
         default: return "unknown error";
     }
 }
@@ -343,16 +385,21 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     h->device = device;
     h->params = prm;
     h->kp = make_kparams(prm);
+#ifdef SYNCR_CDC_DEV
+    // Development library only (libsyncr_cdc_dev.so, used by tools/): variants
+    // and timing-only ablations chosen by environment variables.  The product
+    // library reads no environment at all, so no stray variable can change its
+    // results.
     if (const char *a = getenv("SYNCR_CDC_ABLATE")) h->kp.ablate = (uint32_t)atoi(a);  // timing-only
     if (const char *nt = getenv("SYNCR_CDC_NT")) h->kp.nt = (uint32_t)atoi(nt);
     if (const char *rs = getenv("SYNCR_CDC_RESOLVE")) {
         h->kp.resolve_lane = strcmp(rs, "lane") == 0;
         h->kp.resolve_noburst = strcmp(rs, "noburst") == 0;
     }
+    if (const char *a = getenv("SYNCR_CDC_SERIAL")) h->serial_scans = atoi(a) != 0;
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
     if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
     if (const char *ld = getenv("SYNCR_B3_LOAD")) h->b3_coop = strcmp(ld, "plain") != 0;   // A/B only
-    // scan variant (timing / A-B only; every variant is exact)
     if (const char *k = getenv("SYNCR_CDC_SCAN")) {
         if (strcmp(k, "valu") == 0) h->geom = ScanGeom{SCAN_VALU, DEFAULT_RUN, 0};
         if (strcmp(k, "mfma") == 0) h->geom = ScanGeom{SCAN_MFMA, DEFAULT_NB, MFV_SINGLE | MFV_NOPIPE};
@@ -368,15 +415,23 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *v = getenv("SYNCR_CDC_MFVAR")) {    // MFV_* bits of the MFMA scan
         if (h->geom.kind == SCAN_MFMA) h->geom.var = atoi(v) & 3;
     }
+#endif
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
         cus = 256;
     h->scan_grid = (uint32_t)(cus * scan_blocks_per_cu(h->geom));
+#ifdef SYNCR_CDC_DEV
     if (const char *g = getenv("SYNCR_CDC_SCAN_GRID")) {
         const int v = atoi(g);
         if (v > 0) h->scan_grid = (uint32_t)v;
     }
+#endif
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return SYNCR_CDC_EIO;
+    }
+    if (hipEventCreateWithFlags(&h->scan_done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamDestroy(h->stream);
         delete h;
         return SYNCR_CDC_EIO;
     }
@@ -389,6 +444,15 @@ void syncr_cdc_close(syncr_cdc *h) {
     (void)hipSetDevice(h->device);
     (void)hipStreamSynchronize(h->stream);
     drain_timing(h);
+    {
+        ScanOrder &so = scan_order(h->device);
+        std::lock_guard<std::mutex> g(so.mu);
+        if (so.owner == h) {
+            so.owner = nullptr;
+            so.ev = nullptr;
+        }
+        (void)hipEventDestroy(h->scan_done);
+    }
     DevBuf *bufs[] = {&h->fstart, &h->foff, &h->flen, &h->order, &h->cut_base, &h->cut_cap,
                       &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
                       &h->dense_cnt, &h->dense_bits, &h->super_off, &h->cand, &h->cuts,

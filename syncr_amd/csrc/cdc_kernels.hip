@@ -436,8 +436,11 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
     }
 }
 
+#ifdef SYNCR_CDC_DEV
 // ---------------------------------------------------------------------------
-// MFMA scan.  W at position n is a 64-tap FIR of the bytes:
+// MFMA scan (development library only: north_star asks for integer VALU work,
+// and it measured slightly below the VALU scan).
+// W at position n is a 64-tap FIR of the bytes:
 //     W(n) = sum_{a=0..63} (a+1) * x[n-a],    S(n) = sum_{a=0..63} x[n-a]
 // (the closed form of Bup's s2 / s1 recurrences).  For a block of 32
 // positions [32b, 32b+32) of one stream it is a product with three constant
@@ -628,6 +631,7 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
         publish_tile(data, P, T, tile, t0, wlist, wcount, lane, false);
     }
 }
+#endif  // SYNCR_CDC_DEV
 
 // File starts: the scan treats the batch as ONE byte stream, so its G is exact
 // for p >= f+63 inside a file starting at f.  The 63 head positions of a file
@@ -1342,6 +1346,13 @@ hipError_t launch_read_probe(const uint8_t *d, uint64_t bytes, bool nt, uint32_t
 }
 
 // ---------------------------------------------------------------------------
+// Scan instances.  The product library carries exactly one: RUN = DEFAULT_RUN,
+// non-temporal tile loads, dynamic tile groups (MODE 12).  The development
+// library (-DSYNCR_CDC_DEV, libsyncr_cdc_dev.so, tools/ only) adds the other
+// RUN sizes, the static-stride and timing-only ablations and the MFMA scan,
+// selected by environment variables that the product never reads.
+// ---------------------------------------------------------------------------
+#ifdef SYNCR_CDC_DEV
 static bool valu_run_ok(int run) { return run == 48 || run == 80 || run == 112 || run == 144 || run == 176; }
 static bool mfma_nb_ok(int nb) { return nb == 4 || nb == 6 || nb == 8 || nb == 10 || nb == 12; }
 
@@ -1384,26 +1395,17 @@ static const void *scan_kernel_ptr(ScanGeom g) {
     }
 }
 
-int scan_blocks_per_cu(ScanGeom g) {
-    int n = 0;
-    const void *f = scan_kernel_ptr(g);
-    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 64, scan_lds_bytes(g)) != hipSuccess)
-        return 1;
-    return n > 0 ? n : 1;
-}
-
 template <int RUN>
 static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    constexpr bool ABL = RUN == DEFAULT_RUN || RUN == 144;     // ablation instances
     const size_t lds = lds_wave_bytes(RUN);
-    if (ABL && p.ablate == 1u)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, ABL ? 1 : 0>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (ABL && p.ablate == 2u)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, ABL ? 2 : 0>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (ABL && p.ablate == 3u)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, ABL ? 5 : 0>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (ABL && p.ablate == 4u)                                  // A/B: static stride (exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, ABL ? 4 : 12>), dim3(grid), dim3(64), lds, s, d, p, t);
+    if (p.ablate == 1u)                                              // timing only: staging, no roll
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 1>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 2u)                                         // timing only: roll, no DMA
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 3u)                                         // timing only: staging, nt
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 5>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 4u)                                         // A/B: static stride (exact)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 4>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.nt)                                                   // product: nt loads + dynamic groups
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
     else
@@ -1464,6 +1466,30 @@ hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParam
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+#else   // product: one exact scan instance
+bool scan_supported(ScanGeom g) { return g.kind == SCAN_VALU && g.param == DEFAULT_RUN; }
+int scan_tile_bytes(ScanGeom) { return tile_bytes(DEFAULT_RUN); }
+int scan_lds_bytes(ScanGeom) { return lds_wave_bytes(DEFAULT_RUN); }
+static const void *scan_kernel_ptr(ScanGeom) { return (const void *)&cdc_scan_kernel<DEFAULT_RUN, 12>; }
+
+hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
+                       hipStream_t s) {
+    if (!t.ntiles) return hipSuccess;
+    if (!scan_supported(g)) return hipErrorInvalidValue;
+    grid = grid < t.ntiles ? grid : t.ntiles;
+    hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, 12>), dim3(grid), dim3(64), lds_wave_bytes(DEFAULT_RUN), s,
+                       d, p, t);
+    return hipGetLastError();
+}
+#endif
+
+int scan_blocks_per_cu(ScanGeom g) {
+    int n = 0;
+    const void *f = scan_kernel_ptr(g);
+    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 64, scan_lds_bytes(g)) != hipSuccess)
+        return 1;
+    return n > 0 ? n : 1;
 }
 
 hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s,

@@ -8,8 +8,20 @@
 // (hipMemcpyAsync) and chunked + hashed on its own handle/stream while the next
 // batch fills, so file reads (host), PCIe and the GPU kernels overlap.  Results
 // go back per file, in submission order, through the caller's callback on the
-// caller's thread.  An unreadable file yields status -errno and no chunks, like
-// the reference's warn-and-return-empty (:727-744).
+// caller's thread.
+//
+// One `Pipe` is the pipeline of one device.  syncr_ingest_open drives one Pipe
+// on the caller's thread.  syncr_ingest_open_multi drives one Pipe per listed
+// device, each on its own worker thread (the reference's host is ONE process,
+// src/protocol/factory.rs:116-125, so multi-GPU use needs this in-process
+// fan-out): files are assigned whole to the least-loaded device (ingest_logic.h)
+// and the results are put back into submission order before any callback.
+//
+// Read failures follow compute_file_chunks: a file that cannot be opened, or
+// whose first read fails, yields -errno and no chunks (:727-744); a read that
+// fails later breaks the loop and keeps the chunks cut so far (:776-782,
+// ingest_logic.h read_error_keep); a file that shrank is chunked at the length
+// actually read (reads stop at EOF).
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
@@ -17,9 +29,11 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <new>
@@ -28,6 +42,7 @@
 #include <vector>
 
 #include "../../include/syncr_cdc.h"
+#include "ingest_logic.h"
 
 namespace {
 
@@ -46,7 +61,6 @@ class Pool {
         cv_.notify_all();
         for (auto &t : th_) t.join();
     }
-    unsigned size() const { return (unsigned)th_.size(); }
     // run fn(0..n-1) on the pool plus the calling thread; returns when all done
     void parallel(unsigned n, const std::function<void(unsigned)> &fn) {
         if (n <= 1 || th_.empty()) {
@@ -111,6 +125,7 @@ struct Slot {
     uint64_t cap = 0, used = 0;
     std::vector<uint64_t> off, len, tag;
     std::vector<int32_t> status;
+    std::vector<uint8_t> trunc;       // read error after len > 0 bytes: keep the reference's prefix
     // chunk cache: per file, the key to store the result under ("" = none) and
     // its (mtime, size); a cache hit carries its chunks in cbuf[cstart, +ccount)
     std::vector<std::string> key;
@@ -127,26 +142,25 @@ struct Slot {
 constexpr uint64_t PAR_COPY = 4ull << 20;   // copies above this are split over the pool
 constexpr uint64_t PIECE = 2ull << 20;
 
-}  // namespace
+typedef void (*deliver_fn)(void *owner, uint64_t tag, int32_t status, const syncr_chunk_info *chunks, uint64_t n);
 
-struct syncr_ingest {
+// The pipeline of one device (all calls on one thread at a time).
+struct Pipe {
     int32_t device = 0;
     syncr_cdc_params params{};
     uint64_t batch = 0;
     std::vector<Slot> slots;
     uint32_t cur = 0;
-    syncr_ingest_cb cb = nullptr;
-    void *ctx = nullptr;
+    deliver_fn deliver = nullptr;
+    void *owner = nullptr;
     Pool *pool = nullptr;
     bool reserved = false;           // reserve() outstanding on slots[cur]
     uint64_t reserved_len = 0;
-    uint64_t stats[4] = {0, 0, 0, 0};   // files, bytes, batches, chunks
+    std::atomic<uint64_t> stats[4] = {{0}, {0}, {0}, {0}};   // files, bytes, batches, chunks
     int32_t error = 0;                  // sticky engine error
     syncr_cache *cache = nullptr;       // optional (syncr_ingest_set_cache)
-    uint64_t cache_hits = 0;
+    std::atomic<uint64_t> cache_hits{0};
 };
-
-namespace {
 
 int32_t hip_rc(hipError_t e) {
     if (e == hipSuccess) return SYNCR_CDC_OK;
@@ -154,7 +168,7 @@ int32_t hip_rc(hipError_t e) {
     return SYNCR_CDC_EIO;
 }
 
-void free_slot_buffers(syncr_ingest *g, Slot &s) {
+void free_slot_buffers(Pipe *g, Slot &s) {
     (void)hipSetDevice(g->device);
     if (s.host) (void)hipHostFree(s.host);
     if (s.dev) (void)hipFree(s.dev);
@@ -162,11 +176,12 @@ void free_slot_buffers(syncr_ingest *g, Slot &s) {
     s.cap = 0;
 }
 
-int32_t ensure_slot(syncr_ingest *g, Slot &s, uint64_t bytes) {
+int32_t ensure_slot(Pipe *g, Slot &s, uint64_t bytes) {
     if (bytes <= s.cap && s.host) return SYNCR_CDC_OK;
     free_slot_buffers(g, s);
     const uint64_t want = std::max<uint64_t>(bytes, 64);
-    hipError_t e = hipHostMalloc((void **)&s.host, want, hipHostMallocDefault);
+    hipError_t e = hipSetDevice(g->device);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&s.host, want, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc((void **)&s.dev, want);
     if (e != hipSuccess) {
         free_slot_buffers(g, s);
@@ -176,7 +191,7 @@ int32_t ensure_slot(syncr_ingest *g, Slot &s, uint64_t bytes) {
     return SYNCR_CDC_OK;
 }
 
-void par_copy(syncr_ingest *g, uint8_t *dst, const uint8_t *src, uint64_t n) {
+void par_copy(Pipe *g, uint8_t *dst, const uint8_t *src, uint64_t n) {
     if (n <= PAR_COPY || !g->pool) {
         memcpy(dst, src, n);
         return;
@@ -189,7 +204,7 @@ void par_copy(syncr_ingest *g, uint8_t *dst, const uint8_t *src, uint64_t n) {
 }
 
 // wait for a sealed batch, deliver its files in order, reset the slot
-int32_t complete(syncr_ingest *g, Slot &s) {
+int32_t complete(Pipe *g, Slot &s) {
     if (!s.inflight) return SYNCR_CDC_OK;
     s.inflight = false;
     const uint32_t nf = (uint32_t)s.off.size();
@@ -205,6 +220,7 @@ int32_t complete(syncr_ingest *g, Slot &s) {
         return rc;
     }
     uint64_t o = 0;
+    std::vector<uint64_t> ends;
     for (uint32_t i = 0; i < nf; i++) {
         const syncr_chunk_info *ci;
         uint64_t c;
@@ -212,13 +228,24 @@ int32_t complete(syncr_ingest *g, Slot &s) {
             c = s.ccount[i];
             ci = c ? s.cbuf.data() + s.cstart[i] : nullptr;
         } else {
-            c = s.status[i] ? 0 : s.counts[i];
+            c = s.counts[i];
             for (uint64_t k = 0; k < c; k++) s.out[o + k].file = 0;   // one file per callback
             ci = c ? s.out.data() + o : nullptr;
-            if (g->cache && !s.status[i] && !s.key[i].empty())
+            if (s.status[i]) {
+                if (s.trunc[i]) {                              // read error after len bytes: the reference's prefix
+                    ends.resize(c);
+                    for (uint64_t k = 0; k < c; k++) ends[k] = ci[k].offset + ci[k].len;
+                    c = ingest::read_error_keep(ends.data(), c, s.len[i], g->params.max_chunk,
+                                                g->params.read_cap);
+                } else {
+                    c = 0;
+                }
+                if (!c) ci = nullptr;
+            } else if (g->cache && !s.key[i].empty()) {
                 (void)syncr_cache_put(g->cache, s.key[i].c_str(), s.mtime[i], s.fsize[i], ci, c);
+            }
         }
-        if (g->cb) g->cb(g->ctx, s.tag[i], s.status[i], ci, c);
+        if (g->deliver) g->deliver(g->owner, s.tag[i], s.status[i], ci, c);
         o += s.counts[i];
         g->stats[3] += c;
     }
@@ -226,6 +253,7 @@ int32_t complete(syncr_ingest *g, Slot &s) {
     s.len.clear();
     s.tag.clear();
     s.status.clear();
+    s.trunc.clear();
     s.key.clear();
     s.mtime.clear();
     s.fsize.clear();
@@ -237,7 +265,7 @@ int32_t complete(syncr_ingest *g, Slot &s) {
     return SYNCR_CDC_OK;
 }
 
-int32_t seal(syncr_ingest *g, Slot &s) {
+int32_t seal(Pipe *g, Slot &s) {
     if (s.off.empty()) return SYNCR_CDC_OK;
     int32_t rc = syncr_cdc_plan(s.h, s.off.data(), s.len.data(), (uint32_t)s.off.size(), s.used);
     if (rc) return g->error = rc;
@@ -252,7 +280,7 @@ int32_t seal(syncr_ingest *g, Slot &s) {
 }
 
 // make slots[cur] ready to take `len` more bytes (sealing / completing as needed)
-int32_t room(syncr_ingest *g, uint64_t len) {
+int32_t room(Pipe *g, uint64_t len) {
     Slot *s = &g->slots[g->cur];
     if (s->used && s->used + len > s->cap) {
         int32_t rc = seal(g, *s);
@@ -266,58 +294,67 @@ int32_t room(syncr_ingest *g, uint64_t len) {
     return SYNCR_CDC_OK;
 }
 
-void record(Slot &s, uint64_t len, uint64_t tag, int32_t status, const char *key = nullptr,
+// len bytes at s.used belong to this file (also for a truncated read); status
+// != 0 with trunc = 0 means no chunks at all
+void record(Slot &s, uint64_t len, uint64_t tag, int32_t status, bool trunc = false, const char *key = nullptr,
             uint32_t mtime = 0, uint64_t fsize = 0) {
     s.off.push_back(s.used);
-    s.len.push_back(status ? 0 : len);
+    s.len.push_back(len);
     s.tag.push_back(tag);
     s.status.push_back(status);
+    s.trunc.push_back(trunc ? 1 : 0);
     s.key.emplace_back(key ? key : "");
     s.mtime.push_back(mtime);
     s.fsize.push_back(fsize);
     s.hit.push_back(0);
     s.cstart.push_back(0);
     s.ccount.push_back(0);
-    if (!status) s.used += len;
+    s.used += len;
 }
 
-}  // namespace
+void pipe_close(Pipe *g) {
+    if (!g) return;
+    for (Slot &s : g->slots) {
+        if (s.h) {
+            (void)syncr_cdc_synchronize(s.h);
+            syncr_cdc_close(s.h);
+        }
+        free_slot_buffers(g, s);
+    }
+    delete g->pool;
+    delete g;
+}
 
-extern "C" {
-
-int32_t syncr_ingest_open(int32_t device, const syncr_cdc_params *p, uint64_t batch_bytes, uint32_t depth,
-                          uint32_t copy_threads, syncr_ingest_cb cb, void *ctx, syncr_ingest **out) {
-    if (!out) return SYNCR_CDC_EINVAL;
-    *out = nullptr;
-    if (depth < 1 || depth > 8 || batch_bytes < 4096) return SYNCR_CDC_EINVAL;
-    syncr_ingest *g = new (std::nothrow) syncr_ingest();
+int32_t pipe_open(int32_t device, const syncr_cdc_params &p, uint64_t batch_bytes, uint32_t depth,
+                  uint32_t copy_threads, deliver_fn deliver, void *owner, Pipe **out) {
+    Pipe *g = new (std::nothrow) Pipe();
     if (!g) return SYNCR_CDC_ENOMEM;
     g->device = device;
-    if (p) g->params = *p; else syncr_cdc_default_params(&g->params);
+    g->params = p;
     g->batch = batch_bytes;
-    g->cb = cb;
-    g->ctx = ctx;
+    g->deliver = deliver;
+    g->owner = owner;
     try {
         g->slots.resize(depth);
         for (Slot &s : g->slots) {
             int32_t rc = syncr_cdc_open(device, &g->params, &s.h);
             if (rc == SYNCR_CDC_OK) rc = ensure_slot(g, s, batch_bytes);
             if (rc) {
-                syncr_ingest_close(g);
+                pipe_close(g);
                 return rc;
             }
         }
         if (copy_threads > 1) g->pool = new Pool(std::min<uint32_t>(copy_threads, 64) - 1);
     } catch (...) {
-        syncr_ingest_close(g);
+        pipe_close(g);
         return SYNCR_CDC_ENOMEM;
     }
     *out = g;
     return SYNCR_CDC_OK;
 }
 
-int32_t syncr_ingest_reserve(syncr_ingest *g, uint64_t len, uint8_t **dst) {
-    if (!g || !dst || g->reserved) return g ? (g->reserved ? SYNCR_CDC_ESTATE : SYNCR_CDC_EINVAL) : SYNCR_CDC_EINVAL;
+int32_t pipe_reserve(Pipe *g, uint64_t len, uint8_t **dst) {
+    if (g->reserved) return SYNCR_CDC_ESTATE;
     if (g->error) return g->error;
     int32_t rc = room(g, len);
     if (rc) return rc;
@@ -328,8 +365,7 @@ int32_t syncr_ingest_reserve(syncr_ingest *g, uint64_t len, uint8_t **dst) {
     return SYNCR_CDC_OK;
 }
 
-int32_t syncr_ingest_commit(syncr_ingest *g, uint64_t tag) {
-    if (!g) return SYNCR_CDC_EINVAL;
+int32_t pipe_commit(Pipe *g, uint64_t tag) {
     if (!g->reserved) return SYNCR_CDC_ESTATE;
     g->reserved = false;
     record(g->slots[g->cur], g->reserved_len, tag, 0);
@@ -338,17 +374,15 @@ int32_t syncr_ingest_commit(syncr_ingest *g, uint64_t tag) {
     return SYNCR_CDC_OK;
 }
 
-int32_t syncr_ingest_submit(syncr_ingest *g, const uint8_t *data, uint64_t len, uint64_t tag) {
-    if (!g || (len && !data)) return SYNCR_CDC_EINVAL;
+int32_t pipe_submit(Pipe *g, const uint8_t *data, uint64_t len, uint64_t tag) {
     uint8_t *dst = nullptr;
-    int32_t rc = syncr_ingest_reserve(g, len, &dst);
+    int32_t rc = pipe_reserve(g, len, &dst);
     if (rc) return rc;
     par_copy(g, dst, data, len);
-    return syncr_ingest_commit(g, tag);
+    return pipe_commit(g, tag);
 }
 
-int32_t syncr_ingest_submit_file(syncr_ingest *g, const char *path, uint64_t tag) {
-    if (!g || !path) return SYNCR_CDC_EINVAL;
+int32_t pipe_submit_file(Pipe *g, const char *path, uint64_t tag) {
     if (g->reserved) return SYNCR_CDC_ESTATE;
     if (g->error) return g->error;
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
@@ -390,59 +424,53 @@ int32_t syncr_ingest_submit_file(syncr_ingest *g, const char *path, uint64_t tag
         }
     }
     uint8_t *dst = nullptr;
-    int32_t rc = syncr_ingest_reserve(g, len, &dst);
+    int32_t rc = pipe_reserve(g, len, &dst);
     if (rc) {
         close(fd);
         return rc;
     }
-    // pread straight into pinned memory, split over the pool for big files
-    int err = 0;
-    uint64_t got_total = 0;
-    std::mutex emu;
-    auto read_range = [&](uint64_t a, uint64_t b) {
+    // pread straight into pinned memory, split over the pool for big files.
+    // Per piece: bytes read from its start, and the errno that stopped it (0 =
+    // EOF: the file shrank under us).
+    const unsigned pieces = len ? (unsigned)((len + PIECE - 1) / PIECE) : 0u;
+    std::vector<uint64_t> got(pieces, 0);
+    std::vector<int> perr(pieces, 0);
+    auto read_piece = [&](unsigned i) {
+        const uint64_t a = (uint64_t)i * PIECE, b = std::min<uint64_t>(len, a + PIECE);
         uint64_t pos = a;
         while (pos < b) {
             const ssize_t r = pread(fd, dst + pos, (size_t)(b - pos), (off_t)pos);
             if (r < 0 && errno == EINTR) continue;
-            if (r <= 0) {
-                std::lock_guard<std::mutex> l(emu);
-                if (!err) err = r < 0 ? errno : EIO;   // short file: changed under us
-                return;
-            }
+            if (r < 0) { perr[i] = errno ? errno : EIO; break; }
+            if (r == 0) break;                                   // EOF before st_size
             pos += (uint64_t)r;
         }
-        std::lock_guard<std::mutex> l(emu);
-        got_total += b - a;
+        got[i] = pos - a;
     };
-    if (len > PAR_COPY && g->pool) {
-        const unsigned pieces = (unsigned)((len + PIECE - 1) / PIECE);
-        g->pool->parallel(pieces, [&](unsigned i) {
-            const uint64_t a = (uint64_t)i * PIECE;
-            read_range(a, std::min<uint64_t>(len, a + PIECE));
-        });
-    } else {
-        read_range(0, len);
-    }
+    if (len > PAR_COPY && g->pool) g->pool->parallel(pieces, read_piece);
+    else for (unsigned i = 0; i < pieces; i++) read_piece(i);
     close(fd);
-    g->reserved = false;
-    if (err) {                                       // file_operations.rs:740-743: empty list
-        record(g->slots[g->cur], 0, tag, -err);
-    } else {
-        record(g->slots[g->cur], len, tag, 0, g->cache ? path : nullptr, mt, len);
-        g->stats[1] += len;
+    // the prefix read without a gap: the reference reads sequentially and
+    // stops at the first failure or EOF
+    uint64_t P = 0;
+    int err = 0;
+    for (unsigned i = 0; i < pieces; i++) {
+        P += got[i];
+        const uint64_t want = std::min<uint64_t>(len, (uint64_t)(i + 1) * PIECE) - (uint64_t)i * PIECE;
+        if (got[i] < want) { err = perr[i]; break; }
     }
+    g->reserved = false;
+    if (err) {                                       // file_operations.rs:738-743 (P = 0) / :776-782
+        record(g->slots[g->cur], P, tag, -err, P > 0);
+    } else {                                         // complete, or shrank to P bytes (EOF)
+        record(g->slots[g->cur], P, tag, 0, false, g->cache && P == len ? path : nullptr, mt, len);
+    }
+    g->stats[1] += P;
     g->stats[0]++;
     return SYNCR_CDC_OK;
 }
 
-int32_t syncr_ingest_set_cache(syncr_ingest *g, syncr_cache *c) {
-    if (!g) return SYNCR_CDC_EINVAL;
-    g->cache = c;
-    return SYNCR_CDC_OK;
-}
-
-int32_t syncr_ingest_flush(syncr_ingest *g) {
-    if (!g) return SYNCR_CDC_EINVAL;
+int32_t pipe_flush(Pipe *g) {
     if (g->reserved) return SYNCR_CDC_ESTATE;
     if (g->error) return g->error;
     int32_t rc = seal(g, g->slots[g->cur]);
@@ -457,28 +485,364 @@ int32_t syncr_ingest_flush(syncr_ingest *g) {
     return SYNCR_CDC_OK;
 }
 
+// ---- multi-device front end ------------------------------------------------
+
+struct Result {
+    int32_t status = 0;
+    std::vector<syncr_chunk_info> chunks;
+};
+
+enum JobKind { J_FILE, J_COPY, J_RESERVE, J_COMMIT, J_FLUSH };
+
+struct SyncSlot {                 // a job the caller waits for
+    int32_t rc = 0;
+    uint8_t *dst = nullptr;
+    bool done = false;
+};
+
+struct Job {
+    JobKind kind;
+    std::string path;
+    const uint8_t *data = nullptr;
+    uint64_t len = 0;
+    uint64_t seq = 0;
+    SyncSlot *sync = nullptr;
+};
+
+struct Worker {
+    Pipe *pipe = nullptr;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::deque<Job> q;
+    bool stop = false;
+    int32_t err = 0;
+};
+
+constexpr size_t MAX_QUEUED = 256;   // jobs per worker before submit waits
+
+}  // namespace
+
+struct syncr_ingest {
+    syncr_ingest_cb cb = nullptr;
+    void *ctx = nullptr;
+    std::vector<Pipe *> pipes;
+    bool multi = false;
+    // multi: workers, assignment, in-order delivery
+    std::vector<Worker *> workers;
+    ingest::Assigner *assign = nullptr;
+    ingest::Reorder<Result> reorder;
+    std::deque<uint64_t> tags;        // user tag of seq (next_deliver + k)
+    uint64_t next_seq = 0;
+    bool reserved = false;
+    uint32_t reserve_dev = 0;
+    int32_t error = 0;
+    syncr_cache *cache = nullptr;
+};
+
+namespace {
+
+void deliver_single(void *owner, uint64_t tag, int32_t status, const syncr_chunk_info *c, uint64_t n) {
+    syncr_ingest *g = (syncr_ingest *)owner;
+    if (g->cb) g->cb(g->ctx, tag, status, c, n);
+}
+
+void deliver_multi(void *owner, uint64_t seq, int32_t status, const syncr_chunk_info *c, uint64_t n) {
+    syncr_ingest *g = (syncr_ingest *)owner;
+    Result r;
+    r.status = status;
+    if (n) r.chunks.assign(c, c + n);
+    g->reorder.put(seq, std::move(r));
+}
+
+void worker_main(Worker *w) {
+    (void)hipSetDevice(w->pipe->device);
+    for (;;) {
+        Job j;
+        {
+            std::unique_lock<std::mutex> l(w->mu);
+            w->cv.wait(l, [&] { return w->stop || !w->q.empty(); });
+            if (w->q.empty()) return;                  // stop, queue drained
+            j = std::move(w->q.front());
+            w->q.pop_front();
+        }
+        int32_t rc = SYNCR_CDC_OK;
+        uint8_t *dst = nullptr;
+        Pipe *p = w->pipe;
+        switch (j.kind) {
+            case J_FILE: rc = pipe_submit_file(p, j.path.c_str(), j.seq); break;
+            case J_COPY: rc = pipe_submit(p, j.data, j.len, j.seq); break;
+            case J_RESERVE: rc = pipe_reserve(p, j.len, &dst); break;
+            case J_COMMIT: rc = pipe_commit(p, j.seq); break;
+            case J_FLUSH: rc = pipe_flush(p); break;
+        }
+        {
+            std::lock_guard<std::mutex> l(w->mu);
+            if (rc && !w->err) w->err = rc;
+            if (j.sync) {
+                j.sync->rc = rc;
+                j.sync->dst = dst;
+                j.sync->done = true;
+            }
+        }
+        w->done_cv.notify_all();
+    }
+}
+
+void enqueue(Worker *w, Job j) {
+    std::unique_lock<std::mutex> l(w->mu);
+    w->done_cv.wait(l, [&] { return w->q.size() < MAX_QUEUED; });
+    w->q.push_back(std::move(j));
+    l.unlock();
+    w->cv.notify_one();
+}
+
+int32_t run_sync(Worker *w, Job j) {
+    SyncSlot ss;
+    j.sync = &ss;
+    enqueue(w, std::move(j));
+    std::unique_lock<std::mutex> l(w->mu);
+    w->done_cv.wait(l, [&] { return ss.done; });
+    return ss.rc;
+}
+
+int32_t sticky(syncr_ingest *g) {
+    if (g->error) return g->error;
+    for (Worker *w : g->workers) {
+        std::lock_guard<std::mutex> l(w->mu);
+        if (w->err) return g->error = w->err;
+    }
+    return SYNCR_CDC_OK;
+}
+
+// deliver every result whose predecessors have all been delivered
+void drain(syncr_ingest *g) {
+    Result r;
+    uint64_t seq;
+    while (g->reorder.take(r, seq)) {
+        const uint64_t tag = g->tags.front();
+        g->tags.pop_front();
+        if (g->cb) g->cb(g->ctx, tag, r.status, r.chunks.empty() ? nullptr : r.chunks.data(), r.chunks.size());
+    }
+}
+
+uint64_t new_seq(syncr_ingest *g, uint64_t tag) {
+    g->tags.push_back(tag);
+    return g->next_seq++;
+}
+
+void close_multi(syncr_ingest *g) {
+    for (Worker *w : g->workers) {
+        {
+            std::lock_guard<std::mutex> l(w->mu);
+            w->stop = true;
+        }
+        w->cv.notify_all();
+        if (w->th.joinable()) w->th.join();
+    }
+    for (Worker *w : g->workers) delete w;
+    g->workers.clear();
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t syncr_ingest_open(int32_t device, const syncr_cdc_params *p, uint64_t batch_bytes, uint32_t depth,
+                          uint32_t copy_threads, syncr_ingest_cb cb, void *ctx, syncr_ingest **out) {
+    return syncr_ingest_open_multi(&device, 1, p, batch_bytes, depth, copy_threads, cb, ctx, out);
+}
+
+int32_t syncr_ingest_open_multi(const int32_t *devices, uint32_t ndevices, const syncr_cdc_params *p,
+                                uint64_t batch_bytes, uint32_t depth, uint32_t copy_threads, syncr_ingest_cb cb,
+                                void *ctx, syncr_ingest **out) {
+    if (!out) return SYNCR_CDC_EINVAL;
+    *out = nullptr;
+    if (!devices || ndevices < 1 || ndevices > 64) return SYNCR_CDC_EINVAL;
+    if (depth < 1 || depth > 8 || batch_bytes < 4096) return SYNCR_CDC_EINVAL;
+    syncr_cdc_params prm;
+    if (p) prm = *p; else syncr_cdc_default_params(&prm);
+    syncr_ingest *g = new (std::nothrow) syncr_ingest();
+    if (!g) return SYNCR_CDC_ENOMEM;
+    g->cb = cb;
+    g->ctx = ctx;
+    g->multi = ndevices > 1;
+    try {
+        for (uint32_t k = 0; k < ndevices; k++) {
+            Pipe *pp = nullptr;
+            const int32_t rc = pipe_open(devices[k], prm, batch_bytes, depth, copy_threads,
+                                         g->multi ? deliver_multi : deliver_single, g, &pp);
+            if (rc) {
+                syncr_ingest_close(g);
+                return rc;
+            }
+            g->pipes.push_back(pp);
+        }
+        if (g->multi) {
+            g->assign = new ingest::Assigner(ndevices);
+            for (Pipe *pp : g->pipes) {
+                Worker *w = new Worker();
+                w->pipe = pp;
+                g->workers.push_back(w);
+                w->th = std::thread(worker_main, w);
+            }
+        }
+    } catch (...) {
+        syncr_ingest_close(g);
+        return SYNCR_CDC_ENOMEM;
+    }
+    *out = g;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_ingest_reserve(syncr_ingest *g, uint64_t len, uint8_t **dst) {
+    if (!g || !dst) return SYNCR_CDC_EINVAL;
+    if (!g->multi) return pipe_reserve(g->pipes[0], len, dst);
+    if (g->reserved) return SYNCR_CDC_ESTATE;
+    int32_t rc = sticky(g);
+    if (rc) return rc;
+    const uint32_t d = g->assign->assign(len);
+    Job j{J_RESERVE};
+    j.len = len;
+    SyncSlot ss;
+    j.sync = &ss;
+    Worker *w = g->workers[d];
+    enqueue(w, std::move(j));
+    {
+        std::unique_lock<std::mutex> l(w->mu);
+        w->done_cv.wait(l, [&] { return ss.done; });
+    }
+    drain(g);
+    if (ss.rc) return ss.rc;
+    *dst = ss.dst;
+    g->reserved = true;
+    g->reserve_dev = d;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_ingest_commit(syncr_ingest *g, uint64_t tag) {
+    if (!g) return SYNCR_CDC_EINVAL;
+    if (!g->multi) return pipe_commit(g->pipes[0], tag);
+    if (!g->reserved) return SYNCR_CDC_ESTATE;
+    g->reserved = false;
+    Job j{J_COMMIT};
+    j.seq = new_seq(g, tag);
+    enqueue(g->workers[g->reserve_dev], std::move(j));
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_ingest_submit(syncr_ingest *g, const uint8_t *data, uint64_t len, uint64_t tag) {
+    if (!g || (len && !data)) return SYNCR_CDC_EINVAL;
+    if (!g->multi) return pipe_submit(g->pipes[0], data, len, tag);
+    if (g->reserved) return SYNCR_CDC_ESTATE;
+    int32_t rc = sticky(g);
+    if (rc) return rc;
+    const uint32_t d = g->assign->assign(len);
+    Job j{J_COPY};
+    j.data = data;
+    j.len = len;
+    j.seq = new_seq(g, tag);
+    rc = run_sync(g->workers[d], std::move(j));          // the bytes are copied before we return
+    drain(g);
+    return rc;
+}
+
+int32_t syncr_ingest_submit_file(syncr_ingest *g, const char *path, uint64_t tag) {
+    if (!g || !path) return SYNCR_CDC_EINVAL;
+    if (!g->multi) return pipe_submit_file(g->pipes[0], path, tag);
+    if (g->reserved) return SYNCR_CDC_ESTATE;
+    int32_t rc = sticky(g);
+    if (rc) return rc;
+    struct stat st;
+    const uint64_t size = stat(path, &st) == 0 ? (uint64_t)st.st_size : 0;
+    const uint32_t d = g->assign->assign(size);
+    Job j{J_FILE};
+    j.path = path;
+    j.seq = new_seq(g, tag);
+    enqueue(g->workers[d], std::move(j));                 // read + chunked on that device's thread
+    drain(g);
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_ingest_set_cache(syncr_ingest *g, syncr_cache *c) {
+    if (!g) return SYNCR_CDC_EINVAL;
+    if (c) {
+        syncr_cdc_params cp;
+        int32_t rc = syncr_cache_get_params(c, &cp);
+        if (rc) return rc;
+        const syncr_cdc_params &ip = g->pipes[0]->params;
+        // a chunk list cut under other parameters must never be served
+        if (cp.chunk_bits != ip.chunk_bits || cp.max_chunk != ip.max_chunk || cp.read_cap != ip.read_cap)
+            return SYNCR_CDC_EINVAL;
+    }
+    if (g->multi) {                                       // no job may be using the old cache
+        int32_t rc = syncr_ingest_flush(g);
+        if (rc) return rc;
+    }
+    g->cache = c;
+    for (Pipe *p : g->pipes) p->cache = c;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_ingest_flush(syncr_ingest *g) {
+    if (!g) return SYNCR_CDC_EINVAL;
+    if (!g->multi) return pipe_flush(g->pipes[0]);
+    if (g->reserved) return SYNCR_CDC_ESTATE;
+    int32_t rc = sticky(g);
+    if (rc) return rc;
+    std::vector<SyncSlot> ss(g->workers.size());
+    for (size_t k = 0; k < g->workers.size(); k++) {
+        Job j{J_FLUSH};
+        j.sync = &ss[k];
+        enqueue(g->workers[k], std::move(j));
+    }
+    for (size_t k = 0; k < g->workers.size(); k++) {
+        Worker *w = g->workers[k];
+        std::unique_lock<std::mutex> l(w->mu);
+        w->done_cv.wait(l, [&] { return ss[k].done; });
+    }
+    drain(g);
+    for (auto &s : ss)
+        if (s.rc) return g->error = s.rc;
+    rc = sticky(g);
+    if (rc) return rc;
+    return g->tags.empty() ? SYNCR_CDC_OK : (g->error = SYNCR_CDC_EIO);   // every file delivered
+}
+
 int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4) {
     if (!g || !stats4) return SYNCR_CDC_EINVAL;
-    for (int k = 0; k < 4; k++) stats4[k] = g->stats[k];
+    for (int k = 0; k < 4; k++) {
+        stats4[k] = 0;
+        for (const Pipe *p : g->pipes) stats4[k] += p->stats[k].load();
+    }
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_ingest_device_stats(const syncr_ingest *g, uint64_t *stats, uint32_t n) {
+    if (!g || (n && !stats)) return SYNCR_CDC_EINVAL;
+    if (n < 4 * g->pipes.size()) return SYNCR_CDC_ERANGE;
+    for (size_t k = 0; k < g->pipes.size(); k++) {
+        const Pipe *p = g->pipes[k];
+        stats[4 * k + 0] = (uint64_t)p->device;
+        stats[4 * k + 1] = p->stats[0].load();           // files handled by this device
+        stats[4 * k + 2] = p->stats[1].load();           // bytes
+        stats[4 * k + 3] = p->stats[2].load();           // batches
+    }
     return SYNCR_CDC_OK;
 }
 
 int32_t syncr_ingest_cache_hits(const syncr_ingest *g, uint64_t *hits) {
     if (!g || !hits) return SYNCR_CDC_EINVAL;
-    *hits = g->cache_hits;
+    *hits = 0;
+    for (const Pipe *p : g->pipes) *hits += p->cache_hits.load();
     return SYNCR_CDC_OK;
 }
 
 void syncr_ingest_close(syncr_ingest *g) {
     if (!g) return;
-    for (Slot &s : g->slots) {
-        if (s.h) {
-            (void)syncr_cdc_synchronize(s.h);
-            syncr_cdc_close(s.h);
-        }
-        free_slot_buffers(g, s);
-    }
-    delete g->pool;
+    close_multi(g);
+    for (Pipe *p : g->pipes) pipe_close(p);
+    delete g->assign;
     delete g;
 }
 

@@ -79,3 +79,91 @@ def test_compaction_keeps_last_record(tmp_path):
     with syncr_amd.ChunkCache(p) as c:
         assert c.stats()["entries"] == 1
         assert np.array_equal(c.get("k", 49, int(a["len"].sum())), a)
+
+
+def test_empty_or_torn_header_file_is_a_new_cache(tmp_path):
+    """a zero-length file (pre-created with touch/mkstemp, or a crash
+    before the header reached the disk) and a file torn inside the magic are
+    new caches, not foreign files."""
+    for name, content in (("empty", b""), ("torn_magic", b"SYNC"), ("torn_header", b"SYNCRCC2\x14\x00")):
+        p = tmp_path / name
+        p.write_bytes(content)
+        with syncr_amd.ChunkCache(str(p)) as c:
+            a = chunks(3, 9)
+            c.put("f", 1, int(a["len"].sum()), a)
+        with syncr_amd.ChunkCache(str(p)) as c:                      # reopened: the entry survived
+            assert np.array_equal(c.get("f", 1, int(a["len"].sum())), a), name
+
+
+def test_header_is_durable_before_first_put(tmp_path):
+    p = tmp_path / "c"
+    c = syncr_amd.ChunkCache(str(p))
+    assert os.path.getsize(p) == 32                                  # header written + fsync'ed at open
+    c.close()
+    with syncr_amd.ChunkCache(str(p)) as c:
+        assert c.stats()["entries"] == 0
+
+
+def test_params_are_part_of_the_cache(tmp_path):
+    """chunk lists cut under other chunk_bits / max_chunk / read_cap
+    must never be served.  The log header records the parameters; reopening it
+    under others is refused, and so is attaching it to an ingest pipeline with
+    other parameters (that check runs before any device is touched)."""
+    p = str(tmp_path / "c")
+    with syncr_amd.ChunkCache(p, chunk_bits=20) as c:
+        a = chunks(2, 3)
+        c.put("f", 1, int(a["len"].sum()), a)
+        got = syncr_amd.Params()
+        assert syncr_amd.library().syncr_cache_get_params(c.handle, got) == 0
+        assert (got.chunk_bits, got.max_chunk, got.read_cap) == (20, 16 << 20, 2 << 20)
+    for kw in ({"chunk_bits": 13}, {"max_chunk": 1 << 20}, {"read_cap": 0}):
+        with pytest.raises(syncr_amd.SyncrCdcError) as e:
+            syncr_amd.ChunkCache(p, **kw)
+        assert e.value.code == syncr_amd.E_INVAL, kw
+    with syncr_amd.ChunkCache(p) as c:                               # same parameters: still valid
+        assert np.array_equal(c.get("f", 1, int(a["len"].sum())), a)
+
+
+def test_second_open_of_a_log_is_busy(tmp_path):
+    """Two handles appending to one log would interleave records: flock."""
+    p = str(tmp_path / "c")
+    with syncr_amd.ChunkCache(p):
+        with pytest.raises(syncr_amd.SyncrCdcError) as e:
+            syncr_amd.ChunkCache(p)
+        assert e.value.code == syncr_amd.E_BUSY
+    with syncr_amd.ChunkCache(p):                                     # released on close
+        pass
+
+
+def test_failed_append_is_rolled_back(tmp_path):
+    """a failed write must not leave a torn record that later puts
+    append behind (they would be dropped on the next open).  RLIMIT_FSIZE makes
+    the write of a big record fail part-way, in a child process."""
+    import subprocess
+    import sys
+    p = str(tmp_path / "c")
+    code = f"""
+import resource, signal, numpy as np, syncr_amd
+signal.signal(signal.SIGXFSZ, signal.SIG_IGN)
+c = syncr_amd.ChunkCache({p!r})
+small = np.zeros(1, syncr_amd.CHUNK_INFO_DTYPE); small["len"] = 5
+c.put("ok", 1, 5, small)
+resource.setrlimit(resource.RLIMIT_FSIZE, (4096, 4096))
+big = np.zeros(200, syncr_amd.CHUNK_INFO_DTYPE); big["len"] = 1
+try:
+    c.put("big", 1, 200, big)
+    print("NOERR")
+except syncr_amd.SyncrCdcError:
+    print("EIO")
+try:
+    c.put("after", 1, 5, small)
+    print("NOERR")
+except syncr_amd.SyncrCdcError:
+    print("EIO")
+c.close()
+"""
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), timeout=120)
+    assert out.stdout.split() == ["EIO", "EIO"], out.stdout + out.stderr
+    with syncr_amd.ChunkCache(p) as c:                               # the log is intact up to "ok"
+        assert c.get("ok", 1, 5) is not None and c.stats()["entries"] == 1

@@ -52,14 +52,15 @@ def test_gfx950_code_object(lib):
 
 def test_abi_and_defaults(lib):
     import syncr_amd
-    assert lib.syncr_cdc_abi_version() == syncr_amd.ABI_VERSION == 2
+    assert lib.syncr_cdc_abi_version() == syncr_amd.ABI_VERSION == 3
     p = syncr_amd.Params()
     lib.syncr_cdc_default_params(ctypes.byref(p))
     # src/chunking.rs:7-13 and the 2 MiB tokio read of file_operations.rs:738,776
     assert (p.chunk_bits, p.flags, p.max_chunk, p.read_cap) == (20, 0, 16 << 20, 2 << 20)
     assert syncr_amd.CHUNK_BITS == 20 and syncr_amd.MAX_CHUNK_SIZE == 16 * (1 << 20)
     for code, text in ((0, b"ok"), (-22, b"invalid argument"), (-34, b"output capacity too small"),
-                       (-19, b"no HIP device"), (-5, b"HIP runtime error"), (-71, b"call out of order")):
+                       (-19, b"no HIP device"), (-5, b"HIP runtime error"), (-71, b"call out of order"),
+                       (-16, b"locked by another handle"), (-2, b"no such entry")):
         assert lib.syncr_cdc_strerror(code) == text
 
 
@@ -81,6 +82,30 @@ def test_invalid_params_rejected(lib):
         p = syncr_amd.Params(bits, 0, mx, 0)
         assert lib.syncr_cdc_open(0, ctypes.byref(p), ctypes.byref(h)) in (-22, -19)
     assert lib.syncr_cdc_open(0, None, None) == -22
+    for flags in (4, 8, 1 << 31):                         # only SYNCR_CDC_FLAG_* bits
+        p = syncr_amd.Params(20, flags, 16 << 20, 2 << 20)
+        assert lib.syncr_cdc_open(0, ctypes.byref(p), ctypes.byref(h)) == -22
+    for flags in (0, syncr_amd.FLAG_RESOLVE_LANE, syncr_amd.FLAG_RESOLVE_NOBURST):
+        p = syncr_amd.Params(20, flags, 16 << 20, 2 << 20)
+        assert lib.syncr_cdc_open(0, ctypes.byref(p), ctypes.byref(h)) in (0, -19)
+        if h.value:
+            lib.syncr_cdc_close(h)
+            h = ctypes.c_void_p()
+
+
+def test_product_library_reads_no_environment(lib):
+    """no getenv in the product library (the variants and
+    timing-only ablations are compiled only into libsyncr_cdc_dev.so), and the
+    product carries exactly one scan kernel instance."""
+    import syncr_amd
+    blob = open(syncr_amd.library_path, "rb").read()
+    for name in (b"SYNCR_CDC_ABLATE", b"SYNCR_B3_ABLATE", b"SYNCR_CDC_SCAN", b"SYNCR_CDC_RUN", b"SYNCR_CDC_NT",
+                 b"SYNCR_CDC_RESOLVE", b"SYNCR_B3_LOAD", b"SYNCR_CDC_SERIAL"):
+        assert name not in blob, name
+    dyn = subprocess.run(["nm", "-D", "--undefined-only", syncr_amd.library_path], capture_output=True,
+                         text=True, check=True).stdout
+    assert not re.search(r"\bgetenv\b", dyn)
+    assert b"cdc_scan_kernel" in blob and b"cdc_scan_mfma_kernel" not in blob
 
 
 def test_compute_file_chunks_missing_file_is_empty(tmp_path):

@@ -1,6 +1,7 @@
 """Multi-GPU path on CPU: per-file LPT sharding and the control-plane reductions
 bench.py uses (gloo, world_size 2).  No data-path collective exists: files are
 independent, so ranks only agree on the step time."""
+import json
 import os
 import socket
 
@@ -87,3 +88,55 @@ def test_load_traffic_takes_latest_version(tmp_path, monkeypatch):
     t = bench.load_traffic("zipf10k", 1000, 144)
     assert t["source"] == "r01_v11" and t["hbm_bytes_per_launch"] == 2
     assert bench.load_traffic("uniform1k", 1000, 144) is None
+
+
+def _run_bench(args, env=None, timeout=240):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True,
+                          text=True, timeout=timeout, env=e, cwd=root)
+
+
+def test_bench_gpus2_self_launches_two_ranks():
+    """`bench.py --gpus N` (no launcher) must run N ranks itself.
+    The dry run touches no device: it prints the LPT shard plan gathered from
+    both ranks over gloo."""
+    pytest.importorskip("torch")
+    r = _run_bench(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout                                   # rank 0 only
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["launcher"] == "bench.py"
+    assert [s["rank"] for s in out["shards"]] == [0, 1]
+    assert out["disjoint"] and out["covers_all"]
+    assert all(s["files"] == 10000 and s["bytes"] == 10447937536 for s in out["shards"])
+    assert out["max_over_mean"] < 1.01
+
+
+def test_bench_world_size_must_match_gpus():
+    """Under a launcher (WORLD_SIZE set) --gpus is checked, never ignored."""
+    r = _run_bench(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_gpus1_dry_run():
+    r = _run_bench(["--dry-run", "--workload", "uniform1k"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["n_gpus"] == 1 and out["shards"] == [{"rank": 0, "files": 1024, "bytes": 1 << 30}]
+
+
+def test_dense_workload_pattern_hits_every_64_bytes():
+    """--workload dense: the periodic files hit the Bup edge test once per 64-byte
+    period (checked on the oracle), the constant files never do."""
+    from oracle import oracle as O
+    p = bench.periodic_pattern()
+    ends = O.chunk_production(np.resize(p, 1 << 20))
+    assert np.array_equal(ends, np.arange(64, (1 << 20) + 1, 64))
+    ends = O.chunk_production(np.full(5 << 20, 7, np.uint8))
+    assert np.array_equal(ends, np.arange(2 << 20, (5 << 20) + 1, 2 << 20).tolist() + [5 << 20]) or \
+        ends.tolist() == [2 << 20, 4 << 20, 5 << 20]

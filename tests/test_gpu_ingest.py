@@ -141,3 +141,99 @@ def test_chunk_cache_skips_unchanged_files(tmp_path):
         third, st3 = run(c)
     assert st3["cache_hits"] == len(files) - 1
     check(third, files)
+
+
+# ---- one pipeline over several devices (syncr_ingest_open_multi) ----------
+# The pool's box has one GPU, so "two devices" are two sub-pipelines on device
+# 0: the same code path (one worker thread, handles and streams per listed
+# device, LPT assignment, reordering) as on an 8-GPU node.
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_multi_device_bytes_in_submission_order(devices):
+    files = corpus(90, 21, 3 * M)
+    with syncr_amd.Ingest(batch_bytes=4 * M, depth=2, copy_threads=4, devices=devices) as g:
+        for i, f in enumerate(files):
+            g.submit(f, 1000 + i)
+        g.flush()
+        st, per = g.stats(), g.device_stats()
+        res = g.results
+    assert [t for t, _, _ in res] == [1000 + i for i in range(len(files))]
+    check([(t - 1000, s, a) for t, s, a in res], files)
+    assert st["files"] == len(files) and st["bytes"] == sum(f.size for f in files)
+    assert len(per) == len(devices) and all(p["device"] == 0 for p in per)
+    assert sum(p["files"] for p in per) == len(files) and all(p["files"] > 0 for p in per)
+    loads = [p["bytes"] for p in per]                        # online LPT: within one file of the mean
+    assert max(loads) - min(loads) <= max(f.size for f in files)
+
+
+def test_multi_device_files_errors_and_cache(tmp_path):
+    """submit_file on two sub-pipelines: missing files keep their place in the
+    order with -ENOENT; a cache attached to the multi pipeline serves the
+    second pass from every sub-pipeline."""
+    files = corpus(30, 23, 4 * M)
+    paths = []
+    for i, f in enumerate(files):
+        p = tmp_path / f"f{i}.bin"
+        p.write_bytes(f.tobytes())
+        paths.append(str(p))
+    paths.insert(5, str(tmp_path / "missing.bin"))
+    cpath = str(tmp_path / "c.cache")
+
+    def run(cache):
+        got = []
+        with syncr_amd.Ingest(batch_bytes=6 * M, depth=2, copy_threads=4, devices=[0, 0], cache=cache,
+                              on_file=lambda t, s, a: got.append((t, s, a))) as g:
+            for i, p in enumerate(paths):
+                g.submit_file(p, i)
+            g.flush()
+            return got, g.stats()
+
+    with syncr_amd.ChunkCache(cpath) as c:
+        first, st1 = run(c)
+        second, st2 = run(c)
+    for got in (first, second):
+        assert [t for t, _, _ in got] == list(range(len(paths)))
+        assert got[5][1] == -errno.ENOENT and got[5][2].size == 0
+        rest = [x for k, x in enumerate(got) if k != 5]
+        check([(i, s, a) for i, (_, s, a) in enumerate(rest)], files)
+    assert st1["cache_hits"] == 0 and st2["cache_hits"] == len(files)
+
+
+def test_multi_device_reserve_commit_zipf_subset():
+    """A Zipf-sized subset (SURVEY §8d config 3 sizes, the 300 smallest plus the
+    largest files up to 512 MiB in total) through reserve/commit on two
+    sub-pipelines: every boundary and BLAKE3 bit-exact vs the oracle."""
+    import bench
+    sizes = bench.zipf_sizes()
+    order = np.argsort(sizes, kind="stable")
+    pick = list(order[:300])
+    tot = int(sizes[pick].sum())
+    for i in order[::-1]:
+        if tot + int(sizes[i]) > 512 * M:
+            continue
+        pick.append(i)
+        tot += int(sizes[i])
+        if tot > 480 * M:
+            break
+    pick = sorted(int(i) for i in pick)
+    files = [O.corpus_fill(np.array([sizes[i]], np.uint64), first_index=i)[0] for i in pick]
+    with syncr_amd.Ingest(batch_bytes=64 * M, depth=2, copy_threads=8, devices=[0, 0]) as g:
+        for k, f in enumerate(files):
+            dst = g.reserve(f.size)
+            dst[:] = f
+            g.commit(k)
+        g.flush()
+        res = g.results
+    check(res, files)
+
+
+def test_multi_device_state_errors():
+    with syncr_amd.Ingest(batch_bytes=M, depth=1, devices=[0, 0]) as g:
+        g.reserve(10)
+        with pytest.raises(syncr_amd.SyncrCdcError):
+            g.submit(np.zeros(5, np.uint8), 1)               # reserve outstanding
+        with pytest.raises(syncr_amd.SyncrCdcError):
+            g.flush()
+        g.commit(0)
+        g.flush()
+        assert [t for t, _, _ in g.results] == [0]

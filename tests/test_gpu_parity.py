@@ -308,27 +308,83 @@ def test_kernel_timing_api(chunkers):
         buf.free()
 
 
-def test_resolve_variants_agree(kat_cases):
-    """Wave-per-file (default) and lane-per-file resolve give identical cuts."""
-    import os
+@pytest.mark.parametrize("flags", [syncr_amd.FLAG_RESOLVE_LANE, syncr_amd.FLAG_RESOLVE_NOBURST])
+def test_resolve_variants_agree(kat_cases, flags):
+    """Wave-per-file with burst (default), lane-per-file and wave without burst
+    (params.flags, exact alternatives) give identical cuts on every KAT."""
     sel = [c for c in kat_cases if c["len"] <= 8 * M]
-    os.environ["SYNCR_CDC_RESOLVE"] = "lane"
+    alt = {}
     try:
-        lanes = {}
         for c in sel:
             key = (c["chunk_bits"], c["max_chunk"], c["read_cap"])
-            if key not in lanes:
-                lanes[key] = syncr_amd.Chunker(*key)
-    finally:
-        del os.environ["SYNCR_CDC_RESOLVE"]
-    try:
-        for c in sel:
+            if key not in alt:
+                alt[key] = syncr_amd.Chunker(*key, flags=flags)
             data = make_input(c["recipe"])
-            ch = lanes[(c["chunk_bits"], c["max_chunk"], c["read_cap"])]
-            assert ends_of(ch.cut_array(data)) == c["ends"], c["name"]
+            assert ends_of(alt[key].cut_array(data)) == c["ends"], c["name"]
     finally:
-        for ch in lanes.values():
+        for ch in alt.values():
             ch.close()
+
+
+def test_product_ignores_environment(kat_cases, monkeypatch):
+    """the timing-only ablations and experimental kernels
+    live only in the development library.  With every variable the round-1
+    library read set to a non-exact or experimental value, the product still
+    returns oracle-exact cuts and BLAKE3 hashes."""
+    for k, v in {"SYNCR_CDC_ABLATE": "1", "SYNCR_B3_ABLATE": "1", "SYNCR_CDC_SCAN": "mfma",
+                 "SYNCR_CDC_RUN": "48", "SYNCR_CDC_NB": "4", "SYNCR_CDC_NT": "0", "SYNCR_CDC_RESOLVE": "lane",
+                 "SYNCR_B3_LOAD": "plain", "SYNCR_CDC_SCAN_GRID": "3", "SYNCR_CDC_SERIAL": "0"}.items():
+        monkeypatch.setenv(k, v)
+    with syncr_amd.Chunker() as ch:
+        info = ch.info()
+        assert info["run_bytes"] == 144 and info["scan_kernel"] == "cdc_scan_kernel" and info["scan_grid"] > 3
+        data = O.xorshift_bytes(4242, 12 * M + 77)
+        got = ch.chunk_bytes(data, hashed=True)
+        ends = [c.offset + c.size for c in got]
+        assert ends == O.chunk_production(data).tolist()
+        for c in got:
+            assert c.hash == O.blake3(data[c.offset:c.offset + c.size])
+        for c in [k for k in kat_cases if k["len"] <= 4 * M][:12]:
+            if (c["chunk_bits"], c["max_chunk"], c["read_cap"]) == (20, 16 * M, 2 * M):
+                assert ends_of(ch.cut_array(make_input(c["recipe"]))) == c["ends"], c["name"]
+
+
+def test_two_handles_interleaved_on_one_device():
+    """Handles of one device order their scans (a scan waits for the other
+    handle's last scan, cdc_api.cpp ScanOrder); interleaved launches on two
+    handles and streams, each on its own copy of a corpus, stay exact."""
+    lens = np.array([5 * M + 3, 0, 777, 3 * M, 40 * 1024] * 6, np.uint64)
+    offs = np.zeros_like(lens)
+    offs[1:] = np.cumsum(lens)[:-1]
+    span = int(lens.sum())
+    hs = [syncr_amd.Chunker(), syncr_amd.Chunker()]
+    bufs = []
+    try:
+        for k, h in enumerate(hs):
+            b = syncr_amd.DeviceBuffer(h, span)
+            b.gen_corpus(offs, lens, first_index=100 * k)
+            h.plan(offs, lens, span)
+            bufs.append(b)
+        for step in range(12):
+            h = hs[step % 2]
+            h.launch(bufs[step % 2].ptr, hashed=(step % 3 == 0))
+        for k, h in enumerate(hs):
+            h.launch(bufs[k].ptr, hashed=True)
+        for k, h in enumerate(hs):
+            got = h.fetch(hashed=True)
+            host = bufs[k].download(span)
+            for i in range(lens.size):
+                f = host[int(offs[i]): int(offs[i] + lens[i])]
+                e = (got[i]["offset"] + got[i]["len"]).tolist()
+                assert e == O.chunk_production(f).tolist(), (k, i)
+                for c in got[i]:
+                    o, n = int(c["offset"]), int(c["len"])
+                    assert c["hash"].tobytes() == O.blake3(f[o:o + n])
+    finally:
+        for b in bufs:
+            b.free()
+        for h in hs:
+            h.close()
 
 
 def test_dedup_corpus_full_size():
