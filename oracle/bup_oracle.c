@@ -183,6 +183,41 @@ uint64_t orc_chunk_production_read_error(const uint8_t *file, uint64_t P, uint32
     return sk.n;
 }
 
+/*
+ * The same loop with the buffer as a window into the file instead of a
+ * memmove'd copy: buf[0..n) of the literal loop is always file[offset ..
+ * offset + n) (reads are sequential), so the Bup state machine, the reads and
+ * the cuts are identical; only copy_within's O(n) move per chunk is gone.  The
+ * literal loop costs ~max_chunk bytes of memmove per chunk, which on data with a
+ * cut every 64 bytes (the dense workload) is ~2^18 x the scan itself; tests use
+ * this variant for such inputs, and test_oracle.py checks it against the literal
+ * loop.
+ */
+uint64_t orc_chunk_production_window(const uint8_t *file, uint64_t F, uint32_t bits,
+                                     uint64_t max_chunk, uint64_t read_cap,
+                                     uint64_t *ends, uint64_t ends_cap) {
+    sink_t sk = {ends, ends_cap, 0};
+    const uint64_t cap = read_cap ? read_cap : UINT64_MAX;
+    uint64_t R = F < max_chunk ? F : max_chunk;             /* bytes read so far (:738) */
+    if (R > cap) R = cap;
+    uint64_t offset = 0;
+    bup_t b;
+    while (R > offset) {                                      /* n = R - offset > 0 (:747) */
+        bup_init(&b, bits);
+        const uint64_t n = R - offset;
+        const uint64_t endofs = n < max_chunk ? n : max_chunk;
+        const uint64_t edge = bup_find_chunk_edge(&b, file + offset, endofs);
+        const uint64_t count = edge ? edge : endofs;
+        offset += count;
+        sink_push(&sk, offset);
+        uint64_t want = max_chunk - (R - offset);             /* f.read(&mut buf[n..]) (:776) */
+        if (want > cap) want = cap;
+        if (want > F - R) want = F - R;
+        R += want;
+    }
+    return sk.n;
+}
+
 /* chunk_data (tests/chunking_test.rs:170-192): in-memory "ideal" semantics. */
 uint64_t orc_chunk_ideal(const uint8_t *data, uint64_t len, uint32_t bits,
                          uint64_t max_chunk, uint64_t *ends, uint64_t ends_cap) {

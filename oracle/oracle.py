@@ -52,6 +52,8 @@ def lib():
         L.orc_chunk_production.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                            ctypes.c_uint64, _u64p, ctypes.c_uint64]
         L.orc_chunk_production.restype = ctypes.c_uint64
+        L.orc_chunk_production_window.argtypes = L.orc_chunk_production.argtypes
+        L.orc_chunk_production_window.restype = ctypes.c_uint64
         L.orc_chunk_closed_form.argtypes = L.orc_chunk_production.argtypes
         L.orc_chunk_closed_form.restype = ctypes.c_uint64
         L.orc_chunk_no_head_fixup.argtypes = L.orc_chunk_production.argtypes
@@ -112,6 +114,13 @@ def _run(fn, data, *args) -> np.ndarray:
 def chunk_production(data, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE, read_cap=TOKIO_READ_CAP):
     """Cut END offsets of compute_file_chunks (file_operations.rs:721-788)."""
     return _run(lib().orc_chunk_production, data, bits, max_chunk, read_cap)
+
+
+def chunk_production_window(data, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE, read_cap=TOKIO_READ_CAP):
+    """The literal loop without copy_within's memmove (buffer = window into the
+    file): same reads, same Bup state machine, same cuts; for inputs with very
+    many chunks (bup_oracle.c orc_chunk_production_window)."""
+    return _run(lib().orc_chunk_production_window, data, bits, max_chunk, read_cap)
 
 
 def chunk_ideal(data, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE):

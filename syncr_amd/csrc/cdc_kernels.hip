@@ -30,14 +30,19 @@ __device__ __forceinline__ bool hit_exact(uint32_t S, uint32_t W, uint32_t mask)
     return (dg & mask) == mask;
 }
 
-// first index i in [lo, hi) with a[i] >= key (serial, per lane)
-__device__ __forceinline__ uint32_t lower_bound_serial(const uint64_t *a, uint32_t lo, uint32_t hi,
-                                                       int64_t key) {
-    while (lo < hi) {
-        const uint32_t mid = lo + ((hi - lo) >> 1);
-        if ((int64_t)a[mid] < key) lo = mid + 1; else hi = mid;
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(v, off);
+        if (lane >= off) v += u;
     }
-    return lo;
+    return v;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t k) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // tv = a*b + c on packed u16 pairs, pinned to ONE v_pk_mad_u16: left to itself
@@ -67,49 +72,6 @@ __device__ __forceinline__ uint64_t sload_u64(const void *p) {
     uint64_t v;
     asm volatile("s_nop 4\n\ts_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(u) : "memory");
     return v;
-}
-
-// ---------------------------------------------------------------------------
-// Slow path: one run rolled byte by byte with file-start resets.  Used for the
-// (rare) runs whose windows straddle a file start.  `byte(q)` reads global
-// position q; positions before q0 = rs-64 are treated as outside the window.
-// ---------------------------------------------------------------------------
-template <class ByteFn, class HitFn>
-__device__ __forceinline__ void roll_with_resets(ByteFn byte, int64_t rs, int len,
-                                                 const uint64_t *fstart, uint32_t lo, uint32_t hi,
-                                                 uint32_t mask, HitFn on_hit) {
-    const int64_t q0 = rs - 64;
-    uint32_t j = lower_bound_serial(fstart, lo, hi, q0);
-    int64_t next = j < hi ? (int64_t)fstart[j] : INT64_MAX;
-    int64_t g = q0;                       // window floor: bytes < g read as 0
-    uint32_t S = 0, W = 0;
-    for (int64_t q = q0; q < rs + len; ++q) {
-        if (q == next) {                  // fresh Bup at a file start
-            S = 0; W = 0; g = q;
-            ++j;
-            next = j < hi ? (int64_t)fstart[j] : INT64_MAX;
-        }
-        const uint32_t x = byte(q);
-        const uint32_t d = (q - 64 >= g) ? byte(q - 64) : 0u;
-        S += x - d;
-        W += S - 64u * d;
-        if (q >= rs && hit_exact(S, W, mask)) on_hit(q);
-    }
-}
-
-// First chunk-local hit in [e+1, e+63] for a chunk starting at e+1, as k = hit-e
-// (0 = none).  `byte(k)` returns the byte at e+k.  No drops: the window is fresh.
-template <class ByteFn>
-__device__ __forceinline__ uint32_t head_fix(ByteFn byte, uint32_t kmax, uint32_t mask) {
-    uint32_t S = 0, W = 0, found = 0;
-#pragma unroll 9
-    for (uint32_t k = 1; k <= 63; ++k) {
-        const uint32_t x = k <= kmax ? byte(k) : 0u;
-        S += x;
-        W += S;
-        if (!found && k <= kmax && hit_exact(S, W, mask)) found = k;
-    }
-    return found;
 }
 
 __device__ __forceinline__ void record(uint32_t *wcount, uint32_t *wlist, uint32_t rel) {
@@ -638,35 +600,73 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
 // are the resolve's head scan at s = 0 (a fresh window at f, exactly as after
 // any cut), so file starts need no kernel of their own.
 // ---------------------------------------------------------------------------
-// Dense tiles (more than LISTCAP candidates: low-entropy / adversarial data at
-// small chunk_bits): recompute G for the whole tile into a bitmap, count it.
+// Dense tiles (more than LISTCAP candidates: low-entropy / periodic /
+// adversarial data): recompute G for every position of the tile into a bitmap
+// and count it.  One wave per dense tile: the tile and its 64-byte halo are
+// staged in LDS with coalesced 16-byte loads; lane l rolls the 2*RUN positions
+// [t0 + l*2*RUN, +2*RUN) exactly (S, W and the full digest test) from its 64
+// warm-up bytes (closed form, v_dot4), reading 32 new + 32 dropped bytes per
+// bitmap word as four ds_read_b128.  Stream semantics like the scan: no resets
+// at file starts (file heads are the resolve's head scan).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict__ data, KParams P,
                                                        Tables T) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dbuf[];   // [HALO + tile]
     const uint32_t nd = min(T.ctr[CTR_DENSE], T.dense_cap);
     const int lane = threadIdx.x;
-    const int per_lane = (int)T.tile / 64;             // positions per lane (multiple of 32)
-    const int words_lane = per_lane / 32;
+    const uint32_t TB = T.tile, BUFB = HALO + TB;
+    const uint32_t per_lane = TB / 64;                   // 2 * RUN: a multiple of 32
+    const uint32_t words_lane = per_lane / 32;
+    const int64_t span = (int64_t)T.span;
     for (uint32_t idx = blockIdx.x; idx < nd; idx += gridDim.x) {
         const uint32_t tile = T.dense_list[idx];
-        const int64_t t0 = (int64_t)tile * T.tile;
-        const int64_t rs = t0 + (int64_t)lane * per_lane;
-        const int64_t span = (int64_t)T.span;
-        uint32_t *out = T.dense_bits + (size_t)idx * (T.tile / 32) + lane * words_lane;
-        for (int w = 0; w < words_lane; ++w) out[w] = 0u;
-        auto byte = [&](int64_t q) -> uint32_t { return (q >= 0 && q < span) ? data[q] : 0u; };
-        uint32_t word = 0, cnt = 0;
-        int cur = 0;
-        // stream semantics like the scan (no resets: file heads are the resolve's head scan)
-        roll_with_resets(byte, rs, per_lane, T.fstart, 0u, 0u, P.mask, [&](int64_t q) {
-            if (q < span) {
-                const int r = (int)(q - rs);
-                if ((r >> 5) != cur) { out[cur] = word; word = 0; cur = r >> 5; }
-                word |= 1u << (r & 31);
-                ++cnt;
+        const int64_t base = (int64_t)tile * TB - HALO;
+        __syncthreads();                                 // the previous tile's LDS reads are done
+        for (uint32_t o = (uint32_t)lane * 16u; o < BUFB; o += 1024u) {
+            const int64_t g = base + o;
+            uint4 v;
+            if (g >= 0 && g + 16 <= span) {
+                v = *(const uint4 *)(data + g);          // d_bytes and the tile size are 16-byte aligned
+            } else {                                     // batch edges: zeros outside [0, span)
+                uint32_t w4[4] = {0u, 0u, 0u, 0u};
+                for (int b = 0; b < 16; ++b)
+                    if (g + b >= 0 && g + b < span) w4[b >> 2] |= (uint32_t)data[g + b] << (8 * (b & 3));
+                v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
             }
-        });
-        out[cur] |= word;
+            *(uint4 *)(dbuf + o) = v;
+        }
+        __syncthreads();
+        const uint8_t *lb = dbuf + (size_t)lane * per_lane;        // run start - 64
+        uint32_t S = 0, W = 0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {                   // window before the run (weights 64..1)
+            const uint32_t wd = *(const uint32_t *)(lb + 4 * m);
+            S = __builtin_amdgcn_udot4(wd, 0x01010101u, S, false);
+            W = __builtin_amdgcn_udot4(wd, 0x3D3E3F40u - 0x04040404u * (uint32_t)m, W, false);
+        }
+        const int64_t rs = (int64_t)tile * TB + (int64_t)lane * per_lane;
+        const int64_t lim = span - rs;                   // positions >= span are not bytes
+        uint32_t *out = T.dense_bits + (size_t)idx * (TB / 32) + (size_t)lane * words_lane;
+        uint32_t cnt = 0;
+        for (uint32_t wi = 0; wi < words_lane; ++wi) {
+            const uint4 x0 = *(const uint4 *)(lb + HALO + 32 * wi), x1 = *(const uint4 *)(lb + HALO + 32 * wi + 16);
+            const uint4 d0 = *(const uint4 *)(lb + 32 * wi), d1 = *(const uint4 *)(lb + 32 * wi + 16);
+            const uint32_t xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            const uint32_t ds[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+            uint32_t bits = 0;
+#pragma unroll
+            for (int b = 0; b < 32; ++b) {
+                const uint32_t x = (xs[b >> 2] >> (8 * (b & 3))) & 0xffu;
+                const uint32_t d = (ds[b >> 2] >> (8 * (b & 3))) & 0xffu;
+                S += x - d;
+                W += S - 64u * d;
+                bits |= (hit_exact(S, W, P.mask) ? 1u : 0u) << b;
+            }
+            const int64_t k0 = 32 * (int64_t)wi;
+            if (k0 + 32 > lim) bits &= k0 >= lim ? 0u : ((1u << (uint32_t)(lim - k0)) - 1u);
+            out[wi] = bits;
+            cnt += __builtin_popcount(bits);
+        }
         for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
         if (lane == 0) {
             T.dense_cnt[idx] = cnt;
@@ -737,7 +737,10 @@ __global__ __launch_bounds__(1024) void cdc_prefix_kernel(Tables T) {
 }
 
 // Compact every tile's candidates into T.cand in position order (one wave per
-// 64-tile group; empty groups exit on their bitset word).
+// 64-tile group; empty groups exit on their bitset word).  A sparse tile's
+// lane copies its slot list; the wave then walks the group's dense tiles
+// together: 64 bitmap words at a time, a wave prefix of their popcounts gives
+// each lane its output run.
 __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
     const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -756,31 +759,37 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
             c = meta;
         }
     }
-    uint32_t incl = c;                                  // wave inclusive scan
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t v = __shfl_up(incl, off);
-        if (lane >= off) incl += v;
-    }
+    const uint32_t incl = wave_incl_scan(c, lane);
     const uint64_t base = T.super_off[w] + (incl - c);
-    if (!has || !c) return;
-    if (base + c > T.cand_cap) return;                  // overflow flagged by prefix; host re-runs
-    const uint64_t t0 = (uint64_t)tile * T.tile;
-    if (!(meta & DENSE_BIT)) {
+    const bool dense = has && (meta & DENSE_BIT) && c;
+    if (has && c && !dense && base + c <= T.cand_cap) {   // overflow is flagged by prefix; host re-runs
+        const uint64_t t0 = (uint64_t)tile * T.tile;
         const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
-        for (uint32_t j = 0; j < c; ++j) {
-            const uint2 v = sl[j];
-            T.cand[base + j] = t0 + v.x;               // fix-up: cdc_fix_kernel
-        }
-    } else {
-        const uint32_t *bm = T.dense_bits + (size_t)(meta & ~DENSE_BIT) * (T.tile / 32);
-        uint64_t o = base;
-        for (uint32_t wi = 0; wi < T.tile / 32; ++wi) {
-            uint32_t m = bm[wi];
+        for (uint32_t j = 0; j < c; ++j) T.cand[base + j] = t0 + sl[j].x;    // fix-up: cdc_fix_kernel
+    }
+    unsigned long long dm = __ballot(dense);
+    const uint32_t nw = T.tile / 32;
+    while (dm) {
+        const int j = __builtin_ctzll(dm);
+        dm &= dm - 1;
+        const uint64_t tb = readlane64(base, (uint32_t)j);
+        const uint32_t tc = (uint32_t)__builtin_amdgcn_readlane((int)c, j);
+        if (tb + tc > T.cand_cap) continue;
+        const uint32_t di = (uint32_t)__builtin_amdgcn_readlane((int)meta, j) & ~DENSE_BIT;
+        const uint32_t *bm = T.dense_bits + (size_t)di * nw;
+        const uint64_t t0 = (uint64_t)(w * 64 + (uint32_t)j) * T.tile;
+        uint64_t o = tb;
+        for (uint32_t b0 = 0; b0 < nw; b0 += 64) {
+            const uint32_t wi = b0 + (uint32_t)lane;
+            uint32_t m = wi < nw ? bm[wi] : 0u;
+            const uint32_t pc = (uint32_t)__builtin_popcount(m);
+            const uint32_t ic = wave_incl_scan(pc, lane);
+            uint64_t q = o + (ic - pc);
             while (m) {
-                const uint32_t r = wi * 32 + (uint32_t)__builtin_ctz(m);
+                T.cand[q++] = t0 + wi * 32u + (uint32_t)__builtin_ctz(m);
                 m &= m - 1;
-                T.cand[o++] = t0 + r;
             }
+            o += (uint32_t)__builtin_amdgcn_readlane((int)ic, 63);
         }
     }
 }
@@ -955,20 +964,6 @@ __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restri
 // state is wave-uniform, so the serial compute_file_chunks walk costs a few
 // scalar/vector ops per cut instead of a dependent memory round trip.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t u = __shfl_up(v, off);
-        if (lane >= off) v += u;
-    }
-    return v;
-}
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t k) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k);
-    return ((uint64_t)hi << 32) | lo;
-}
 
 // The walk of one file, in file-relative offsets of type Off (uint32_t for
 // files below 4 GiB: every comparison and min stays in the scalar unit, which
@@ -1497,7 +1492,7 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
     if (!t.ntiles) return hipSuccess;
     if (t.dense_cap) {
         const uint32_t blocks = t.dense_cap < 2048u ? t.dense_cap : 2048u;
-        hipLaunchKernelGGL(cdc_dense_kernel, dim3(blocks), dim3(64), 0, s, d, p, t);
+        hipLaunchKernelGGL(cdc_dense_kernel, dim3(blocks), dim3(64), HALO + t.tile, s, d, p, t);
     }
     hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
     hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4), dim3(256), 0, s, t);

@@ -139,6 +139,39 @@ def test_periodic_pattern_every_64(chunkers):
         assert ends_of(ch.cut_array(data)) == oracle_ends(data, bits, 1 << 16, cap)
 
 
+def test_dense_workload_subset(chunkers):
+    """bench.py --workload dense at test size: files that are the bits-20
+    periodic pattern (a cut every 64 bytes: dense tiles, candidate-array and
+    cut-capacity overflow re-runs, long chained resolve walks), constant-byte
+    files (MAX / read-cap cuts) and random files, packed back to back at
+    unaligned offsets, in both semantics; every cut bit-exact vs the oracle."""
+    import bench
+    pat = bench.periodic_pattern()
+    rng = np.random.default_rng(77)
+    files = []
+    for i in range(24):
+        n = int(rng.integers(0, 5 * M)) if i % 5 else int(rng.integers(0, 300))
+        k = i % 3
+        files.append(np.resize(pat, n) if k == 0 else
+                     (np.full(n, i, np.uint8) if k == 1 else O.xorshift_bytes(900 + i, n)))
+    files.append(np.resize(pat, 18 * M + 13))                  # > MAX: forced cut, then saturated walk
+    lens = np.array([f.size for f in files], np.uint64)
+    gaps = rng.integers(0, 40, lens.size).astype(np.uint64)
+    offs = np.zeros_like(lens)
+    offs[1:] = np.cumsum(lens + gaps)[:-1]
+    span = int(offs[-1] + lens[-1]) + 5
+    data = np.zeros(span, np.uint8)
+    for o, f in zip(offs.tolist(), files):
+        data[o:o + f.size] = f
+    for cap in (2 << 20, 0):
+        res = chunkers(20, 16 << 20, cap).batch_arrays(data, offs, lens)
+        for i, (o, n) in enumerate(zip(offs.tolist(), lens.tolist())):
+            # the literal loop without copy_within (O(n) per 64-byte chunk here)
+            want = (O.chunk_production_window(data[o:o + n], 20, 16 << 20, cap) if cap
+                    else O.chunk_ideal(data[o:o + n], 20, 16 << 20)).tolist()
+            assert ends_of(res[i]) == want, (i, n, cap)
+
+
 def test_error_contract(chunkers):
     import ctypes
     L = syncr_amd.library()

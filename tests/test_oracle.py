@@ -125,3 +125,20 @@ def test_corpus_seed_rule():
     for j, (o, n) in enumerate(zip(offs.tolist(), [100, 7, 0, 33])):
         ref = O.xorshift_bytes((0x9E3779B97F4A7C15 * (5 + j + 1)) % 2**64, n, discard=64)
         assert np.array_equal(buf[o:o + n], ref)
+
+
+def test_window_variant_equals_literal_loop():
+    """orc_chunk_production_window (no copy_within) == the literal loop, on
+    random, low-entropy, periodic (a cut every 64 bytes) and zero data, with and
+    without the read cap -- it stands in for the literal loop only where the
+    literal loop's O(buffer) memmove per chunk would take hours."""
+    import bench
+    pat = bench.periodic_pattern()
+    inputs = [O.xorshift_bytes(31, 5 * M + 3), np.resize(pat, 300 * 1024 + 7),
+              (O.xorshift_bytes(32, 3 * M) & 3).astype(np.uint8), np.zeros(5 * M + 1, np.uint8),
+              np.concatenate([np.resize(pat, M), O.xorshift_bytes(33, 2 * M)])]
+    for data in inputs:
+        for bits, mx, cap in ((20, 16 * M, 2 * M), (20, 16 * M, 0), (13, 1 << 17, 3000), (8, 4096, 1000)):
+            assert np.array_equal(O.chunk_production_window(data, bits, mx, cap),
+                                  O.chunk_production(data, bits, mx, cap)), (data.size, bits, mx, cap)
+    assert O.chunk_production_window(np.zeros(0, np.uint8)).size == 0
