@@ -110,7 +110,10 @@ struct DirtySlot {             // 80 bytes
     uint32_t flags;            // bit0: check A, bit1: check B
 };
 
-template <int RUN>
+// ROLL2: the same values with single-op dependency chains per byte pair:
+// V = S - 64 d (one v_pk_mad_u16 off the T chain), then T += k V (one
+// v_pk_mad_u16 on it), instead of two dependent v_pk_mad_u16 on T.
+template <int RUN, bool ROLL2 = false>
 __device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
                                           const uint32_t (&B)[(HALO + RUN) / 4], const KParams &P,
                                           int lane, bool recA, bool recB, uint32_t *dcount,
@@ -140,8 +143,13 @@ __device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
             const int i = g * 16 + jj;
             const uint32_t x = pair_at<RUN>(A, B, HALO + i), d = pair_at<RUN>(A, B, i);
             S = S + x - d;
-            Tv = pk_mad(S, P.kk, Tv);
-            Tv = pk_mad(d, P.kmv, Tv);
+            if constexpr (ROLL2) {
+                const u16x2 V = pk_mad(d, 0xFFC0FFC0u, as_u16x2(S));   // S - 64 d (mod 2^16 per half)
+                Tv = pk_mad(as_u32(V), P.kk, Tv);                       // T += k (S - 64 d)
+            } else {
+                Tv = pk_mad(S, P.kk, Tv);
+                Tv = pk_mad(d, P.kmv, Tv);
+            }
             acc = __builtin_elementwise_min(acc, Tv);
         }
         const uint32_t a = as_u32(acc);
@@ -385,7 +393,7 @@ __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict_
             continue;
         }
         const int64_t lim_rel = span - t0;                           // positions >= span are not bytes
-        roll_fast<RUN>(A, B, P, lane, true, true, dcount, dslots);
+        roll_fast<RUN, (MODE & 16) != 0>(A, B, P, lane, true, true, dcount, dslots);
         if constexpr ((MODE & 3) == 2) continue;                          // diagnostics: rolling only
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -1401,6 +1409,10 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 5>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 4u)                                         // A/B: static stride (exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 4>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 5u)                                         // A/B: ROLL2 (exact)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 6u)                                         // timing only: ROLL2, roll, no DMA
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.nt)                                                   // product: nt loads + dynamic groups
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
     else

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of engine variants in ONE process on ONE device.
 
-Variants are environment settings read by syncr_cdc_open (SYNCR_CDC_RUN,
-SYNCR_CDC_PRIO, SYNCR_CDC_ABLATE, SYNCR_CDC_SCAN_GRID, ...).  The corpus is
+Variants are environment settings read by syncr_cdc_open of the DEVELOPMENT
+library (libsyncr_cdc_dev.so, `python -m syncr_amd.build --dev`; the product
+library reads no environment): SYNCR_CDC_RUN, SYNCR_CDC_ABLATE,
+SYNCR_CDC_SCAN_GRID, SYNCR_B3_*, ...  The corpus is
 generated once; each round times every variant for --steps launches; the
 median scan-kernel time and step time per variant are printed.  Cross-call
 comparisons are not trusted (devices and clocks differ between gpurun boxes).
@@ -22,6 +24,8 @@ import numpy as np  # noqa: E402
 
 import bench  # noqa: E402
 import syncr_amd  # noqa: E402
+
+syncr_amd.use_dev_library()
 
 
 def main():

@@ -21,6 +21,9 @@ import numpy as np  # noqa: E402
 import bench  # noqa: E402
 import syncr_amd  # noqa: E402
 
+if "--dev" in sys.argv:                  # variants by environment (SYNCR_CDC_ABLATE=5: ROLL2)
+    syncr_amd.use_dev_library()
+
 
 def main():
     sizes, idx, _ = bench.workload("zipf10k", 1)
