@@ -97,6 +97,9 @@ def workload(name: str, world: int):
     elif name == "big1":
         one = np.full(1, 128 * M, np.uint64)
         desc = "diagnostic: one 128 MiB file (the longest resolve walk of zipf10k)"
+    elif name == "dense1":
+        one = np.full(1, 128 * M, np.uint64)
+        desc = "diagnostic: one 128 MiB periodic-64 file (2 M chained cuts: the dense workload's longest walk)"
     elif name == "uniform1k":
         one = np.full(1024, M, np.uint64)
         desc = "SURVEY §8d config 2: 1024 x 1 MiB files per GPU, LPT-sharded per file"
@@ -345,7 +348,7 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "dense", "big1"])
+    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "dense", "big1", "dense1"])
     ap.add_argument("--mode", default="production", choices=["production", "ideal"])
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -399,6 +402,8 @@ def main(argv=None):
         b.gen_corpus(offs, lens, indices=idx)
         if args.workload == "dense":
             fill_dense(b, offs, lens, idx)
+        elif args.workload == "dense1":
+            b.upload(np.resize(periodic_pattern(), span))
         h.plan(offs, lens, span)
         slots.append((h, b))
     ch, dbuf = slots[0]
@@ -522,7 +527,8 @@ def main(argv=None):
         }
 
     cpu = None
-    if d.rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # dense1 is one periodic file: the literal loop would memmove 16 MiB per 64-byte chunk
+    if d.rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "dense1":
         skip = None
         if args.workload == "dense":
             # the literal loop memmoves its buffer (copy_within, file_operations.rs:771)

@@ -310,12 +310,16 @@ __device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, u
 // tile: wait for its DMA, copy the runs into registers, hand the buffer to the
 // next tile's DMA, then roll.  The DMA latency hides under the rolling of this
 // tile and under the other resident waves.  The scan knows nothing about files:
-// it computes G over the batch as one continuous stream (see cdc_boundary_kernel).
+// it computes G over the batch as one continuous stream.
 // ---------------------------------------------------------------------------
-// MODE bits 0-1: 0 is the product; 1 (staging only) and 2 (no DMA) are
-// timing-only ablations selected by SYNCR_CDC_ABLATE, compiled separately so
-// they cannot perturb the product's register allocation.  Bit 2: non-temporal
-// tile loads (SYNCR_CDC_NT).
+// MODE bits 0-1: 0 is exact; 1 (staging only) and 2 (no DMA) are timing-only
+// ablations, instantiated only in the development library.  Bit 2:
+// non-temporal tile loads.  Bit 3: dynamic tile groups.  Bit 4: ROLL2.
+// The product's scan: non-temporal tile loads (4) + dynamic tile groups (8) +
+// single-op dependency chains in the roll (16; same process, zipf10k: scan
+// 1.591 vs 1.640 ms, profiles/r02_ab_roll2.log).
+constexpr int SCAN_PRODUCT_MODE = 4 | 8 | 16;
+
 template <int RUN, int MODE>
 __global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P,
                                                       Tables T) {
@@ -1367,7 +1371,7 @@ int scan_lds_bytes(ScanGeom g) {
     return g.kind == SCAN_VALU ? lds_wave_bytes(g.param) : mf_lds_bytes(g.param, (g.var & MFV_SINGLE) ? 1 : 2);
 }
 
-template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN, 12>; }
+template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>; }
 template <int NB> static const void *mfma_fn(int var) {
     switch (var & 3) {
         case 0: return (const void *)&cdc_scan_mfma_kernel<NB, 4, true>;
@@ -1409,14 +1413,14 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 5>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 4u)                                         // A/B: static stride (exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 4>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 5u)                                         // A/B: ROLL2 (exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 6u)                                         // timing only: ROLL2, roll, no DMA
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.nt)                                                   // product: nt loads + dynamic groups
+    else if (p.ablate == 5u)                                         // A/B: round-1 roll (two dependent mads, exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 6u)                                         // timing only: roll, no DMA
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.nt)                                                   // product: nt loads + dynamic groups + ROLL2
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 8>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE & ~4>), dim3(grid), dim3(64), lds, s, d, p, t);
 }
 
 template <int NB, int V>
@@ -1478,15 +1482,15 @@ hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParam
 bool scan_supported(ScanGeom g) { return g.kind == SCAN_VALU && g.param == DEFAULT_RUN; }
 int scan_tile_bytes(ScanGeom) { return tile_bytes(DEFAULT_RUN); }
 int scan_lds_bytes(ScanGeom) { return lds_wave_bytes(DEFAULT_RUN); }
-static const void *scan_kernel_ptr(ScanGeom) { return (const void *)&cdc_scan_kernel<DEFAULT_RUN, 12>; }
+static const void *scan_kernel_ptr(ScanGeom) { return (const void *)&cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>; }
 
 hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
                        hipStream_t s) {
     if (!t.ntiles) return hipSuccess;
     if (!scan_supported(g)) return hipErrorInvalidValue;
     grid = grid < t.ntiles ? grid : t.ntiles;
-    hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, 12>), dim3(grid), dim3(64), lds_wave_bytes(DEFAULT_RUN), s,
-                       d, p, t);
+    hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
+                       lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
     return hipGetLastError();
 }
 #endif
