@@ -39,6 +39,16 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t k) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k);
@@ -1076,30 +1086,69 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
             // Burst of chained hops: while every cut lands on a window candidate
             // with no head hit after it (fix 0), the next cut is the candidate
             // nx[] names, if it lies below the read limit.  Those iterations of
-            // the loop below reduce to this scalar chain; the cuts are marked in
-            // a lane mask and written in parallel afterwards (one lane per cut).
+            // the loop below reduce to a chain through the window, found here
+            // in O(log 64) wave steps instead of one scalar hop per cut:
+            //   * list ranking by pointer jumping over f = nx (64 = the chain
+            //     ends: past the window, fix-up unknown or non-zero, no candidate);
+            //   * lane j lies on the chain from jlast iff f^(r[jlast]-r[j])(jlast) == j;
+            //   * the read limit after the m-th cut of the chain is
+            //     R_m = min(F, s_m + MAX, R_{m-1} + CAP)  (file_operations.rs:776)
+            //         = min(F, m*CAP + min(R_0, min_{i<=m} (s_i + MAX - i*CAP))),
+            //     a prefix minimum over the chain's lanes; the chain is cut
+            //     short at its first candidate at or past the limit before it.
+            // The cuts are then written in parallel (one lane per cut).
             if (head == 1 && fix == 0 && jlast >= 0 && !P.resolve_noburst) {
                 uint64_t mk = 0;
                 const Off s0 = s, n0 = cnt;
-                // nxv: the chain continues past a cut at lane j only if j's
-                // fix-up is known and zero; otherwise 64 ends the burst there
-                const uint32_t nxv = (wk & 0x1ffu) == 0x100u ? nx : 64u;
                 int j = jlast;
-                for (;;) {
-                    const uint32_t jn = (uint32_t)__builtin_amdgcn_readlane((int)nxv, j);
-                    if (jn >= 64) break;
-                    const Off c = rl(wr, jn);
-                    // c < s + 63: never for a sorted window; keeps the walk moving
-                    // forward after a candidate overflow (see the chained hop below)
-                    if (c < s + 63 || c >= R) break;                 // general iteration decides
-                    mk |= 1ull << jn;
-                    s = c + 1;                                       // cut = edge + 1 (:754-755, :771)
-                    Off rd = MAX - (R - s);                          // :776
-                    rd = min(rd, CAP);
-                    asm volatile("" : "+s"(rd));
-                    rd = min(rd, (Off)(Fo - R));
-                    R += rd;
-                    j = (int)jn;
+                uint32_t f = (wk & 0x1ffu) == 0x100u ? nx : 64u;
+                if (wr == OMAX || f <= (uint32_t)lane) f = 64u;     // past the file / unsorted (overflow re-run)
+                uint32_t rk = f < 64u ? 1u : 0u, nxt = f;
+                uint32_t J[6];                                      // J[k] = f^(2^k)
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    J[k] = nxt;
+                    const int src = (int)(nxt & 63u);
+                    const uint32_t rn = (uint32_t)__shfl((int)rk, src), nn = (uint32_t)__shfl((int)nxt, src);
+                    if (nxt < 64u) { rk += rn; nxt = nn; }
+                }
+                const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rk, j);
+                const uint32_t t = r0 - rk;                         // hops from jlast to this lane, if on the chain
+                const bool cand = lane > j && rk <= r0;
+                uint32_t x = (uint32_t)j;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    const uint32_t jx = (uint32_t)__shfl((int)J[k], (int)(x & 63u));
+                    if (((t >> k) & 1u) && x < 64u) x = jx;
+                }
+                const bool on = cand && x == (uint32_t)lane;
+                const unsigned long long pm = __ballot(on);
+                if (pm) {
+                    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+                    const int64_t capv = (int64_t)CAP, maxv = (int64_t)MAX;
+                    const int64_t m = on ? (int64_t)__builtin_popcountll(pm & lt) + 1 : 0;
+                    int64_t a = on ? (int64_t)wr + 1 + maxv - m * capv : INT64_MAX;
+#pragma unroll
+                    for (int off = 1; off < 64; off <<= 1) {        // inclusive prefix minimum
+                        const int64_t u = (int64_t)shfl_up64((uint64_t)a, off);
+                        if (lane >= off && u < a) a = u;
+                    }
+                    const int64_t R0 = (int64_t)R, Fv = (int64_t)Fo;
+                    const int64_t B = a < R0 ? a : R0;
+                    int64_t Rm = m * capv + B;
+                    if (Rm > Fv) Rm = Fv;
+                    const unsigned long long below = pm & lt;
+                    const int pl = below ? 63 - __builtin_clzll(below) : 0;
+                    const int64_t Rprev = below ? (int64_t)shfl64((uint64_t)Rm, pl) : R0;
+                    const int64_t wprev = below ? (int64_t)(Off)__shfl((int)wr, pl) : (int64_t)s - 1;
+                    const bool ok = on && (int64_t)wr < Rprev && (int64_t)wr >= wprev + 64;
+                    const unsigned long long bad = __ballot(on && !ok);
+                    mk = bad ? pm & ((1ull << __builtin_ctzll(bad)) - 1ull) : pm;
+                    if (mk) {
+                        j = 63 - __builtin_clzll(mk);
+                        s = rl(wr, (uint32_t)j) + 1;                 // cut = edge + 1 (:754-755, :771)
+                        R = (Off)readlane64((uint64_t)Rm, (uint32_t)j);
+                    }
                 }
                 if (mk) {
                     cnt += (Off)__builtin_popcountll(mk);
