@@ -1139,8 +1139,13 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     if (Rm > Fv) Rm = Fv;
                     const unsigned long long below = pm & lt;
                     const int pl = below ? 63 - __builtin_clzll(below) : 0;
-                    const int64_t Rprev = below ? (int64_t)shfl64((uint64_t)Rm, pl) : R0;
-                    const int64_t wprev = below ? (int64_t)(Off)__shfl((int)wr, pl) : (int64_t)s - 1;
+                    // shuffles with every lane active: under a per-lane condition the
+                    // source lane (the chain's first lane has no predecessor) would be
+                    // inactive and read back as 0
+                    const int64_t Rsh = (int64_t)shfl64((uint64_t)Rm, pl);
+                    const int64_t wsh = (int64_t)(Off)__shfl((int)wr, pl);
+                    const int64_t Rprev = below ? Rsh : R0;
+                    const int64_t wprev = below ? wsh : (int64_t)s - 1;
                     const bool ok = on && (int64_t)wr < Rprev && (int64_t)wr >= wprev + 64;
                     const unsigned long long bad = __ballot(on && !ok);
                     mk = bad ? pm & ((1ull << __builtin_ctzll(bad)) - 1ull) : pm;

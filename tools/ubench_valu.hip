@@ -32,10 +32,18 @@
                  INSN " %0, %0, %1\n\t" INSN " %0, %0, %1"                             \
                  : "+v"(a0) : "v"(k))
 
-constexpr int NOPS = 12;
+#define SDWA8(INSN)                                                                                    \
+    asm volatile(INSN " %0, %0, %8 src1_sel:BYTE_1\n\t" INSN " %1, %1, %8 src1_sel:BYTE_1\n\t"             \
+                 INSN " %2, %2, %8 src1_sel:BYTE_1\n\t" INSN " %3, %3, %8 src1_sel:BYTE_1\n\t"             \
+                 INSN " %4, %4, %8 src1_sel:BYTE_1\n\t" INSN " %5, %5, %8 src1_sel:BYTE_1\n\t"             \
+                 INSN " %6, %6, %8 src1_sel:BYTE_1\n\t" INSN " %7, %7, %8 src1_sel:BYTE_1"                   \
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) \
+                 : "v"(k))
+
+constexpr int NOPS = 15;
 const char *names[NOPS] = {"v_add_u32", "v_xor_b32", "v_add3_u32", "v_alignbit_b32(12)", "v_pk_add_u16",
                            "v_pk_mad_u16", "v_pk_min_u16", "v_perm_b32", "v_dot4_u32_u8", "v_lshl_add_u32",
-                           "dep v_add_u32", "dep v_xor_b32"};
+                           "dep v_add_u32", "dep v_xor_b32", "v_add_u32_e64", "v_add_u32_sdwa", "v_min_u16"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void kern(unsigned *out, unsigned long long *clk, unsigned seed, int iters) {
@@ -55,6 +63,9 @@ __global__ __launch_bounds__(256) void kern(unsigned *out, unsigned long long *c
         if (OP == 9) OP8_3("v_lshl_add_u32");
         if (OP == 10) DEP8("v_add_u32");
         if (OP == 11) DEP8("v_xor_b32");
+        if (OP == 12) OP8("v_add_u32_e64");
+        if (OP == 13) SDWA8("v_add_u32_sdwa");
+        if (OP == 14) OP8("v_min_u16");
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
@@ -90,7 +101,7 @@ void run(unsigned *d, unsigned long long *clk, int cus, int per_simd, int iters)
 
 template <int OP>
 void all(unsigned *d, unsigned long long *clk, int cus) {
-    for (int w : {1, 2, 4}) run<OP>(d, clk, cus, w, 20000);
+    for (int w : {1, 2, 3, 4}) run<OP>(d, clk, cus, w, 20000);
 }
 
 int main() {
@@ -103,6 +114,7 @@ int main() {
     all<0>(d, clk, cus); all<1>(d, clk, cus); all<2>(d, clk, cus); all<3>(d, clk, cus);
     all<4>(d, clk, cus); all<5>(d, clk, cus); all<6>(d, clk, cus); all<7>(d, clk, cus);
     all<8>(d, clk, cus); all<9>(d, clk, cus); all<10>(d, clk, cus); all<11>(d, clk, cus);
+    all<12>(d, clk, cus); all<13>(d, clk, cus); all<14>(d, clk, cus);
     hipFree(d);
     hipFree(clk);
     return 0;
