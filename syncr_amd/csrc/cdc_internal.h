@@ -63,10 +63,11 @@ struct KParams {
     uint32_t k;        // scalar k
     uint64_t max_chunk;
     uint64_t read_cap; // 0 = unlimited (ideal semantics)
-    uint32_t ablate;   // timing-only diagnostics (SYNCR_CDC_ABLATE): 1 = no rolling, 2 = no DMA, 3 = 1 with nt
+    uint32_t ablate;   // development library only (SYNCR_CDC_ABLATE): scan variants / timing-only ablations
     uint32_t nt;       // 1: non-temporal tile loads (SYNCR_CDC_NT=1)
-    uint32_t resolve_lane;  // 1: lane-per-file resolve (SYNCR_CDC_RESOLVE=lane); 0: wave-per-file
-    uint32_t resolve_noburst;  // 1: no burst of chained hops in the wave resolve (SYNCR_CDC_RESOLVE=noburst, A/B)
+    uint32_t resolve_lane;  // 1: lane-per-file resolve (SYNCR_CDC_FLAG_RESOLVE_LANE); 0: wave-per-file
+    uint32_t resolve_noburst;  // 1: no burst of chained hops in the wave resolve (SYNCR_CDC_FLAG_RESOLVE_NOBURST)
+    uint32_t fuse_fix;         // 1 (product): head fix-ups inside the dense / gather launches; 0: dev A/B only
 };
 
 struct DevCut {        // == syncr_cut

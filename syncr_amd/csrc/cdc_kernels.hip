@@ -330,9 +330,10 @@ __device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, u
 // 1.591 vs 1.640 ms, profiles/r02_ab_roll2.log).
 constexpr int SCAN_PRODUCT_MODE = 4 | 8 | 16;
 
+// MODE bit 5: ask for 3 waves per SIMD (VGPRs <= 168; development A/B only)
 template <int RUN, int MODE>
-__global__ __launch_bounds__(64) void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P,
-                                                      Tables T) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((MODE & 32) ? 3 : 1)))
+void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int BUF = buf_bytes(RUN);
     constexpr int TILE = tile_bytes(RUN);
@@ -621,6 +622,72 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
 // for p >= f+63 inside a file starting at f.  The 63 head positions of a file
 // are the resolve's head scan at s = 0 (a fresh window at f, exactly as after
 // any cut), so file starts need no kernel of their own.
+// Head fix-ups, computed before the resolve so its serial walk never waits
+// on byte loads: of every candidate e (first chunk-local hit in [e+1, e+63],
+// by the gather kernel) and of every read-boundary grid point (first
+// chunk-local hit in [p, min(p+63, file end)), stored as offset + 1, by the
+// dense kernel's launch).
+// First chunk-local hit in [e+1, e+63] (as k = hit - e; 0 = none) for a chunk
+// starting at e+1, from global memory.  The window's bytes are fetched in one
+// round: four unaligned 16-byte loads (gfx950 global loads are
+// unaligned-capable) when the 64 bytes after e lie inside the batch.  Bytes at
+// or past `lim` are outside the file: no hit there.
+__device__ __forceinline__ uint32_t head_fix_fast(const uint8_t *__restrict__ data, uint64_t span, uint64_t lim,
+                                                  uint64_t e, uint32_t mask) {
+    const uint64_t a = e + 1;
+    uint32_t w[16];
+    if (a + 64 <= span) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint4 v;
+            __builtin_memcpy(&v, data + a + 16 * i, 16);
+            w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            uint32_t x = 0;
+            for (int b = 0; b < 4; ++b)
+                if (a + 4 * i + b < span) x |= (uint32_t)data[a + 4 * i + b] << (8 * b);
+            w[i] = x;
+        }
+    }
+    const uint32_t n = lim > a ? (uint32_t)min<uint64_t>(63ull, lim - a) : 0u;
+    uint32_t S = 0, W = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 63; ++k) {
+        const uint32_t x = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+        S += x;
+        W += S;
+        if (k < n && hit_exact(S, W, mask)) return k + 1;
+    }
+    return 0;
+}
+
+#ifdef SYNCR_CDC_DEV
+// Development A/B (SYNCR_CDC_FUSEFIX=0): the round-1 separate fix-up launch,
+// one thread per candidate and per grid point.
+__global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict__ data, KParams P,
+                                                      Tables T) {
+    const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
+    const uint64_t n = total < T.cand_cap ? total : T.cand_cap;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n + T.ngrid; i += (uint64_t)gridDim.x * 256) {
+        if (i < n) {
+            const uint64_t e = T.cand[i] & CAND_POS_MASK;
+            const uint32_t fix = head_fix_fast(data, T.span, T.span, e, P.mask);
+            T.cand[i] = e | ((uint64_t)fix << 48) | CAND_KNOWN;
+        } else {
+            const uint64_t g = i - n;
+            const uint64_t p = T.gpos[g];
+            // head_fix_fast(p - 1) scans [p, p+63) with the window reset at p
+            const uint64_t end = T.gend[g];
+            uint32_t f = head_fix_fast(data, T.span, end, p - 1, P.mask);
+            T.gfix[g] = (uint8_t)f;
+        }
+    }
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // Dense tiles (more than LISTCAP candidates: low-entropy / periodic /
 // adversarial data): recompute G for every position of the tile into a bitmap
@@ -631,11 +698,20 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
 // bitmap word as four ds_read_b128.  Stream semantics like the scan: no resets
 // at file starts (file heads are the resolve's head scan).
 // ---------------------------------------------------------------------------
+// GRID: the launch also computes the head fix-ups of the read-boundary grid
+// points (no scan output needed), saving the separate fix-up launch.
+template <bool GRID>
 __global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict__ data, KParams P,
                                                        Tables T) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dbuf[];   // [HALO + tile]
-    const uint32_t nd = min(T.ctr[CTR_DENSE], T.dense_cap);
     const int lane = threadIdx.x;
+    if constexpr (GRID) {
+        for (uint32_t g = blockIdx.x * 64u + (uint32_t)lane; g < T.ngrid; g += gridDim.x * 64u) {
+            // head_fix_fast(p - 1) scans [p, p+63) with the window reset at p
+            T.gfix[g] = (uint8_t)head_fix_fast(data, T.span, T.gend[g], T.gpos[g] - 1, P.mask);
+        }
+    }
+    const uint32_t nd = min(T.ctr[CTR_DENSE], T.dense_cap);
     const uint32_t TB = T.tile, BUFB = HALO + TB;
     const uint32_t per_lane = TB / 64;                   // 2 * RUN: a multiple of 32
     const uint32_t words_lane = per_lane / 32;
@@ -763,7 +839,10 @@ __global__ __launch_bounds__(1024) void cdc_prefix_kernel(Tables T) {
 // lane copies its slot list; the wave then walks the group's dense tiles
 // together: 64 bitmap words at a time, a wave prefix of their popcounts gives
 // each lane its output run.
-__global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
+// FIX: each candidate is stored with its head fix-up (head_fix_fast), which
+// the separate fix-up launch computed in round 1.
+template <bool FIX>
+__global__ __launch_bounds__(256) void cdc_gather_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (w >= T.nwords) return;
@@ -787,7 +866,11 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
     if (has && c && !dense && base + c <= T.cand_cap) {   // overflow is flagged by prefix; host re-runs
         const uint64_t t0 = (uint64_t)tile * T.tile;
         const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
-        for (uint32_t j = 0; j < c; ++j) T.cand[base + j] = t0 + sl[j].x;    // fix-up: cdc_fix_kernel
+        for (uint32_t j = 0; j < c; ++j) {
+            const uint64_t e = t0 + sl[j].x;
+            T.cand[base + j] = FIX ? (e | ((uint64_t)head_fix_fast(data, T.span, T.span, e, P.mask) << 48) | CAND_KNOWN)
+                                   : e;
+        }
     }
     unsigned long long dm = __ballot(dense);
     const uint32_t nw = T.tile / 32;
@@ -808,71 +891,12 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
             const uint32_t ic = wave_incl_scan(pc, lane);
             uint64_t q = o + (ic - pc);
             while (m) {
-                T.cand[q++] = t0 + wi * 32u + (uint32_t)__builtin_ctz(m);
+                const uint64_t e = t0 + wi * 32u + (uint32_t)__builtin_ctz(m);
+                T.cand[q++] = FIX ? (e | ((uint64_t)head_fix_fast(data, T.span, T.span, e, P.mask) << 48) | CAND_KNOWN)
+                                  : e;
                 m &= m - 1;
             }
             o += (uint32_t)__builtin_amdgcn_readlane((int)ic, 63);
-        }
-    }
-}
-
-// Head fix-up of every candidate e (first chunk-local hit in [e+1, e+63]),
-// one thread per candidate, so the resolve walk never waits on byte loads;
-// then the head hit of every read-boundary grid point (first chunk-local hit
-// in [p, min(p+63, file end)), stored as offset + 1).
-// First chunk-local hit in [e+1, e+63] (as k = hit - e; 0 = none) for a chunk
-// starting at e+1, from global memory.  The window's bytes are fetched in one
-// round: four unaligned 16-byte loads (gfx950 global loads are
-// unaligned-capable) when the 64 bytes after e lie inside the batch.  Bytes at
-// or past `lim` are outside the file: no hit there.
-__device__ __forceinline__ uint32_t head_fix_fast(const uint8_t *__restrict__ data, uint64_t span, uint64_t lim,
-                                                  uint64_t e, uint32_t mask) {
-    const uint64_t a = e + 1;
-    uint32_t w[16];
-    if (a + 64 <= span) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            uint4 v;
-            __builtin_memcpy(&v, data + a + 16 * i, 16);
-            w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            uint32_t x = 0;
-            for (int b = 0; b < 4; ++b)
-                if (a + 4 * i + b < span) x |= (uint32_t)data[a + 4 * i + b] << (8 * b);
-            w[i] = x;
-        }
-    }
-    const uint32_t n = lim > a ? (uint32_t)min<uint64_t>(63ull, lim - a) : 0u;
-    uint32_t S = 0, W = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 63; ++k) {
-        const uint32_t x = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        S += x;
-        W += S;
-        if (k < n && hit_exact(S, W, mask)) return k + 1;
-    }
-    return 0;
-}
-
-__global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict__ data, KParams P,
-                                                      Tables T) {
-    const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
-    const uint64_t n = total < T.cand_cap ? total : T.cand_cap;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n + T.ngrid; i += (uint64_t)gridDim.x * 256) {
-        if (i < n) {
-            const uint64_t e = T.cand[i] & CAND_POS_MASK;
-            const uint32_t fix = head_fix_fast(data, T.span, T.span, e, P.mask);
-            T.cand[i] = e | ((uint64_t)fix << 48) | CAND_KNOWN;
-        } else {
-            const uint64_t g = i - n;
-            const uint64_t p = T.gpos[g];
-            // head_fix_fast(p - 1) scans [p, p+63) with the window reset at p
-            const uint64_t end = T.gend[g];
-            uint32_t f = head_fix_fast(data, T.span, end, p - 1, P.mask);
-            T.gfix[g] = (uint8_t)f;
         }
     }
 }
@@ -1471,6 +1495,9 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 6u)                                         // timing only: roll, no DMA
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 7u)                                         // A/B: product + 3 waves per SIMD hint
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, d, p,
+                           t);
     else if (p.nt)                                                   // product: nt loads + dynamic groups + ROLL2
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else
@@ -1560,17 +1587,22 @@ int scan_blocks_per_cu(ScanGeom g) {
 hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s,
                        hipEvent_t) {
     if (!t.ntiles) return hipSuccess;
-    if (t.dense_cap) {
-        const uint32_t blocks = t.dense_cap < 2048u ? t.dense_cap : 2048u;
-        hipLaunchKernelGGL(cdc_dense_kernel, dim3(blocks), dim3(64), HALO + t.tile, s, d, p, t);
-    }
-    hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
-    hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4), dim3(256), 0, s, t);
-    {
+    const uint32_t dblocks = t.dense_cap < 2048u ? (t.dense_cap ? t.dense_cap : 1u) : 2048u;
+#ifdef SYNCR_CDC_DEV
+    if (!p.fuse_fix) {                                   // A/B: round-1 sequence with the fix-up launch
+        hipLaunchKernelGGL(cdc_dense_kernel<false>, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
+        hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
+        hipLaunchKernelGGL(cdc_gather_kernel<false>, dim3((t.nwords + 3) / 4), dim3(256), 0, s, d, p, t);
         const uint64_t want = (t.cand_cap + t.ngrid + 255) / 256;
         const uint32_t blocks = (uint32_t)(want < 2048 ? (want ? want : 1) : 2048);
         hipLaunchKernelGGL(cdc_fix_kernel, dim3(blocks), dim3(256), 0, s, d, p, t);
+        return hipGetLastError();
     }
+#endif
+    // dense tiles + grid-point fix-ups, prefix, gather + candidate fix-ups
+    hipLaunchKernelGGL(cdc_dense_kernel<true>, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
+    hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
+    hipLaunchKernelGGL(cdc_gather_kernel<true>, dim3((t.nwords + 3) / 4), dim3(256), 0, s, d, p, t);
     return hipGetLastError();
 }
 
