@@ -136,7 +136,6 @@ KParams make_kparams(const syncr_cdc_params &p) {
     k.max_chunk = p.max_chunk;
     k.read_cap = p.read_cap;
     k.nt = 1;              // tile bytes are read once: non-temporal loads
-    k.fuse_fix = 1;
     // exact alternative resolves, for cross-checks (include/syncr_cdc.h)
     k.resolve_lane = (p.flags & SYNCR_CDC_FLAG_RESOLVE_LANE) ? 1u : 0u;
     k.resolve_noburst = (p.flags & SYNCR_CDC_FLAG_RESOLVE_NOBURST) ? 1u : 0u;
@@ -398,7 +397,6 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
         h->kp.resolve_noburst = strcmp(rs, "noburst") == 0;
     }
     if (const char *a = getenv("SYNCR_CDC_SERIAL")) h->serial_scans = atoi(a) != 0;
-    if (const char *a = getenv("SYNCR_CDC_FUSEFIX")) h->kp.fuse_fix = atoi(a) != 0;
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
     if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
     if (const char *ld = getenv("SYNCR_B3_LOAD")) h->b3_coop = strcmp(ld, "plain") != 0;   // A/B only

@@ -67,7 +67,6 @@ struct KParams {
     uint32_t nt;       // 1: non-temporal tile loads (SYNCR_CDC_NT=1)
     uint32_t resolve_lane;  // 1: lane-per-file resolve (SYNCR_CDC_FLAG_RESOLVE_LANE); 0: wave-per-file
     uint32_t resolve_noburst;  // 1: no burst of chained hops in the wave resolve (SYNCR_CDC_FLAG_RESOLVE_NOBURST)
-    uint32_t fuse_fix;         // 1 (product): head fix-ups inside the dense / gather launches; 0: dev A/B only
 };
 
 struct DevCut {        // == syncr_cut

@@ -623,10 +623,9 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
 // are the resolve's head scan at s = 0 (a fresh window at f, exactly as after
 // any cut), so file starts need no kernel of their own.
 // Head fix-ups, computed before the resolve so its serial walk never waits
-// on byte loads: of every candidate e (first chunk-local hit in [e+1, e+63],
-// by the gather kernel) and of every read-boundary grid point (first
-// chunk-local hit in [p, min(p+63, file end)), stored as offset + 1, by the
-// dense kernel's launch).
+// on byte loads: of every candidate e (first chunk-local hit in [e+1, e+63])
+// and of every read-boundary grid point (first chunk-local hit in
+// [p, min(p+63, file end)), stored as offset + 1).
 // First chunk-local hit in [e+1, e+63] (as k = hit - e; 0 = none) for a chunk
 // starting at e+1, from global memory.  The window's bytes are fetched in one
 // round: four unaligned 16-byte loads (gfx950 global loads are
@@ -664,9 +663,10 @@ __device__ __forceinline__ uint32_t head_fix_fast(const uint8_t *__restrict__ da
     return 0;
 }
 
-#ifdef SYNCR_CDC_DEV
-// Development A/B (SYNCR_CDC_FUSEFIX=0): the round-1 separate fix-up launch,
-// one thread per candidate and per grid point.
+// One thread per candidate and per grid point.  (Fusing these into the dense
+// and gather launches -- no separate launch -- measured 8 us SLOWER per step on
+// zipf10k: the per-lane serial fix-ups lengthen the gather's critical path;
+// profiles/r02_ab_run_fusefix.log.)
 __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict__ data, KParams P,
                                                       Tables T) {
     const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
@@ -686,7 +686,6 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
         }
     }
 }
-#endif
 
 // ---------------------------------------------------------------------------
 // Dense tiles (more than LISTCAP candidates: low-entropy / periodic /
@@ -698,19 +697,10 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
 // bitmap word as four ds_read_b128.  Stream semantics like the scan: no resets
 // at file starts (file heads are the resolve's head scan).
 // ---------------------------------------------------------------------------
-// GRID: the launch also computes the head fix-ups of the read-boundary grid
-// points (no scan output needed), saving the separate fix-up launch.
-template <bool GRID>
 __global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict__ data, KParams P,
                                                        Tables T) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dbuf[];   // [HALO + tile]
     const int lane = threadIdx.x;
-    if constexpr (GRID) {
-        for (uint32_t g = blockIdx.x * 64u + (uint32_t)lane; g < T.ngrid; g += gridDim.x * 64u) {
-            // head_fix_fast(p - 1) scans [p, p+63) with the window reset at p
-            T.gfix[g] = (uint8_t)head_fix_fast(data, T.span, T.gend[g], T.gpos[g] - 1, P.mask);
-        }
-    }
     const uint32_t nd = min(T.ctr[CTR_DENSE], T.dense_cap);
     const uint32_t TB = T.tile, BUFB = HALO + TB;
     const uint32_t per_lane = TB / 64;                   // 2 * RUN: a multiple of 32
@@ -839,10 +829,7 @@ __global__ __launch_bounds__(1024) void cdc_prefix_kernel(Tables T) {
 // lane copies its slot list; the wave then walks the group's dense tiles
 // together: 64 bitmap words at a time, a wave prefix of their popcounts gives
 // each lane its output run.
-// FIX: each candidate is stored with its head fix-up (head_fix_fast), which
-// the separate fix-up launch computed in round 1.
-template <bool FIX>
-__global__ __launch_bounds__(256) void cdc_gather_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
+__global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
     const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (w >= T.nwords) return;
@@ -866,11 +853,7 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(const uint8_t *__restri
     if (has && c && !dense && base + c <= T.cand_cap) {   // overflow is flagged by prefix; host re-runs
         const uint64_t t0 = (uint64_t)tile * T.tile;
         const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
-        for (uint32_t j = 0; j < c; ++j) {
-            const uint64_t e = t0 + sl[j].x;
-            T.cand[base + j] = FIX ? (e | ((uint64_t)head_fix_fast(data, T.span, T.span, e, P.mask) << 48) | CAND_KNOWN)
-                                   : e;
-        }
+        for (uint32_t j = 0; j < c; ++j) T.cand[base + j] = t0 + sl[j].x;    // fix-up: cdc_fix_kernel
     }
     unsigned long long dm = __ballot(dense);
     const uint32_t nw = T.tile / 32;
@@ -891,9 +874,7 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(const uint8_t *__restri
             const uint32_t ic = wave_incl_scan(pc, lane);
             uint64_t q = o + (ic - pc);
             while (m) {
-                const uint64_t e = t0 + wi * 32u + (uint32_t)__builtin_ctz(m);
-                T.cand[q++] = FIX ? (e | ((uint64_t)head_fix_fast(data, T.span, T.span, e, P.mask) << 48) | CAND_KNOWN)
-                                  : e;
+                T.cand[q++] = t0 + wi * 32u + (uint32_t)__builtin_ctz(m);
                 m &= m - 1;
             }
             o += (uint32_t)__builtin_amdgcn_readlane((int)ic, 63);
@@ -1034,12 +1015,24 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
     uint32_t wk = 0, nx = 64;
     // the window after the current one is loaded ahead (a slide then costs no
     // dependent HBM round trip on this serial walk)
+    // unconditional load of the raw word (clamped index; entries past ncand are
+    // masked when the window is consumed): an exec-predicated load, or using
+    // the value at issue, makes the waitcnt pass drain vmcnt(0) right there,
+    // which defeats the prefetch
     auto fetch = [&](uint64_t b) -> uint64_t {
-        return b + (uint64_t)lane < ncand ? T.cand[b + lane] : NONE;
+        const uint64_t k = b + (uint64_t)lane;
+        return T.cand[k < ncand ? k : 0];
     };
-    uint64_t pf_cur = fetch(wb), pf_next = fetch(wb + 64);
+    // PF windows ahead: a slide then waits only for a load issued PF-1 windows
+    // earlier (a chained walk cuts a 64-candidate window in ~1 us, an HBM
+    // round trip is ~2 us)
+    constexpr int PF = 4;
+    uint64_t pf[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) pf[k] = fetch(wb + 64ull * k);
+    uint64_t &pf_cur = pf[0];
     auto load_window = [&]() {
-        const uint64_t c = pf_cur;
+        const uint64_t c = wb + (uint64_t)lane < ncand ? pf_cur : NONE;
         wr = OMAX;
         wk = 0;
         if (c != NONE) {
@@ -1280,8 +1273,9 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     }
                     if (wb + 64 >= ncand) break;             // whole window below `from`: slide
                     wb += 64;
-                    pf_cur = pf_next;
-                    pf_next = fetch(wb + 64);
+#pragma unroll
+                    for (int k = 0; k + 1 < PF; ++k) pf[k] = pf[k + 1];
+                    pf[PF - 1] = fetch(wb + 64ull * (PF - 1));
                     load_window();
                 }
             }
@@ -1588,21 +1582,12 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
                        hipEvent_t) {
     if (!t.ntiles) return hipSuccess;
     const uint32_t dblocks = t.dense_cap < 2048u ? (t.dense_cap ? t.dense_cap : 1u) : 2048u;
-#ifdef SYNCR_CDC_DEV
-    if (!p.fuse_fix) {                                   // A/B: round-1 sequence with the fix-up launch
-        hipLaunchKernelGGL(cdc_dense_kernel<false>, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
-        hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
-        hipLaunchKernelGGL(cdc_gather_kernel<false>, dim3((t.nwords + 3) / 4), dim3(256), 0, s, d, p, t);
-        const uint64_t want = (t.cand_cap + t.ngrid + 255) / 256;
-        const uint32_t blocks = (uint32_t)(want < 2048 ? (want ? want : 1) : 2048);
-        hipLaunchKernelGGL(cdc_fix_kernel, dim3(blocks), dim3(256), 0, s, d, p, t);
-        return hipGetLastError();
-    }
-#endif
-    // dense tiles + grid-point fix-ups, prefix, gather + candidate fix-ups
-    hipLaunchKernelGGL(cdc_dense_kernel<true>, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
+    hipLaunchKernelGGL(cdc_dense_kernel, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
     hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
-    hipLaunchKernelGGL(cdc_gather_kernel<true>, dim3((t.nwords + 3) / 4), dim3(256), 0, s, d, p, t);
+    hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4), dim3(256), 0, s, t);
+    const uint64_t want = (t.cand_cap + t.ngrid + 255) / 256;
+    const uint32_t blocks = (uint32_t)(want < 2048 ? (want ? want : 1) : 2048);
+    hipLaunchKernelGGL(cdc_fix_kernel, dim3(blocks), dim3(256), 0, s, d, p, t);
     return hipGetLastError();
 }
 
