@@ -1026,7 +1026,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
     // PF windows ahead: a slide then waits only for a load issued PF-1 windows
     // earlier (a chained walk cuts a 64-candidate window in ~1 us, an HBM
     // round trip is ~2 us)
-    constexpr int PF = 4;
+    constexpr int PF = 2;         // 4 measured no faster on dense1 (the slide is not load-bound)
     uint64_t pf[PF];
 #pragma unroll
     for (int k = 0; k < PF; ++k) pf[k] = fetch(wb + 64ull * k);
@@ -1120,26 +1120,40 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                 int j = jlast;
                 uint32_t f = (wk & 0x1ffu) == 0x100u ? nx : 64u;
                 if (wr == OMAX || f <= (uint32_t)lane) f = 64u;     // past the file / unsorted (overflow re-run)
-                uint32_t rk = f < 64u ? 1u : 0u, nxt = f;
-                uint32_t J[6];                                      // J[k] = f^(2^k)
+                // fast path: a chain of consecutive lanes (nx[j] == j + 1, periodic
+                // data) ending in the window or at a lane whose chain ends
+                const unsigned long long contig = __ballot(f == (uint32_t)lane + 1u);   // f == 64 at lane 63: end
+                const unsigned long long fromj = contig >> j;
+                const uint32_t run = ~fromj ? (uint32_t)__builtin_ctzll(~fromj) : 64u - (uint32_t)j;
+                const uint32_t last = (uint32_t)j + run;            // reached; its own f is not last + 1
+                const uint32_t flast = last < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)f, (int)last) : 64u;
+                unsigned long long pm;
+                if (flast >= 64u) {
+                    const unsigned long long upto = last >= 63u ? ~0ull : ((2ull << last) - 1ull);   // lanes <= last
+                    const unsigned long long thru = j >= 63 ? ~0ull : ((2ull << j) - 1ull);          // lanes <= j
+                    pm = upto & ~thru;
+                } else {
+                    uint32_t rk = f < 64u ? 1u : 0u, nxt = f;
+                    uint32_t J[6];                                  // J[k] = f^(2^k)
 #pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    J[k] = nxt;
-                    const int src = (int)(nxt & 63u);
-                    const uint32_t rn = (uint32_t)__shfl((int)rk, src), nn = (uint32_t)__shfl((int)nxt, src);
-                    if (nxt < 64u) { rk += rn; nxt = nn; }
-                }
-                const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rk, j);
-                const uint32_t t = r0 - rk;                         // hops from jlast to this lane, if on the chain
-                const bool cand = lane > j && rk <= r0;
-                uint32_t x = (uint32_t)j;
+                    for (int k = 0; k < 6; ++k) {
+                        J[k] = nxt;
+                        const int src = (int)(nxt & 63u);
+                        const uint32_t rn = (uint32_t)__shfl((int)rk, src), nn = (uint32_t)__shfl((int)nxt, src);
+                        if (nxt < 64u) { rk += rn; nxt = nn; }
+                    }
+                    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)rk, j);
+                    const uint32_t t = r0 - rk;                     // hops from jlast to this lane, if on the chain
+                    const bool cand = lane > j && rk <= r0;
+                    uint32_t x = (uint32_t)j;
 #pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    const uint32_t jx = (uint32_t)__shfl((int)J[k], (int)(x & 63u));
-                    if (((t >> k) & 1u) && x < 64u) x = jx;
+                    for (int k = 0; k < 6; ++k) {
+                        const uint32_t jx = (uint32_t)__shfl((int)J[k], (int)(x & 63u));
+                        if (((t >> k) & 1u) && x < 64u) x = jx;
+                    }
+                    pm = __ballot(cand && x == (uint32_t)lane);
                 }
-                const bool on = cand && x == (uint32_t)lane;
-                const unsigned long long pm = __ballot(on);
+                const bool on = (pm >> lane) & 1ull;
                 if (pm) {
                     const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
                     const int64_t capv = (int64_t)CAP, maxv = (int64_t)MAX;
