@@ -2,13 +2,20 @@
 """Summarise a tools/prof.sh run (gpurun_out/prof_<tag>/) into profiles/.
 
 Writes
-  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
-  profiles/<tag>_pmc_traffic.json   HBM bytes per cdc_scan_kernel launch
-  profiles/<tag>_bench_trace.json   the bench JSON line of the traced run
+  profiles/<tag>_kernel_stats.csv     rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<tag>_bench_trace.json     the bench JSON line of the traced run
+  profiles/<tag>_dispatches.json      scan / BLAKE3-leaf durations per dispatch, in order, and the
+                                      mean over the bench's timed window vs over every launch
+  profiles/<tag>_pmc_traffic.json     HBM bytes per launch: scan (main) and every other kernel
+  profiles/<tag>_pmc_sq.json          per scan dispatch: shader clock and SQ instruction counters
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB
 and collected in separate passes; on gfx950 FETCH_SIZE reports exactly half of
 the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled.
+That correction is calibrated for the scan's access pattern (1 KiB contiguous
+per wave instruction; the read probe lands at 1.000x); other patterns (the
+BLAKE3 leaf's 64-byte runs) are uncalibrated, so their doubled figure is an
+upper bound (see `correction` in the JSON).
 """
 import csv
 import json
@@ -20,15 +27,19 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def short(name):
+    n = name.split("(")[0].replace("void ", "")
+    if "cdc_scan_kernel" in n:
+        return "cdc::cdc_scan_kernel"
+    if "b3_leaf_kernel" in n:
+        return "cdc::b3_leaf_kernel"
+    return n
+
+
 def counters(path):
     agg = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        if "cdc_scan_kernel" in name:
-            name = "cdc::cdc_scan_kernel"
-        if "b3_leaf_kernel" in name:
-            name = "cdc::b3_leaf_kernel"
-        agg[(name, r["Counter_Name"])].append(float(r["Counter_Value"]))
+        agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
     return agg
 
 
@@ -39,6 +50,26 @@ def bench_line(log):
     return None
 
 
+def dispatches(trace_csv, line):
+    rows = sorted(csv.DictReader(open(trace_csv)), key=lambda r: int(r["Start_Timestamp"]))
+    scans = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows
+             if short(r["Kernel_Name"]) == "cdc::cdc_scan_kernel"]
+    leaf = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows
+            if short(r["Kernel_Name"]) == "cdc::b3_leaf_kernel"]
+    w, k = (line or {}).get("warmup", 0), (line or {}).get("steps", 0)
+    timed = scans[w:w + k]                     # bench.py: W warm-up scans, then the K timed ones
+    mean = lambda v: sum(v) / len(v) if v else None   # noqa: E731
+    return {
+        "scan_ms_per_dispatch": [round(x, 4) for x in scans],
+        "scan_ms_mean_all": mean(scans), "scan_launches": len(scans),
+        "scan_ms_mean_timed_window": mean(timed), "timed_window": [w, w + k],
+        "bench_line_scan_ms": (line or {}).get("roofline", {}).get("kernel_ms"),
+        "leaf_ms_per_dispatch": [round(x, 4) for x in leaf], "leaf_ms_mean": mean(leaf),
+        "note": "rocprofv3 kernel-trace durations; the bench line's kernel_ms is the HIP-event mean over the "
+                "same timed window of an unprofiled-equivalent stream (profiling adds a few % per dispatch)",
+    }
+
+
 def main(tag, src=None):
     src = src or os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
@@ -46,30 +77,59 @@ def main(tag, src=None):
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     b = bench_line(os.path.join(src, "bench_trace.log"))
     json.dump(b, open(os.path.join(dst, f"{tag}_bench_trace.json"), "w"), indent=1)
+    json.dump(dispatches(os.path.join(src, "trace", "run_kernel_trace.csv"), b),
+              open(os.path.join(dst, f"{tag}_dispatches.json"), "w"), indent=1)
     f = counters(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
     w = counters(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
+    fb = bench_line(os.path.join(src, "bench_fetch.log")) or {}
+    span = fb.get("config", {}).get("bytes_per_gpu")
+
+    def hbm(kname):
+        fv, wv = f.get((kname, "FETCH_SIZE"), []), w.get((kname, "WRITE_SIZE"), [])
+        if not fv:
+            return None
+        return 2 * 1024 * sum(fv) / len(fv) + (1024 * sum(wv) / len(wv) if wv else 0.0)
+
     k = "cdc::cdc_scan_kernel"
     fetch_kib = sum(f[(k, "FETCH_SIZE")]) / len(f[(k, "FETCH_SIZE")])
     write_kib = sum(w[(k, "WRITE_SIZE")]) / len(w[(k, "WRITE_SIZE")])
-    fb = json.load(open(os.path.join(dst, f"{tag}_bench_trace.json"))) if b else {}
-    span = fb.get("config", {}).get("bytes_per_gpu")
-    hbm = 2 * fetch_kib * 1024 + write_kib * 1024
+    scan_hbm = 2 * fetch_kib * 1024 + write_kib * 1024
+    kernels = sorted({kk[0] for kk in f})
     out = {
         "kernel": k, "workload": fb.get("config", {}).get("workload", "").split(":")[0],
         "run_bytes": fb.get("config", {}).get("engine", {}).get("run_bytes"),
         "span": span, "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
-        "hbm_bytes_per_launch": int(hbm), "algorithmic_bytes_per_launch": span,
-        "traffic_over_algorithmic": (hbm / span) if span else None,
-        "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halves wide streaming reads)",
+        "hbm_bytes_per_launch": int(scan_hbm), "algorithmic_bytes_per_launch": span,
+        "traffic_over_algorithmic": (scan_hbm / span) if span else None,
+        "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halves wide streaming reads; "
+                      "calibrated for 1 KiB-contiguous wave loads, an upper bound for the BLAKE3 leaf's 64-byte runs)",
         "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/prof.sh {tag}",
-        "other_kernels": {kk[0]: sum(v) / len(v) for kk, v in {**f, **w}.items() if kk[0] != k},
-        "per_kernel_hbm_bytes": {
-            kk[0]: int(2 * 1024 * sum(v) / len(v) + 1024 * (sum(w[(kk[0], "WRITE_SIZE")]) / max(len(w[(kk[0], "WRITE_SIZE")]), 1)))
-            for kk, v in f.items() if kk[1] == "FETCH_SIZE"},
+        "per_kernel_hbm_bytes": {kn: int(hbm(kn)) for kn in kernels if hbm(kn) is not None},
+        "per_kernel_traffic_over_span": {kn: round(hbm(kn) / span, 4) for kn in kernels
+                                         if hbm(kn) is not None and span},
     }
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w"), indent=1)
-    print(json.dumps(out, indent=1))
+    sq_csv = os.path.join(src, "pmc_sq", "run_counter_collection.csv")
+    if os.path.exists(sq_csv):
+        per = defaultdict(dict)
+        for r in csv.DictReader(open(sq_csv)):
+            if short(r["Kernel_Name"]) != k:
+                continue
+            d = per[int(r["Dispatch_Id"])]
+            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            d["dur_ms"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        rows = []
+        for disp in sorted(per):
+            d = per[disp]
+            clk = d.get("GRBM_GUI_ACTIVE", 0) / 8 / (d["dur_ms"] / 1e3) / 1e9 if d.get("dur_ms") else None
+            rows.append({"dispatch": disp, "ms": round(d["dur_ms"], 4), "clock_ghz": round(clk, 3) if clk else None,
+                         **{c: d[c] for c in d if c.startswith("SQ_")}})
+        json.dump({"kernel": k, "source": f"tools/prof.sh {tag} pass 4", "per_dispatch": rows,
+                   "units": "SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* in quad-cycles (MI355X_MICROARCH.md); "
+                            "clock = GRBM_GUI_ACTIVE / 8 XCDs / duration"},
+                  open(os.path.join(dst, f"{tag}_pmc_sq.json"), "w"), indent=1)
+    print(json.dumps({kk: v for kk, v in out.items() if kk != "per_kernel_hbm_bytes"}, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else None)
+    main(sys.argv[1] if len(sys.argv) > 1 else "r02", sys.argv[2] if len(sys.argv) > 2 else None)
