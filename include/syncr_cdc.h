@@ -163,8 +163,10 @@ int32_t syncr_cdc_format_chunks(const syncr_chunk_info *chunks, uint64_t n, int3
  * could not be opened or read, following compute_file_chunks: when the open or
  * the first read fails n = 0 (the reference's empty list,
  * file_operations.rs:727-744); when a later read fails, the chunks the
- * reference cuts before its loop breaks (:776-782).  A file that shrinks while
- * being read is chunked at the length read (status 0).  In callbacks chunk.file
+ * reference cuts before its loop breaks (:776-782).  A file is read at its
+ * fstat size: one that shrinks while being read is chunked at the length read
+ * (status 0); bytes appended after the fstat are not read (the reference reads
+ * to EOF).  In callbacks chunk.file
  * is 0.  A file larger than batch_bytes gets a batch of its own.  copy_threads:
  * host threads used for large copies / reads into pinned memory (1 = the caller
  * only). */

@@ -237,3 +237,28 @@ def test_multi_device_state_errors():
         g.commit(0)
         g.flush()
         assert [t for t, _, _ in g.results] == [0]
+
+
+def test_first_read_failure_is_empty(tmp_path):
+    """A directory opens but its first read fails (EISDIR): compute_file_chunks
+    warns and returns an empty list (file_operations.rs:738-743); the pipeline
+    reports -EISDIR with no chunks and keeps the order of the other files."""
+    files = corpus(6, 29, 2 * M)
+    paths = []
+    for i, f in enumerate(files):
+        p = tmp_path / f"f{i}.bin"
+        p.write_bytes(f.tobytes())
+        paths.append(str(p))
+    d = tmp_path / "subdir"
+    d.mkdir()
+    paths.insert(2, str(d))
+    for devices in (None, [0, 0]):
+        got = []
+        with syncr_amd.Ingest(batch_bytes=4 * M, depth=2, devices=devices,
+                              on_file=lambda t, s, a: got.append((t, s, a))) as g:
+            for i, p in enumerate(paths):
+                g.submit_file(p, i)
+            g.flush()
+        assert [t for t, _, _ in got] == list(range(len(paths)))
+        assert got[2][1] == -errno.EISDIR and got[2][2].size == 0
+        check([(i, s, a) for i, (_, s, a) in enumerate(got[:2] + got[3:])], files)
