@@ -278,6 +278,13 @@ __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
 }
 
 // ---------------------------------------------------------------------------
+// Loader kinds of the leaf kernel (template parameter LD): per-lane global
+// loads (LD_PLAIN, development A/B only), the cooperative LDS-DMA loader one
+// 64-byte block per task per issue round (LD_COOP64), or two blocks (one
+// 128-byte run) per task per round (LD_PAIR).
+constexpr int LD_PLAIN = 0, LD_COOP64 = 1, LD_PAIR = 2;
+
+// ---------------------------------------------------------------------------
 // Cooperative block loader (COOP): the wave steps through block index t in
 // lockstep (t < wave max of the tasks' block counts).  Block t+1 of all 64
 // tasks is fetched by four global_load_lds_dwordx4: instruction i moves one
@@ -293,7 +300,17 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-template <bool NT, int ABLATE>
+//
+// LD_PAIR: blocks t, t+1 (t even) of all 64 tasks are fetched together by
+// eight instructions (instruction i: tasks 8i..8i+7, one 128-byte run each),
+// into an 8 KiB slot (task q at slot + 128 q, 16-byte pieces of each 64-byte
+// half rotated by (q >> 1) & 3).  A 128-byte run at a line-aligned task start
+// is one L2 line, read once; the 64-byte rounds touch every line in two
+// consecutive rounds, and the second touch misses L2 for a third of the
+// lines (profiles/r02_fetch_calibration.json: 1.34x the input bytes).
+// The next pair is issued once block t+1 is in registers, so it lands under
+// block t+1's compression, as the single-block round lands under block t's.
+template <bool NT, int ABLATE, int LD>
 __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ data, uint64_t span, uint32_t stage,
                                                  uint32_t *stage_ptr, int lane, bool act, uint64_t tp,
                                                  uint32_t nbytes, uint32_t nblk, uint32_t nl, uint32_t nleaves,
@@ -311,22 +328,36 @@ __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ dat
     // the piece sources are re-derived from the owners' registers at every
     // issue (ds_bpermute): holding four 64-bit sources and limits across the
     // compression cost 5 -> 4 waves/SIMD
-    auto issue = [&](uint32_t t) {
+    constexpr bool PAIR = LD == LD_PAIR;
+    auto issue = [&](uint32_t t) {           // PAIR: t is even, blocks t and t+1
         // opaque copies: keep the shuffles here instead of hoisted out of the loop
         uint32_t tl = (uint32_t)tp, th = (uint32_t)(tp >> 32), pl = plim;
         asm volatile("" : "+v"(tl), "+v"(th), "+v"(pl));
+        if constexpr (PAIR) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int q = 16 * i + (lane >> 2);
-            const uint32_t pc = ((uint32_t)lane & 3u) ^ (((uint32_t)q >> 2) & 3u);   // piece this lane moves
-            const uint32_t ps = t * 64u + pc * 16u;
-            const uint32_t l = (uint32_t)__shfl((int)pl, q);
-            const uint64_t src = ((uint64_t)(uint32_t)__shfl((int)th, q) << 32) | (uint32_t)__shfl((int)tl, q);
-            if (ps < l) dma16<NT>(data + src + ps, stage + (uint32_t)i * 1024u);
+            for (int i = 0; i < 8; ++i) {
+                const int q = 8 * i + (lane >> 3);
+                const uint32_t pos = (uint32_t)lane & 7u;                     // 16-byte position in the run
+                const uint32_t pc = (pos & 4u) | ((pos & 3u) ^ (((uint32_t)q >> 1) & 3u));   // piece moved
+                const uint32_t ps = t * 64u + pc * 16u;
+                const uint32_t l = (uint32_t)__shfl((int)pl, q);
+                const uint64_t src = ((uint64_t)(uint32_t)__shfl((int)th, q) << 32) | (uint32_t)__shfl((int)tl, q);
+                if (ps < l) dma16<NT>(data + src + ps, stage + (uint32_t)i * 1024u);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int q = 16 * i + (lane >> 2);
+                const uint32_t pc = ((uint32_t)lane & 3u) ^ (((uint32_t)q >> 2) & 3u);   // piece this lane moves
+                const uint32_t ps = t * 64u + pc * 16u;
+                const uint32_t l = (uint32_t)__shfl((int)pl, q);
+                const uint64_t src = ((uint64_t)(uint32_t)__shfl((int)th, q) << 32) | (uint32_t)__shfl((int)tl, q);
+                if (ps < l) dma16<NT>(data + src + ps, stage + (uint32_t)i * 1024u);
+            }
         }
     };
-    const uint32_t rot = ((uint32_t)lane >> 2) & 3u;
-    uint8_t *mine = (uint8_t *)stage_ptr + lane * 64;
+    const uint32_t rot = PAIR ? (((uint32_t)lane >> 1) & 3u) : (((uint32_t)lane >> 2) & 3u);
+    uint8_t *const mine0 = (uint8_t *)stage_ptr + lane * (PAIR ? 128 : 64);
     if (ABLATE != 2 && tmax) issue(0);
 #pragma unroll
     for (uint32_t jj = 0; jj < B3_LANE_LEAVES; ++jj) {
@@ -344,7 +375,8 @@ __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ dat
     #pragma unroll
                     for (int q = 0; q < 16; ++q) m[q] = (uint32_t)lane * 0x9E3779B9u + q + off;
                 } else {
-                    wait_vmcnt<0>();                                    // block t has landed
+                    uint8_t *const mine = mine0 + (PAIR ? (t & 1u) * 64u : 0u);
+                    if (!PAIR || (t & 1u) == 0u) wait_vmcnt<0>();     // block t has landed
                     // bytes of my block that are past the chunk or were not DMA'd
                     const uint32_t dma_end = plim > off ? min(64u, (plim - off + 15u) & ~15u) : 0u;
                     const uint32_t fix = min(vb, dma_end);
@@ -363,7 +395,11 @@ __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ dat
                         m[4 * i] = v.x; m[4 * i + 1] = v.y; m[4 * i + 2] = v.z; m[4 * i + 3] = v.w;
                     }
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // slot free for block t+1
-                    if (t + 1 < tmax) issue(t + 1);
+                    if (PAIR) {
+                        if ((t & 1u) && t + 1 < tmax) issue(t + 1);
+                    } else if (t + 1 < tmax) {
+                        issue(t + 1);
+                    }
                 }
                 if (b < lb) {
                     uint32_t fl = (b == 0 ? B3_START : 0u) | (b + 1 == lb ? B3_END : 0u);
@@ -399,14 +435,15 @@ __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ dat
 // the packed classes 6..0.  Per lane: a chunk slot, its task k (leaves
 // LPL*k .. LPL*k+LPL-1) and the merge geometry of that chunk within the wave.
 // ---------------------------------------------------------------------------
-template <bool NT, int ABLATE, bool COOP>
+template <bool NT, int ABLATE, int LD>
 __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, const Tables &T,
                                              const HashTables &H) {
     constexpr uint32_t LPL = B3_LANE_LEAVES;
     const int lane = threadIdx.x & 63;
-    // COOP: per-wave staging slot for the cooperative block loader (4 KiB)
-    __shared__ __attribute__((aligned(16))) uint32_t stage_mem[COOP ? 4 * 1024 : 1];
-    uint32_t *stage_ptr = stage_mem + (COOP ? (threadIdx.x >> 6) * 1024 : 0);
+    constexpr bool COOP = LD != LD_PLAIN;
+    constexpr uint32_t SLOT = LD == LD_PAIR ? 2048 : 1024;       // words: per-wave staging slot (8 / 4 KiB)
+    __shared__ __attribute__((aligned(16))) uint32_t stage_mem[COOP ? 4 * SLOT : 1];
+    uint32_t *stage_ptr = stage_mem + (COOP ? (threadIdx.x >> 6) * SLOT : 0);
     const uint32_t stage = (uint32_t)__builtin_amdgcn_readfirstlane(lds_addr(stage_ptr));
     const uint64_t nbig = min(H.ctr[B3C_ITEMS], H.items_cap);
     uint64_t npk[B3_CLASSES], total = nbig;
@@ -491,7 +528,7 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
         const bool task_root = root && mm == 1;                  // the task is the whole chunk
         uint32_t x[8];
         if constexpr (COOP) {
-            leaf_blocks_coop<NT, ABLATE>(data, T.span, stage, stage_ptr, lane, act, cstart + lane_off, nbytes,
+            leaf_blocks_coop<NT, ABLATE, LD>(data, T.span, stage, stage_ptr, lane, act, cstart + lane_off, nbytes,
                                          nblk, nl, nleaves, j0, task_root, x);
         } else {
             uint32_t lc[LPL][8];                                 // leaf CVs
@@ -606,12 +643,12 @@ __global__ __launch_bounds__(256) void b3_tree_kernel(Tables T, HashTables H) {
     }
 }
 
-template <bool NT, int ABLATE, bool COOP>
+template <bool NT, int ABLATE, int LD>
 __global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict__ data, Tables T, HashTables H) {
-    b3_leaf_body<NT, ABLATE, COOP>(data, T, H);
+    b3_leaf_body<NT, ABLATE, LD>(data, T, H);
 }
 
-template <bool NT, int AB, bool CO>
+template <bool NT, int AB, int CO>
 static void launch_leaf(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
@@ -626,7 +663,7 @@ static void launch_leaf(int device, const uint8_t *d, const Tables &t, const Has
 #ifdef SYNCR_CDC_DEV
 // development library only: per-lane loads, non-temporal loads and the
 // timing-only ablations (loads only / no loads), selected by SYNCR_B3_* variables
-template <bool CO>
+template <int CO>
 static hipError_t launch_leaf_v(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
     switch (ht.ablate * 2 + (ht.nt ? 1 : 0)) {
         case 0: launch_leaf<false, 0, CO>(device, d, t, ht, s); break;
@@ -646,10 +683,14 @@ hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const Hash
     if (!t.nfiles) return hipSuccess;
     hipLaunchKernelGGL(b3_items_kernel, dim3((t.nfiles + 255) / 256), dim3(256), 0, s, t, ht);
 #ifdef SYNCR_CDC_DEV
-    e = ht.coop ? launch_leaf_v<true>(device, d, t, ht, s) : launch_leaf_v<false>(device, d, t, ht, s);
+    e = ht.coop == 2   ? launch_leaf_v<LD_PAIR>(device, d, t, ht, s)
+        : ht.coop == 1 ? launch_leaf_v<LD_COOP64>(device, d, t, ht, s)
+                       : launch_leaf_v<LD_PLAIN>(device, d, t, ht, s);
     if (e != hipSuccess) return e;
 #else
-    launch_leaf<false, 0, true>(device, d, t, ht, s);    // the one exact product instance
+    // the one exact product instance: two blocks per loader round (zipf10k, same
+    // process: leaf HBM reads 1.34x -> 1.255x of the input, time within 0.5 %)
+    launch_leaf<false, 0, LD_PAIR>(device, d, t, ht, s);
 #endif
     const uint64_t want = (ht.trees_cap + 3) / 4;
     const uint32_t blocks = (uint32_t)(want < 4096 ? (want ? want : 1) : 4096);

@@ -76,7 +76,7 @@ struct syncr_cdc {
         dense_list, dense_cnt, dense_bits, super_off, cand, cuts, counts;
     // BLAKE3 of every chunk (launch_hashed)
     bool hash_on = false;
-    uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 1;
+    uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 2;     // dev A/B knobs; coop 2 = the product's LD_PAIR
     uint64_t items_cap = 0, trees_cap = 0;
     DevBuf hctr, items, trees, gcv, hashes, packed;
     // read-boundary grid (Tables::gpos...): production semantics only
@@ -399,7 +399,8 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_CDC_SERIAL")) h->serial_scans = atoi(a) != 0;
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
     if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
-    if (const char *ld = getenv("SYNCR_B3_LOAD")) h->b3_coop = strcmp(ld, "plain") != 0;   // A/B only
+    if (const char *ld = getenv("SYNCR_B3_LOAD"))                                         // A/B only
+        h->b3_coop = strcmp(ld, "plain") == 0 ? 0u : (strcmp(ld, "coop") == 0 ? 1u : 2u);
     if (const char *k = getenv("SYNCR_CDC_SCAN")) {
         if (strcmp(k, "valu") == 0) h->geom = ScanGeom{SCAN_VALU, DEFAULT_RUN, 0};
         if (strcmp(k, "mfma") == 0) h->geom = ScanGeom{SCAN_MFMA, DEFAULT_NB, MFV_SINGLE | MFV_NOPIPE};

@@ -9,13 +9,13 @@ Writes
   profiles/<tag>_pmc_traffic.json     HBM bytes per launch: scan (main) and every other kernel
   profiles/<tag>_pmc_sq.json          per scan dispatch: shader clock and SQ instruction counters
 
-HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB
-and collected in separate passes; on gfx950 FETCH_SIZE reports exactly half of
-the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled.
-That correction is calibrated for the scan's access pattern (1 KiB contiguous
-per wave instruction; the read probe lands at 1.000x); other patterns (the
-BLAKE3 leaf's 64-byte runs) are uncalibrated, so their doubled figure is an
-upper bound (see `correction` in the JSON).
+Read bytes come from the L2->EA request-size counters (pass 2, prof.sh r02+):
+64*TCC_EA0_RDREQ_64B + 128*TCC_EA0_RDREQ_128B + 32*TCC_EA0_RDREQ_32B.  gfx950's
+FETCH_SIZE formula weights 128-byte requests by TCC_BUBBLE, which reads 0 on
+gfx950, so FETCH_SIZE counts every 128-byte request as 64 B (exactly half on
+streaming reads); profiles/r02_fetch_calibration.json measures both on known
+byte counts (tools/ubench_fetch.hip).  Older runs (FETCH_SIZE pass) are doubled,
+which is exact only when every request is 128 B.  Write bytes: WRITE_SIZE, own pass.
 """
 import csv
 import json
@@ -83,27 +83,41 @@ def main(tag, src=None):
     w = counters(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
     fb = bench_line(os.path.join(src, "bench_fetch.log")) or {}
     span = fb.get("config", {}).get("bytes_per_gpu")
+    mean = lambda v: sum(v) / len(v) if v else 0.0   # noqa: E731
+    sized = any(c == "TCC_EA0_RDREQ_128B" for _, c in f)
+
+    def read_bytes(kname):
+        if sized:
+            v = {c: mean(f.get((kname, c), [])) for c in ("TCC_EA0_RDREQ_32B", "TCC_EA0_RDREQ_64B",
+                                                          "TCC_EA0_RDREQ_128B")}
+            if not f.get((kname, "TCC_EA0_RDREQ_128B")):
+                return None
+            return 32 * v["TCC_EA0_RDREQ_32B"] + 64 * v["TCC_EA0_RDREQ_64B"] + 128 * v["TCC_EA0_RDREQ_128B"]
+        fv = f.get((kname, "FETCH_SIZE"), [])
+        return 2 * 1024 * mean(fv) if fv else None
 
     def hbm(kname):
-        fv, wv = f.get((kname, "FETCH_SIZE"), []), w.get((kname, "WRITE_SIZE"), [])
-        if not fv:
-            return None
-        return 2 * 1024 * sum(fv) / len(fv) + (1024 * sum(wv) / len(wv) if wv else 0.0)
+        r = read_bytes(kname)
+        return None if r is None else r + 1024 * mean(w.get((kname, "WRITE_SIZE"), []))
 
     k = "cdc::cdc_scan_kernel"
-    fetch_kib = sum(f[(k, "FETCH_SIZE")]) / len(f[(k, "FETCH_SIZE")])
-    write_kib = sum(w[(k, "WRITE_SIZE")]) / len(w[(k, "WRITE_SIZE")])
-    scan_hbm = 2 * fetch_kib * 1024 + write_kib * 1024
+    read_b = read_bytes(k)
+    write_kib = mean(w[(k, "WRITE_SIZE")])
+    scan_hbm = hbm(k)
     kernels = sorted({kk[0] for kk in f})
     out = {
         "kernel": k, "workload": fb.get("config", {}).get("workload", "").split(":")[0],
         "run_bytes": fb.get("config", {}).get("engine", {}).get("run_bytes"),
-        "span": span, "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
+        "span": span, "read_bytes": int(read_b), "write_size_kib": write_kib,
         "hbm_bytes_per_launch": int(scan_hbm), "algorithmic_bytes_per_launch": span,
         "traffic_over_algorithmic": (scan_hbm / span) if span else None,
-        "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halves wide streaming reads; "
-                      "calibrated for 1 KiB-contiguous wave loads, an upper bound for the BLAKE3 leaf's 64-byte runs)",
-        "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/prof.sh {tag}",
+        "correction": ("bytes = 32*TCC_EA0_RDREQ_32B + 64*TCC_EA0_RDREQ_64B + 128*TCC_EA0_RDREQ_128B + WRITE_SIZE*1024 "
+                       "(gfx950 FETCH_SIZE counts 128-byte requests as 64 B: profiles/r02_fetch_calibration.json)"
+                       if sized else "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (exact when every request is 128 B)"),
+        "scope": "L2 -> EA (fabric) requests: Infinity Cache hits are included, so this bounds HBM bytes from above",
+        "source": (f"rocprofv3 --pmc TCC_EA0_RDREQ_{{32B,64B,128B}} TCC_EA0_RDREQ / --pmc WRITE_SIZE (separate passes), "
+                   f"tools/prof.sh {tag}" if sized else
+                   f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/prof.sh {tag}"),
         "per_kernel_hbm_bytes": {kn: int(hbm(kn)) for kn in kernels if hbm(kn) is not None},
         "per_kernel_traffic_over_span": {kn: round(hbm(kn) / span, 4) for kn in kernels
                                          if hbm(kn) is not None and span},
