@@ -365,6 +365,9 @@ def main(argv=None):
     ap.add_argument("--sustained-steps", type=int, default=80,
                     help="untimed steps before the `sustained` re-timing of K steps (0 = skip)")
     ap.add_argument("--dry-run", action="store_true", help="shard plan only, no device")
+    ap.add_argument("--fetch-at", default="first", choices=["first", "end"],
+                    help="where inside the W warm-up steps the results are fetched once (capacity re-runs settle "
+                         "there): after the first step (default) or after the last, right before the timed region")
     ap.add_argument("--dev-lib", action="store_true",
                     help="tools/ only: run against libsyncr_cdc_dev.so (variants / ablations by env)")
     args = ap.parse_args(argv)
@@ -418,8 +421,18 @@ def main(argv=None):
         for h, _ in slots[:nslots]:
             h.synchronize()
 
-    run_steps(1, args.warmup)
-    ch.fetch(hashed=head_hashed)              # settles any capacity re-run before timing
+    # W warm-up steps in all; results are fetched once inside them so a
+    # capacity re-run settles before timing.  Fetching after the FIRST warm-up
+    # step keeps the host-side gap (D2H + host work) away from the timed
+    # region: on MI355X the shader clock dips for ~20 launches whenever the
+    # scan load resumes after a gap (profiles/r02_v2_dispatches.json)
+    if args.fetch_at == "first" and args.warmup > 0:
+        run_steps(1, 1)
+        ch.fetch(hashed=head_hashed)
+        run_steps(1, args.warmup - 1)
+    else:
+        run_steps(1, args.warmup)
+        ch.fetch(hashed=head_hashed)
     d.barrier()
     ch.synchronize()
     ch.set_timing(True, scan_only=True)       # HIP events around the scan kernel, on its stream
@@ -583,6 +596,8 @@ def main(argv=None):
                 "max_chunk": syncr_amd.MAX_CHUNK_SIZE, "read_cap": read_cap, "mode": args.mode,
                 "parallelism": f"file-sharded x{world} (LPT), one process + HIP stream per GPU, no collective",
                 "launcher": os.environ.get("SYNCR_BENCH_LAUNCHER", "torchrun/env" if world > 1 else "none"),
+                "warmup_fetch": f"results fetched after warm-up step {1 if args.fetch_at == 'first' else args.warmup} "
+                                f"of {args.warmup}",
                 "slots_agree_rank0": slots_agree,
                 "cuts_rank0": ncuts, "coverage_ok_rank0": covered,
                 "candidates_rank0": int(stats["candidates"]), "dense_tiles_rank0": int(stats["dense_tiles"]),

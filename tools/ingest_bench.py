@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--file-gib", type=float, default=2.0)
     ap.add_argument("--check-files", type=int, default=200)
+    ap.add_argument("--devices", default=None,
+                    help="comma-separated device list for syncr_ingest_open_multi (e.g. 0,0 on a one-GPU box); "
+                         "default: one device, syncr_ingest_open")
     ap.add_argument("--no-fill", action="store_true",
                     help="diagnostic: reserve/commit without writing the bytes (pipeline ceiling without the "
                          "host copy; results are not checked)")
@@ -63,10 +66,11 @@ def main():
         if tag in check_ids:
             keep[tag] = a
 
+    devices = [int(x) for x in args.devices.split(",")] if args.devices else None
     out = {"workload": "zipf10k", "bytes": span, "files": len(files), "batch_mib": args.batch_mib,
-           "depth": args.depth, "copy_threads": args.copy_threads}
+           "depth": args.depth, "copy_threads": args.copy_threads, "devices": devices}
     with syncr_amd.Ingest(batch_bytes=args.batch_mib << 20, depth=args.depth,
-                          copy_threads=args.copy_threads, on_file=on_file) as g:
+                          copy_threads=args.copy_threads, on_file=on_file, devices=devices) as g:
         best = None
         for _ in range(args.reps):
             counts["files"] = counts["chunks"] = 0
@@ -87,6 +91,8 @@ def main():
             return
         st = g.stats()
         out["batches_per_pass"] = st["batches"] // args.reps
+        if devices:
+            out["device_stats"] = g.device_stats()
 
         # correctness sample vs the oracle (boundaries + BLAKE3)
         from oracle import oracle as O
