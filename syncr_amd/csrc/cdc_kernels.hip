@@ -1043,6 +1043,16 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
         // nx: window index of the first candidate >= this lane's + 64, where the
         // search resumes after a cut at it with no head hit (64 = past the window)
         const Off key = wr == OMAX ? OMAX : (Off)(wr + 64);
+        if constexpr (sizeof(Off) == 4) {
+            // dense windows (periodic data: a candidate every 64 bytes): every
+            // lane's answer is the next lane, found with one shuffle instead of
+            // six dependent ones.  (nx of a lane past the file is never read.)
+            const Off up = (Off)__shfl_down((int)wr, 1);
+            if (__ballot(lane == 63 || up >= key) == ~0ull) {
+                nx = (uint32_t)lane + 1u;
+                return;
+            }
+        }
         uint32_t idx = 0;
 #pragma unroll
         for (uint32_t st = 32; st >= 1; st >>= 1) {
@@ -1128,7 +1138,8 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                 const uint32_t last = (uint32_t)j + run;            // reached; its own f is not last + 1
                 const uint32_t flast = last < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)f, (int)last) : 64u;
                 unsigned long long pm;
-                if (flast >= 64u) {
+                const bool chain_contig = flast >= 64u;             // pm = lanes j+1 .. last
+                if (chain_contig) {
                     const unsigned long long upto = last >= 63u ? ~0ull : ((2ull << last) - 1ull);   // lanes <= last
                     const unsigned long long thru = j >= 63 ? ~0ull : ((2ull << j) - 1ull);          // lanes <= j
                     pm = upto & ~thru;
@@ -1159,24 +1170,47 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     const int64_t capv = (int64_t)CAP, maxv = (int64_t)MAX;
                     const int64_t m = on ? (int64_t)__builtin_popcountll(pm & lt) + 1 : 0;
                     int64_t a = on ? (int64_t)wr + 1 + maxv - m * capv : INT64_MAX;
-#pragma unroll
-                    for (int off = 1; off < 64; off <<= 1) {        // inclusive prefix minimum
-                        const int64_t u = (int64_t)shfl_up64((uint64_t)a, off);
-                        if (lane >= off && u < a) a = u;
-                    }
                     const int64_t R0 = (int64_t)R, Fv = (int64_t)Fo;
-                    const int64_t B = a < R0 ? a : R0;
-                    int64_t Rm = m * capv + B;
-                    if (Rm > Fv) Rm = Fv;
                     const unsigned long long below = pm & lt;
-                    const int pl = below ? 63 - __builtin_clzll(below) : 0;
-                    // shuffles with every lane active: under a per-lane condition the
-                    // source lane (the chain's first lane has no predecessor) would be
-                    // inactive and read back as 0
-                    const int64_t Rsh = (int64_t)shfl64((uint64_t)Rm, pl);
-                    const int64_t wsh = (int64_t)(Off)__shfl((int)wr, pl);
-                    const int64_t Rprev = below ? Rsh : R0;
-                    const int64_t wprev = below ? wsh : (int64_t)s - 1;
+                    int64_t Rm, Rprev, wprev;
+                    // consecutive chain lanes whose candidates are less than CAP apart
+                    // (periodic data): a_m falls with m, so the prefix minimum is a_m
+                    // itself and R_{m-1} follows from the previous lane's candidate --
+                    // one shuffle instead of the 6-step scan and two more shuffles
+                    const Off wup = (Off)__shfl_up((int)wr, 1);
+                    const bool mono = chain_contig &&
+                                      __ballot(on && below && (int64_t)wr - (int64_t)wup >= capv) == 0ull;
+                    if (mono) {
+                        const int64_t B = a < R0 ? a : R0;
+                        Rm = m * capv + B;
+                        if (Rm > Fv) Rm = Fv;
+                        if (below) {
+                            const int64_t ap = (int64_t)wup + 1 + maxv - (m - 1) * capv;
+                            Rprev = (m - 1) * capv + (ap < R0 ? ap : R0);
+                            if (Rprev > Fv) Rprev = Fv;
+                            wprev = (int64_t)wup;
+                        } else {
+                            Rprev = R0;
+                            wprev = (int64_t)s - 1;
+                        }
+                    } else {
+#pragma unroll
+                        for (int off = 1; off < 64; off <<= 1) {    // inclusive prefix minimum
+                            const int64_t u = (int64_t)shfl_up64((uint64_t)a, off);
+                            if (lane >= off && u < a) a = u;
+                        }
+                        const int64_t B = a < R0 ? a : R0;
+                        Rm = m * capv + B;
+                        if (Rm > Fv) Rm = Fv;
+                        const int pl = below ? 63 - __builtin_clzll(below) : 0;
+                        // shuffles with every lane active: under a per-lane condition the
+                        // source lane (the chain's first lane has no predecessor) would be
+                        // inactive and read back as 0
+                        const int64_t Rsh = (int64_t)shfl64((uint64_t)Rm, pl);
+                        const int64_t wsh = (int64_t)(Off)__shfl((int)wr, pl);
+                        Rprev = below ? Rsh : R0;
+                        wprev = below ? wsh : (int64_t)s - 1;
+                    }
                     const bool ok = on && (int64_t)wr < Rprev && (int64_t)wr >= wprev + 64;
                     const unsigned long long bad = __ballot(on && !ok);
                     mk = bad ? pm & ((1ull << __builtin_ctzll(bad)) - 1ull) : pm;
