@@ -365,6 +365,9 @@ def main(argv=None):
     ap.add_argument("--sustained-steps", type=int, default=80,
                     help="untimed steps before the `sustained` re-timing of K steps (0 = skip)")
     ap.add_argument("--dry-run", action="store_true", help="shard plan only, no device")
+    ap.add_argument("--device-map", default=None,
+                    help="rehearsal only: comma-separated device per local rank (e.g. 0,0 runs two ranks on one "
+                         "GPU); default: device = LOCAL_RANK")
     ap.add_argument("--fetch-at", default="first", choices=["first", "end"],
                     help="where inside the W warm-up steps the results are fetched once (capacity re-runs settle "
                          "there): after the first step (default) or after the last, right before the timed region")
@@ -388,7 +391,13 @@ def main(argv=None):
     if args.dev_lib:
         syncr_amd.use_dev_library()
     read_cap = syncr_amd.TOKIO_READ_CAP if args.mode == "production" else 0
-    ch = syncr_amd.Chunker(syncr_amd.CHUNK_BITS, syncr_amd.MAX_CHUNK_SIZE, read_cap, device=d.local_rank)
+    dev_id = d.local_rank
+    if args.device_map:
+        dmap = [int(x) for x in args.device_map.split(",")]
+        if len(dmap) < world:
+            raise SystemExit(f"--device-map names {len(dmap)} devices for {world} ranks")
+        dev_id = dmap[d.local_rank]
+    ch = syncr_amd.Chunker(syncr_amd.CHUNK_BITS, syncr_amd.MAX_CHUNK_SIZE, read_cap, device=dev_id)
 
     sizes, indices, desc = workload(args.workload, world)
     mine = lpt_shard(sizes, world)[d.rank]
@@ -402,7 +411,7 @@ def main(argv=None):
     slots = []                                # (handle, corpus copy): one batch in flight each
     for k in range(depth):
         h = ch if k == 0 else syncr_amd.Chunker(syncr_amd.CHUNK_BITS, syncr_amd.MAX_CHUNK_SIZE, read_cap,
-                                                 device=d.local_rank)
+                                                 device=dev_id)
         b = syncr_amd.DeviceBuffer(h, span)   # own buffer: no slot reads another's bytes from cache
         b.gen_corpus(offs, lens, indices=idx)
         if args.workload == "dense":
@@ -596,6 +605,7 @@ def main(argv=None):
                 "max_chunk": syncr_amd.MAX_CHUNK_SIZE, "read_cap": read_cap, "mode": args.mode,
                 "parallelism": f"file-sharded x{world} (LPT), one process + HIP stream per GPU, no collective",
                 "launcher": os.environ.get("SYNCR_BENCH_LAUNCHER", "torchrun/env" if world > 1 else "none"),
+                "device_map": args.device_map or "device = LOCAL_RANK",
                 "warmup_fetch": f"results fetched after warm-up step {1 if args.fetch_at == 'first' else args.warmup} "
                                 f"of {args.warmup}",
                 "slots_agree_rank0": slots_agree,
