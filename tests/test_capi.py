@@ -122,3 +122,18 @@ def test_product_never_touches_oracle():
             if fn.endswith((".py", ".cpp", ".hip", ".h")):
                 src = open(os.path.join(dirpath, fn)).read()
                 assert "oracle" not in src.replace("oracle/", ""), fn
+
+
+def test_integration_rust_block_covers_the_header():
+    """INTEGRATION.md's extern "C" appendix is generated from the header
+    (tools/gen_rust_ffi.py) and names every declared entry point."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_rust_ffi.py"), "--check"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    header = open(os.path.join(root, "include", "syncr_cdc.h")).read()
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    declared = set(re.findall(r"\b(syncr_\w+)\s*\(", header))
+    missing = [s for s in sorted(declared) if f"pub fn {s}(" not in doc]
+    assert not missing, missing
