@@ -431,11 +431,127 @@ __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ dat
 }
 
 // ---------------------------------------------------------------------------
+// Cross-lane merges by quads (MQ).  The shuffle merge (one `parent` per level
+// with the whole wave issuing a full compression for 64 / 2d active lanes)
+// spends 6 x 688 VALU instructions on the 63 parents of a group item.  Here a
+// parent is computed by four lanes, one per column of the state: the column
+// G, three quad rotations (DPP quad_perm), the diagonal G, three rotations
+// back -- 30 instructions per round instead of 96 -- so the 16 parents of a
+// level take one pass of the wave (level 1: two).  Node CVs live in the
+// wave's LDS slot, compacted per level: node n of a level at byte 36 n (the
+// 4-byte pad spreads the quads over the banks), so the two children of parent
+// p are the 72 bytes at 72 p and parent p becomes node p of the next level.
+// A lane's message words are read from LDS at per-lane addresses fixed for
+// the whole merge (quad p = lane >> 2 always reads message p; lane i of the
+// quad needs words SCHED[r][2i, 2i+1, 8+2i, 9+2i] of round r).  All LDS reads
+// of a pass precede its writes in program order, and a wave's LDS accesses
+// complete in order, so the in-place compaction needs no barrier.
+// ---------------------------------------------------------------------------
+constexpr uint32_t mq_off(int r, int s, int i) {          // byte offset of the word in its 72-byte message
+    const int k = s < 2 ? 2 * i + s : 8 + 2 * i + (s - 2);
+    const uint32_t w = SCHED.s[r][k];
+    return w < 8 ? 4 * w : 4 * w + 4;
+}
+constexpr uint32_t mq_pack(int r, int s) {                // the four lanes' offsets, one byte each
+    return mq_off(r, s, 0) | (mq_off(r, s, 1) << 8) | (mq_off(r, s, 2) << 16) | (mq_off(r, s, 3) << 24);
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+constexpr int QP_NEXT1 = 0x39, QP_NEXT2 = 0x4E, QP_NEXT3 = 0x93;   // lane i <- lane (i+1|2|3) & 3
+
+#define MQ_G(a, b, c, d, mx, my)      \
+    do {                              \
+        a = a + b + (mx);             \
+        d = rotr(d ^ a, 16);          \
+        c = c + d;                    \
+        b = rotr(b ^ c, 12);          \
+        a = a + b + (my);             \
+        d = rotr(d ^ a, 8);           \
+        c = c + d;                    \
+        b = rotr(b ^ c, 7);           \
+    } while (0)
+
+// Merge the lanes' CVs x of each unit (aligned runs of dmax lanes, dmax > 1,
+// wave-uniform; node km of a unit is at lane U + km) into the unit's CV, left
+// in x of every lane of the unit.  km, mm, act, root as in b3_leaf_body.
+__device__ __forceinline__ void merge_quads(uint32_t *slot_ptr, int lane, uint32_t dmax, bool act, uint32_t km,
+                                            uint32_t mm, bool root, uint32_t x[8]) {
+    uint8_t *const lds = (uint8_t *)slot_ptr;
+    // opaque copies: the per-lane tables below are loop-invariant, and hoisted
+    // out of the wave-item loop they would stay live through the block loop
+    // (153 VGPRs, 3 waves/SIMD)
+    uint32_t i = (uint32_t)lane & 3u, q = (uint32_t)lane >> 2;
+    asm volatile("" : "+v"(i), "+v"(q));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *(uint32_t *)(lds + lane * 36 + 4 * k) = x[k];     // level-1 nodes
+    uint32_t ad[7][4];                                    // this lane's message word addresses (pass 0)
+#pragma unroll
+    for (int r = 0; r < 7; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ad[r][s] = q * 72u + __builtin_amdgcn_ubfe(mq_pack(r, s), 8u * i, 8u);
+    const uint32_t ivA = i == 0 ? IV0 : (i == 1 ? IV1 : (i == 2 ? IV2 : IV3));
+    const uint32_t ivB = i == 0 ? IV4 : (i == 1 ? IV5 : (i == 2 ? IV6 : IV7));
+    const uint32_t dfix = i == 2 ? 64u : 0u;              // v[12..14] = counter 0, 0, block length 64
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        if (d >= dmax) break;                             // uniform
+        // parent p of this level merges the nodes at lanes 2pd and (2p+1)d; the
+        // left child's lane knows whether it merges (1), is promoted (2) or is
+        // not a node; bit 3: ROOT
+        const uint32_t code = !act ? 0u : (km + d < mm ? (1u | ((root && mm <= 2 * d) ? B3_ROOT : 0u)) : 2u);
+#pragma unroll
+        for (uint32_t pass = 0; pass < 2; ++pass) {
+            if (pass == 1 && d != 1) break;               // 32 parents only at level 1
+            const uint32_t p = q + 16u * pass;
+            const uint32_t L = 2u * p * d;
+            const uint32_t c = (uint32_t)__shfl((int)code, (int)(L & 63u));
+            const uint32_t my = L < 64u ? c : 0u;
+            if (__ballot(my != 0u) == 0ull) continue;
+            const uint32_t pb = pass * 1152u;             // messages 16..31
+            // promoted node: words i, 4+i of the left child (read before any write)
+            const uint32_t c0 = *(const uint32_t *)(lds + pb + q * 72u + 4u * i);
+            const uint32_t c1 = *(const uint32_t *)(lds + pb + q * 72u + 16u + 4u * i);
+            uint32_t a = ivA, b = ivB, cc = ivA, dd = i == 3 ? (B3_PARENT | (my & B3_ROOT)) : dfix;
+#pragma unroll
+            for (int r = 0; r < 7; ++r) {
+                const uint32_t m0 = *(const uint32_t *)(lds + pb + ad[r][0]);
+                const uint32_t m1 = *(const uint32_t *)(lds + pb + ad[r][1]);
+                const uint32_t m2 = *(const uint32_t *)(lds + pb + ad[r][2]);
+                const uint32_t m3 = *(const uint32_t *)(lds + pb + ad[r][3]);
+                MQ_G(a, b, cc, dd, m0, m1);                                   // column i
+                b = quad_perm<QP_NEXT1>(b);
+                cc = quad_perm<QP_NEXT2>(cc);
+                dd = quad_perm<QP_NEXT3>(dd);
+                MQ_G(a, b, cc, dd, m2, m3);                                   // diagonal i
+                b = quad_perm<QP_NEXT3>(b);
+                cc = quad_perm<QP_NEXT2>(cc);
+                dd = quad_perm<QP_NEXT1>(dd);
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (my) {
+                const bool merge = (my & 1u) != 0u;
+                *(uint32_t *)(lds + p * 36u + 4u * i) = merge ? (a ^ cc) : c0;
+                *(uint32_t *)(lds + p * 36u + 16u + 4u * i) = merge ? (b ^ dd) : c1;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    // the unit's CV: node U / dmax of the last level
+    const uint32_t node = (uint32_t)lane >> __builtin_ctz(dmax);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = *(const uint32_t *)(lds + node * 36u + 4 * k);
+}
+#undef MQ_G
+
+// ---------------------------------------------------------------------------
 // Persistent waves pull wave items: the group items of big chunks first, then
 // the packed classes 6..0.  Per lane: a chunk slot, its task k (leaves
 // LPL*k .. LPL*k+LPL-1) and the merge geometry of that chunk within the wave.
 // ---------------------------------------------------------------------------
-template <bool NT, int ABLATE, int LD>
+template <bool NT, int ABLATE, int LD, bool MQ>
 __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, const Tables &T,
                                              const HashTables &H) {
     constexpr uint32_t LPL = B3_LANE_LEAVES;
@@ -587,6 +703,9 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
             for (int q = 0; q < 8; ++q) x[q] = lc[0][q];
         }
         // merge the tasks of each chunk (runs of 2^c lanes, or the 64 lanes of a group)
+        if constexpr (MQ && COOP) {
+            if (dmax > 1) merge_quads(stage_ptr, lane, dmax, act, km, mm, root, x);
+        } else {
 #pragma unroll
         for (uint32_t d = 1; d < 64; d <<= 1) {
             if (d < dmax) {                                      // uniform
@@ -596,6 +715,7 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
                 if (act && (km & (2 * d - 1)) == 0 && km + d < mm)
                     parent(x, r, (root && mm <= 2 * d) ? B3_ROOT : 0u);
             }
+        }
         }
         if (act && km == 0) {
             uint32_t *dst = root ? H.hashes + slot * 8 : H.gcv + out_item * 8;
@@ -643,34 +763,34 @@ __global__ __launch_bounds__(256) void b3_tree_kernel(Tables T, HashTables H) {
     }
 }
 
-template <bool NT, int ABLATE, int LD>
+template <bool NT, int ABLATE, int LD, bool MQ>
 __global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict__ data, Tables T, HashTables H) {
-    b3_leaf_body<NT, ABLATE, LD>(data, T, H);
+    b3_leaf_body<NT, ABLATE, LD, MQ>(data, T, H);
 }
 
-template <bool NT, int AB, int CO>
+template <bool NT, int AB, int CO, bool MQ = false>
 static void launch_leaf(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
         cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)&b3_leaf_kernel<NT, AB, CO>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)&b3_leaf_kernel<NT, AB, CO, MQ>, 256, 0) !=
             hipSuccess ||
         per <= 0)
         per = 1;
-    hipLaunchKernelGGL((b3_leaf_kernel<NT, AB, CO>), dim3((uint32_t)(cus * per)), dim3(256), 0, s, d, t, ht);
+    hipLaunchKernelGGL((b3_leaf_kernel<NT, AB, CO, MQ>), dim3((uint32_t)(cus * per)), dim3(256), 0, s, d, t, ht);
 }
 
 #ifdef SYNCR_CDC_DEV
 // development library only: per-lane loads, non-temporal loads and the
 // timing-only ablations (loads only / no loads), selected by SYNCR_B3_* variables
-template <int CO>
+template <int CO, bool MQ = false>
 static hipError_t launch_leaf_v(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
     switch (ht.ablate * 2 + (ht.nt ? 1 : 0)) {
-        case 0: launch_leaf<false, 0, CO>(device, d, t, ht, s); break;
-        case 1: launch_leaf<true, 0, CO>(device, d, t, ht, s); break;
-        case 2: launch_leaf<false, 1, CO>(device, d, t, ht, s); break;
-        case 3: launch_leaf<true, 1, CO>(device, d, t, ht, s); break;
-        case 4: case 5: launch_leaf<true, 2, CO>(device, d, t, ht, s); break;
+        case 0: launch_leaf<false, 0, CO, MQ>(device, d, t, ht, s); break;
+        case 1: launch_leaf<true, 0, CO, MQ>(device, d, t, ht, s); break;
+        case 2: launch_leaf<false, 1, CO, MQ>(device, d, t, ht, s); break;
+        case 3: launch_leaf<true, 1, CO, MQ>(device, d, t, ht, s); break;
+        case 4: case 5: launch_leaf<true, 2, CO, MQ>(device, d, t, ht, s); break;
         default: return hipErrorInvalidValue;
     }
     return hipSuccess;
@@ -683,7 +803,8 @@ hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const Hash
     if (!t.nfiles) return hipSuccess;
     hipLaunchKernelGGL(b3_items_kernel, dim3((t.nfiles + 255) / 256), dim3(256), 0, s, t, ht);
 #ifdef SYNCR_CDC_DEV
-    e = ht.coop == 2   ? launch_leaf_v<LD_PAIR>(device, d, t, ht, s)
+    e = ht.coop == 3   ? launch_leaf_v<LD_PAIR, true>(device, d, t, ht, s)
+        : ht.coop == 2 ? launch_leaf_v<LD_PAIR>(device, d, t, ht, s)
         : ht.coop == 1 ? launch_leaf_v<LD_COOP64>(device, d, t, ht, s)
                        : launch_leaf_v<LD_PLAIN>(device, d, t, ht, s);
     if (e != hipSuccess) return e;

@@ -400,7 +400,9 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
     if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
     if (const char *ld = getenv("SYNCR_B3_LOAD"))                                         // A/B only
-        h->b3_coop = strcmp(ld, "plain") == 0 ? 0u : (strcmp(ld, "coop") == 0 ? 1u : 2u);
+        h->b3_coop = strcmp(ld, "plain") == 0  ? 0u
+                     : strcmp(ld, "coop") == 0 ? 1u
+                     : strcmp(ld, "pairmq") == 0 ? 3u : 2u;    // pairmq: + quad merges
     if (const char *k = getenv("SYNCR_CDC_SCAN")) {
         if (strcmp(k, "valu") == 0) h->geom = ScanGeom{SCAN_VALU, DEFAULT_RUN, 0};
         if (strcmp(k, "mfma") == 0) h->geom = ScanGeom{SCAN_MFMA, DEFAULT_NB, MFV_SINGLE | MFV_NOPIPE};
