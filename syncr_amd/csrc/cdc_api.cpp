@@ -76,7 +76,7 @@ struct syncr_cdc {
         dense_list, dense_cnt, dense_bits, super_off, cand, cuts, counts;
     // BLAKE3 of every chunk (launch_hashed)
     bool hash_on = false;
-    uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 2;     // dev A/B knobs; coop 2 = the product's LD_PAIR
+    uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 3;     // dev A/B knobs; coop 3 = the product (LD_PAIR + quad merges)
     uint64_t items_cap = 0, trees_cap = 0;
     DevBuf hctr, items, trees, gcv, hashes, packed;
     // read-boundary grid (Tables::gpos...): production semantics only
@@ -402,7 +402,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *ld = getenv("SYNCR_B3_LOAD"))                                         // A/B only
         h->b3_coop = strcmp(ld, "plain") == 0  ? 0u
                      : strcmp(ld, "coop") == 0 ? 1u
-                     : strcmp(ld, "pairmq") == 0 ? 3u : 2u;    // pairmq: + quad merges
+                     : strcmp(ld, "pair") == 0 ? 2u : 3u;      // default / pairmq: + quad merges
     if (const char *k = getenv("SYNCR_CDC_SCAN")) {
         if (strcmp(k, "valu") == 0) h->geom = ScanGeom{SCAN_VALU, DEFAULT_RUN, 0};
         if (strcmp(k, "mfma") == 0) h->geom = ScanGeom{SCAN_MFMA, DEFAULT_NB, MFV_SINGLE | MFV_NOPIPE};

@@ -137,8 +137,9 @@ struct HashTables {
     uint32_t *hashes;              // [sum cut_cap * 8] BLAKE3 of each cut slot
     uint32_t ablate;               // timing-only (SYNCR_B3_ABLATE): 1 = loads only, 2 = no loads
     uint32_t nt;                   // 1: non-temporal chunk loads (SYNCR_B3_NT)
-    uint32_t coop;                 // 2 (product): cooperative LDS-DMA loader, two blocks per round; 1: one
-                                   //   block per round (SYNCR_B3_LOAD=coop); 0: per-lane loads (=plain)
+    uint32_t coop;                 // 3 (product): cooperative LDS-DMA loader, two blocks per round, quad
+                                   //   merges; 2: shuffle merges (SYNCR_B3_LOAD=pair); 1: one block per
+                                   //   round (=coop); 0: per-lane loads (=plain)
 };
 
 // launchers (cdc_kernels.hip)
