@@ -103,6 +103,10 @@ def workload(name: str, world: int):
     elif name == "uniform1k":
         one = np.full(1024, M, np.uint64)
         desc = "SURVEY §8d config 2: 1024 x 1 MiB files per GPU, LPT-sharded per file"
+    elif name in ("uniform2k", "uniform4k"):
+        n = 2048 if name == "uniform2k" else 4096
+        one = np.full(n, M, np.uint64)
+        desc = f"diagnostic: {n} x 1 MiB files per GPU (batch-size sweep between uniform1k and zipf10k)"
     else:
         raise SystemExit(f"unknown workload {name}")
     sizes = np.tile(one, world)
@@ -348,7 +352,7 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "dense", "big1", "dense1"])
+    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "uniform2k", "uniform4k", "dense", "big1", "dense1"])
     ap.add_argument("--mode", default="production", choices=["production", "ideal"])
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -329,6 +329,15 @@ __device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, u
 // single-op dependency chains in the roll (16; same process, zipf10k: scan
 // 1.591 vs 1.640 ms, profiles/r02_ab_roll2.log).
 constexpr int SCAN_PRODUCT_MODE = 4 | 8 | 16;
+// Small batches use the static stride: a group of 8 tiles is ~46 us of one
+// wave's roll, and below ~80-100 tiles per wave the last groups' imbalance
+// costs more than the dynamic grab recovers (same process, ROLL2 in both,
+// tools/ab_bench.py: profiles/r02_ab_schedule.log).  scan_dynamic() picks.
+constexpr int SCAN_STATIC_MODE = 4 | 16;
+constexpr uint32_t SCAN_DYN_MIN_TILES_PER_WAVE = 96;
+__host__ __device__ constexpr bool scan_dynamic(uint32_t ntiles, uint32_t grid) {
+    return (uint64_t)ntiles >= (uint64_t)grid * SCAN_DYN_MIN_TILES_PER_WAVE;
+}
 
 // MODE bit 5: ask for 3 waves per SIMD (VGPRs <= 168; development A/B only)
 template <int RUN, int MODE>
@@ -1531,8 +1540,10 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 3u)                                         // timing only: staging, nt
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 5>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 4u)                                         // A/B: static stride (exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 4>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 4u)                                         // A/B: static stride always (exact)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 8u)                                         // A/B: dynamic groups always (exact)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 5u)                                         // A/B: round-1 roll (two dependent mads, exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 6u)                                         // timing only: roll, no DMA
@@ -1540,8 +1551,10 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
     else if (p.ablate == 7u)                                         // A/B: product + 3 waves per SIMD hint
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, d, p,
                            t);
-    else if (p.nt)                                                   // product: nt loads + dynamic groups + ROLL2
+    else if (p.nt && scan_dynamic(t.ntiles, grid))                   // product: nt loads + dynamic groups + ROLL2
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.nt)                                                   // product, small batch: static stride
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE & ~4>), dim3(grid), dim3(64), lds, s, d, p, t);
 }
@@ -1612,8 +1625,12 @@ hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParam
     if (!t.ntiles) return hipSuccess;
     if (!scan_supported(g)) return hipErrorInvalidValue;
     grid = grid < t.ntiles ? grid : t.ntiles;
-    hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
-                       lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
+    if (scan_dynamic(t.ntiles, grid))
+        hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
+                           lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
+    else
+        hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64),
+                           lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
     return hipGetLastError();
 }
 #endif
