@@ -100,6 +100,10 @@ def workload(name: str, world: int):
     elif name == "dense1":
         one = np.full(1, 128 * M, np.uint64)
         desc = "diagnostic: one 128 MiB periodic-64 file (2 M chained cuts: the dense workload's longest walk)"
+    elif name == "dedup":
+        one = np.array([p[4] for p in dedup_plan()], np.uint64)
+        desc = ("SURVEY §8d config 5: 1000 files per GPU, each one 1-256 byte edit (50 % overwrite, 25 % insert, "
+                "25 % delete) of one random 32 MiB base, ~32 GiB (boundary stability in config.dedup)")
     elif name == "uniform1k":
         one = np.full(1024, M, np.uint64)
         desc = "SURVEY §8d config 2: 1024 x 1 MiB files per GPU, LPT-sharded per file"
@@ -111,6 +115,70 @@ def workload(name: str, world: int):
         raise SystemExit(f"unknown workload {name}")
     sizes = np.tile(one, world)
     return sizes, np.arange(sizes.size, dtype=np.uint64), desc
+
+
+DEDUP_BASE = 32 * M
+
+
+def dedup_plan(n: int = 1000, seed: int = 20251212):
+    """(kind, pos, len, inserted bytes, file size) of the dedup corpus's variants."""
+    rng = np.random.default_rng(seed)
+    plan = []
+    for _ in range(n):
+        pos = int(rng.integers(0, DEDUP_BASE))
+        ln = int(rng.integers(1, 257))
+        kind = ("overwrite", "overwrite", "insert", "delete")[int(rng.integers(0, 4))]
+        ins = rng.integers(0, 256, ln, dtype=np.uint8)
+        d = min(ln, DEDUP_BASE - pos)
+        size = DEDUP_BASE + (ln if kind == "insert" else (-d if kind == "delete" else 0))
+        plan.append((kind, pos, ln, ins, size))
+    return plan
+
+
+def dedup_base() -> np.ndarray:
+    return np.random.default_rng(31337).integers(0, 256, DEDUP_BASE, dtype=np.uint8)
+
+
+def dedup_file(base: np.ndarray, entry) -> tuple[np.ndarray, int, int]:
+    """One variant's bytes and its edit (position, size delta)."""
+    kind, pos, ln, ins, _ = entry
+    if kind == "overwrite":
+        f = base.copy()
+        k = max(0, min(ln, base.size - pos))
+        f[pos:pos + k] = ins[:k]
+        return f, pos, 0
+    if kind == "insert":
+        return np.concatenate([base[:pos], ins, base[pos:]]), pos, ln
+    d = min(ln, base.size - pos)
+    return np.concatenate([base[:pos], base[pos + d:]]), pos, -d
+
+
+def fill_dedup(dbuf, offs, lens, idx):
+    """Upload the dedup variants (file j is variant idx[j] % 1000 of the plan)."""
+    plan, base = dedup_plan(), dedup_base()
+    for j in range(lens.size):
+        f, _, _ = dedup_file(base, plan[int(idx[j]) % len(plan)])
+        assert f.size == int(lens[j])
+        dbuf.upload(f, offset=int(offs[j]))
+
+
+def dedup_stability(cuts, idx) -> dict:
+    """Fraction of the base's cut positions each variant keeps (shift-adjusted)."""
+    plan, base = dedup_plan(), dedup_base()
+    import syncr_amd
+    with syncr_amd.Chunker() as c:
+        bc = c.batch_arrays(base, np.zeros(1, np.uint64), np.array([base.size], np.uint64))[0]
+    base_cuts = set((bc["offset"].astype(np.int64) + bc["len"].astype(np.int64)).tolist())
+    kept = []
+    for c, i in zip(cuts, idx.tolist()):
+        kind, pos, ln, _, _ = plan[int(i) % len(plan)]
+        delta = ln if kind == "insert" else (-min(ln, DEDUP_BASE - pos) if kind == "delete" else 0)
+        ends = (c["offset"].astype(np.int64) + c["len"].astype(np.int64)).tolist()
+        adj = {e - delta if e > pos else e for e in ends}
+        kept.append(len(adj & base_cuts) / max(len(base_cuts), 1))
+    return {"base_cuts": len(base_cuts), "kept_median": round(float(np.median(kept)), 4),
+            "kept_min": round(float(np.min(kept)), 4),
+            "note": "share of the base file's cut offsets present in each variant (offsets past the edit shifted back)"}
 
 
 def lpt_shard(sizes: np.ndarray, world: int) -> list[np.ndarray]:
@@ -352,7 +420,8 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "uniform2k", "uniform4k", "dense", "big1", "dense1"])
+    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "uniform2k", "uniform4k", "dense", "big1", "dense1",
+                                                           "dedup"])
     ap.add_argument("--mode", default="production", choices=["production", "ideal"])
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -422,6 +491,8 @@ def main(argv=None):
             fill_dense(b, offs, lens, idx)
         elif args.workload == "dense1":
             b.upload(np.resize(periodic_pattern(), span))
+        elif args.workload == "dedup":
+            fill_dedup(b, offs, lens, idx)
         h.plan(offs, lens, span)
         slots.append((h, b))
     ch, dbuf = slots[0]
@@ -601,8 +672,10 @@ def main(argv=None):
             "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic: per-file xorshift64 corpus generated in HBM (SURVEY §8d seed rule)"
-                    + ("; adversarial files uploaded from the host (dense_kind)" if args.workload == "dense" else ""),
+            "data": ("synthetic: one random 32 MiB base (numpy PCG64, seed 31337) and its single-edit variants, "
+                     "uploaded from the host" if args.workload == "dedup" else
+                     "synthetic: per-file xorshift64 corpus generated in HBM (SURVEY §8d seed rule)"
+                     + ("; adversarial files uploaded from the host (dense_kind)" if args.workload == "dense" else "")),
             "config": {
                 "workload": f"{args.workload}: {desc}", "files_per_gpu": int(lens.size),
                 "bytes_per_gpu": span, "total_bytes": int(total_bytes), "chunk_bits": 20,
@@ -623,6 +696,8 @@ def main(argv=None):
             "sustained": sustained,
             "hashed": hashed,
         }
+        if args.workload == "dedup":
+            out["config"]["dedup"] = dedup_stability(cuts, idx)
         if args.workload == "dense":
             kinds = np.array([dense_kind(int(i)) for i in idx.tolist()])
             out["config"]["adversarial_bytes_frac"] = {
