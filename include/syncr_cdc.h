@@ -203,6 +203,8 @@ int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4);
 /* per sub-pipeline k: stats[4k..4k+3] = [device, files, bytes, batches];
  * SYNCR_CDC_ERANGE if n < 4 * ndevices */
 int32_t syncr_ingest_device_stats(const syncr_ingest *g, uint64_t *stats, uint32_t n);
+/* release everything; files not yet delivered (no flush since their submit)
+ * get no callback */
 void syncr_ingest_close(syncr_ingest *g);
 
 /* --- chunk cache (skip re-chunking unchanged files) ---------------------------
