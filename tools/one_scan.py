@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Run one engine variant on the zipf10k corpus for --launches launches (for
 rocprofv3 counter passes).  The variant is taken from the environment
-(SYNCR_CDC_NB, SYNCR_CDC_MFVAR, SYNCR_CDC_ABLATE, SYNCR_CDC_RUN, ...).
+(SYNCR_CDC_NB, SYNCR_CDC_MFVAR, SYNCR_CDC_ABLATE, SYNCR_CDC_RUN, ...), read only by
+the development library (python -m syncr_amd.build --dev), which this loads.
 
     rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d out -- python3 tools/one_scan.py
 """
@@ -16,6 +17,8 @@ import numpy as np  # noqa: E402
 
 import bench  # noqa: E402
 import syncr_amd  # noqa: E402
+
+syncr_amd.use_dev_library()                  # the product library ignores the environment
 
 
 def main():

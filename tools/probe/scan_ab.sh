@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 4
 tail -2 gpurun_out/scan_tests.log
 for ab in 0 2; do
  for i in 1 2; do
-  for L in tools/probe/old.so syncr_amd/libsyncr_cdc.so; do
+  for L in tools/probe/old.so syncr_amd/libsyncr_cdc_dev.so; do     # ablations: development builds only
     SYNCR_CDC_ABLATE=$ab timeout -k 10 200 python -u tools/probe/benchlib.py $L --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/sab.json 2>gpurun_out/sab.err || { tail gpurun_out/sab.err; exit 2; }
     python3 -c "import json;d=json.load(open('gpurun_out/sab.json'));r=d['roofline'];print('ablate $ab', '$L'.split('/')[-1], d['value'], d['ms_per_step'], r['kernel_ms'], r['frac'])"
   done

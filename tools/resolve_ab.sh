@@ -12,7 +12,7 @@ tail -2 "$O/gpu_tests.log"
 for w in big1 zipf10k; do
   for v in ${@:-default noburst}; do
     if [ $v = default ]; then unset SYNCR_CDC_RESOLVE; else export SYNCR_CDC_RESOLVE=$v; fi
-    timeout -k 10 200 python -u bench.py --workload $w --no-cpu-baseline --no-read-probe --pipeline-depth 1 > "$O/ab_${w}_$v.json" 2> "$O/ab_${w}_$v.err" || { echo "bench $w $v failed"; tail -5 "$O/ab_${w}_$v.err"; exit 12; }
+    timeout -k 10 200 python -u bench.py --dev-lib --workload $w --no-cpu-baseline --no-read-probe --pipeline-depth 1 > "$O/ab_${w}_$v.json" 2> "$O/ab_${w}_$v.err" || { echo "bench $w $v failed"; tail -5 "$O/ab_${w}_$v.err"; exit 12; }
     python -c "import json;d=json.load(open('$O/ab_${w}_$v.json'));r=d['roofline'];print('$w $v', d['value'], d['ms_per_step'], r['kernel_ms'], r['resolve_ms'])"
   done
 done
