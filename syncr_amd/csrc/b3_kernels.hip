@@ -201,8 +201,8 @@ __device__ __forceinline__ uint32_t ceil_log2(uint32_t t) { return t <= 1 ? 0u :
 // whose cuts overflowed its output slots is skipped (the host re-launches).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
-    constexpr int NL = B3_CLASSES + 2;                   // lists: classes, group items, trees
-    constexpr int LIST_ITEMS = B3_CLASSES, LIST_TREES = B3_CLASSES + 1;
+    constexpr int NL = B3_CLASSES + 3;                   // lists: classes, group items, trees, pieces
+    constexpr int LIST_ITEMS = B3_CLASSES, LIST_TREES = B3_CLASSES + 1, LIST_PIECES = B3_CLASSES + 2;
     __shared__ uint32_t cnt[NL];
     __shared__ uint64_t gbase[NL];
     __shared__ uint32_t foff[257];                       // exclusive prefix of cut counts
@@ -226,6 +226,31 @@ __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
     if (t == 0) foff[0] = 0;
     __syncthreads();
     const uint32_t total = foff[256];
+    // a unit of r tasks (first task k0) whose r is not a power of two becomes
+    // popcount(r) pieces, the binary digits of r largest first
+    auto put_pieces = [&](bool place, uint64_t slot, uint32_t k0, uint32_t r, uint64_t &pbase) {
+        const uint32_t np = (uint32_t)__builtin_popcount(r);
+        const uint32_t lpc = atomicAdd(&cnt[LIST_PIECES], np);
+        pbase = place ? gbase[LIST_PIECES] + lpc : 0ull;
+        uint32_t off = k0, p = 0;
+        for (int b = 6; b >= 0; --b) {
+            if (!((r >> b) & 1u)) continue;
+            const uint32_t li = atomicAdd(&cnt[b], 1u);
+            if (place) {
+                const uint64_t pi = pbase + p;
+                const uint64_t idx = gbase[b] + li;
+                if (pi < H.pieces_cap) {
+                    H.pieces[pi] = make_ulonglong2(slot, off);
+                    if (idx < H.packed_cap) H.packed[b * H.packed_cap + idx] = B3_PIECE | pi;
+                } else {
+                    atomicOr((unsigned long long *)&H.ctr[B3C_FLAGS], 2ull);
+                }
+            }
+            off += 1u << b;
+            ++p;
+        }
+        return np;
+    };
     auto visit = [&](bool place) {
         for (uint32_t q = t; q < total; q += 256) {
             uint32_t lo = 0, hi = 256;                   // last f with foff[f] <= q
@@ -236,24 +261,40 @@ __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
             const uint64_t slot = fbase[lo] + (q - foff[lo]);
             const uint32_t tk = chunk_tasks(T.cuts[slot].len);
             if (tk <= 64) {
-                const uint32_t c = ceil_log2(tk);
-                const uint32_t li = atomicAdd(&cnt[c], 1u);
-                if (place) {
-                    const uint64_t idx = gbase[c] + li;
-                    if (idx < H.packed_cap) H.packed[c * H.packed_cap + idx] = slot;
+                if ((tk & (tk - 1)) == 0 || H.nosplit) {  // one unit: the whole chunk
+                    const uint32_t c = ceil_log2(tk);
+                    const uint32_t li = atomicAdd(&cnt[c], 1u);
+                    if (place) {
+                        const uint64_t idx = gbase[c] + li;
+                        if (idx < H.packed_cap) H.packed[c * H.packed_cap + idx] = slot;
+                    }
+                } else {                                 // pieces, folded (with ROOT) by the tree kernel
+                    uint64_t pb = 0;
+                    const uint32_t np = put_pieces(place, slot, 0u, tk, pb);
+                    const uint32_t lt = atomicAdd(&cnt[LIST_TREES], 1u);
+                    if (place) {
+                        const uint64_t ti = gbase[LIST_TREES] + lt;
+                        if (ti < H.trees_cap) {
+                            H.trees[ti] = make_ulonglong2(slot, ~0ull);
+                            H.tpieces[ti] = (pb << 8) | np;
+                        }
+                    }
                 }
             } else {                                     // big chunk: full group items + tail unit
                 const uint32_t tail = tk % 64, ng = tk / 64 + (tail ? 1u : 0u);
                 const uint32_t li = atomicAdd(&cnt[LIST_ITEMS], ng);
                 const uint32_t lt = atomicAdd(&cnt[LIST_TREES], 1u);
+                const bool split = tail && (tail & (tail - 1)) != 0 && !H.nosplit;
                 const uint32_t c = ceil_log2(tail);
-                const uint32_t lp = tail ? atomicAdd(&cnt[c], 1u) : 0u;
+                const uint32_t lp = (tail && !split) ? atomicAdd(&cnt[c], 1u) : 0u;
+                uint64_t pb = 0;
+                const uint32_t np = split ? put_pieces(place, slot, (ng - 1) * 64u, tail, pb) : 0u;
                 if (place) {
                     const uint64_t first = gbase[LIST_ITEMS] + li;
                     if (first + ng <= H.items_cap) {
                         for (uint32_t g = 0; g < ng; ++g)   // the tail's entry is a placeholder
                             H.items[first + g] = (slot << 24) | g | (tail && g + 1 == ng ? B3_TAIL : 0ull);
-                        if (tail) {
+                        if (tail && !split) {
                             const uint64_t idx = gbase[c] + lp;
                             if (idx < H.packed_cap) H.packed[c * H.packed_cap + idx] = B3_TAIL | (first + ng - 1);
                         }
@@ -261,7 +302,10 @@ __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
                         atomicOr((unsigned long long *)&H.ctr[B3C_FLAGS], 1ull);
                     }
                     const uint64_t ti = gbase[LIST_TREES] + lt;
-                    if (ti < H.trees_cap) H.trees[ti] = make_ulonglong2(slot, first);
+                    if (ti < H.trees_cap) {
+                        H.trees[ti] = make_ulonglong2(slot, first);
+                        H.tpieces[ti] = (pb << 8) | np;
+                    }
                 }
             }
         }
@@ -269,7 +313,8 @@ __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
     visit(false);                                        // pass 1: count per list
     __syncthreads();
     if (t < NL) {
-        const uint32_t gi = t < B3_CLASSES ? B3C_PK0 + t : (t == LIST_ITEMS ? B3C_ITEMS : B3C_TREES);
+        const uint32_t gi = t < B3_CLASSES ? B3C_PK0 + t
+                          : (t == LIST_ITEMS ? B3C_ITEMS : (t == LIST_TREES ? B3C_TREES : B3C_PIECES));
         gbase[t] = cnt[t] ? atomicAdd((unsigned long long *)&H.ctr[gi], (unsigned long long)cnt[t]) : 0ull;
         cnt[t] = 0;
     }
@@ -581,8 +626,8 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
         uint32_t dmax;           // merge levels: lanes per unit in this wave (uniform)
         bool root;               // this unit is the whole chunk (its merge gets ROOT)
         const bool group = w < nbig;                             // uniform
-        uint64_t out_item = w;                                   // group item / tail: its gcv slot
-        bool tail = false;
+        uint64_t out_item = w;                                   // group item / tail: its gcv slot; piece: index
+        bool tail = false, piece = false;
         uint32_t k0 = 0;                                         // first task of this unit
         if (group) {                                             // 64 tasks of a big chunk
             const uint64_t code = H.items[w];
@@ -607,21 +652,28 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
             k = (uint32_t)lane & ((1u << c) - 1u);
             km = k;
             valid = idx < npk[c];
+            piece = false;
             if (valid) {
                 const uint64_t code = H.packed[c * H.packed_cap + idx];
                 tail = (code & B3_TAIL) != 0;
+                piece = (code & B3_PIECE) != 0;
                 if (tail) {                                      // T % 64 tail tasks of a big chunk
                     out_item = code & ~B3_TAIL;
                     const uint64_t ic = H.items[out_item] & ~B3_TAIL;
                     slot = ic >> 24;
                     k0 = ((uint32_t)ic & 0xffffffu) * 64;
+                } else if (piece) {                              // 2^c tasks of a split unit
+                    out_item = code & ~B3_PIECE;
+                    const ulonglong2 pd = H.pieces[out_item];
+                    slot = pd.x;
+                    k0 = (uint32_t)pd.y;
                 } else {
                     slot = code;
                 }
             }
             mm = 0;
             dmax = 1u << c;
-            root = !tail;
+            root = !tail && !piece;
         }
         uint32_t len = 0;
         uint64_t cstart = 0;
@@ -631,9 +683,12 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
             cstart = T.foff[cu.file] + cu.offset;                // batch offset of the chunk
             if (!group) {
                 k += k0;
-                mm = chunk_tasks(len) - k0;
+                mm = min(dmax, chunk_tasks(len) - k0);           // a piece before the last one is full
             }
         }
+        // where the unit's CV goes, fixed before the block loop (slot and
+        // out_item then need not stay live through it)
+        uint32_t *const dst = root ? H.hashes + slot * 8 : (piece ? H.pcv : H.gcv) + out_item * 8;
         const uint32_t nleaves = chunk_leaves(len);
         const uint32_t j0 = k * LPL;
         const bool act = valid && j0 < nleaves;
@@ -718,7 +773,6 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
         }
         }
         if (act && km == 0) {
-            uint32_t *dst = root ? H.hashes + slot * 8 : H.gcv + out_item * 8;
             *(uint4 *)dst = make_uint4(x[0], x[1], x[2], x[3]);
             *(uint4 *)(dst + 4) = make_uint4(x[4], x[5], x[6], x[7]);
         }
@@ -735,8 +789,34 @@ __global__ __launch_bounds__(256) void b3_tree_kernel(Tables T, HashTables H) {
     for (uint64_t w = blockIdx.x * 4ull + (threadIdx.x >> 6); w < ntrees; w += gridDim.x * 4ull) {
         const ulonglong2 e = H.trees[w];
         const uint64_t slot = e.x;
+        const bool small = e.y == ~0ull;                 // a split packed chunk: pieces only
+        uint32_t n = small ? 1u : (chunk_tasks(T.cuts[slot].len) + 63) / 64;
+        const uint64_t tp = H.tpieces[w];
+        const uint32_t np = (uint32_t)(tp & 0xffu);
+        if (np) {
+            // fold the pieces right to left (each left piece is a complete left
+            // subtree of the rest): the unit's CV, or the chunk's hash
+            const uint64_t pb = tp >> 8;
+            uint32_t x[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) x[q] = H.pcv[(pb + np - 1) * 8 + q];
+            for (int p = (int)np - 2; p >= 0; --p) {
+                uint32_t l[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) l[q] = H.pcv[(pb + (uint32_t)p) * 8 + q];
+                parent(l, x, (small && p == 0) ? B3_ROOT : 0u);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) x[q] = l[q];
+            }
+            if (lane == 0) {
+                uint32_t *dst = small ? H.hashes + slot * 8 : H.gcv + (e.y + n - 1) * 8;   // the tail's item
+                *(uint4 *)dst = make_uint4(x[0], x[1], x[2], x[3]);
+                *(uint4 *)(dst + 4) = make_uint4(x[4], x[5], x[6], x[7]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the tail CV is read below
+        }
+        if (small) continue;
         uint32_t *nodes = H.gcv + e.y * 8;
-        uint32_t n = (chunk_tasks(T.cuts[slot].len) + 63) / 64;
         while (n > 1) {
             const uint32_t nb = (n + 63) / 64;
             for (uint32_t b = 0; b < nb; ++b) {
@@ -764,7 +844,7 @@ __global__ __launch_bounds__(256) void b3_tree_kernel(Tables T, HashTables H) {
 }
 
 template <bool NT, int ABLATE, int LD, bool MQ>
-__global__ __launch_bounds__(256) void b3_leaf_kernel(const uint8_t *__restrict__ data, Tables T, HashTables H) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b3_leaf_kernel(const uint8_t *__restrict__ data, Tables T, HashTables H) {
     b3_leaf_body<NT, ABLATE, LD, MQ>(data, T, H);
 }
 

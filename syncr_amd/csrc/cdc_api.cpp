@@ -76,9 +76,10 @@ struct syncr_cdc {
         dense_list, dense_cnt, dense_bits, super_off, cand, cuts, counts;
     // BLAKE3 of every chunk (launch_hashed)
     bool hash_on = false;
-    uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 3;     // dev A/B knobs; coop 3 = the product (LD_PAIR + quad merges)
+    uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 3, b3_nosplit = 0;     // dev A/B knobs; coop 3 = the product (LD_PAIR + quad merges)
     uint64_t items_cap = 0, trees_cap = 0;
-    DevBuf hctr, items, trees, gcv, hashes, packed;
+    DevBuf hctr, items, trees, gcv, hashes, packed, tpieces, pieces, pcv;
+    uint64_t pieces_cap = 0;
     // read-boundary grid (Tables::gpos...): production semantics only
     uint32_t ngrid = 0;
     DevBuf gpos, gend, gfix, gbase;
@@ -208,6 +209,11 @@ int32_t upload_cut_tables(syncr_cdc *h) {
     CHECK_HIP(h->gcv.ensure(h->items_cap * 32));
     CHECK_HIP(h->hashes.ensure(std::max<uint64_t>(acc, 1) * 32));
     CHECK_HIP(h->packed.ensure((size_t)B3_CLASSES * std::max<uint64_t>(acc, 1) * 8));
+    // pieces: at most popcount(63) = 6 per chunk (a split unit has under 64 tasks)
+    h->pieces_cap = std::max<uint64_t>(6 * acc, 1);
+    CHECK_HIP(h->tpieces.ensure(h->trees_cap * 8));
+    CHECK_HIP(h->pieces.ensure(h->pieces_cap * 16));
+    CHECK_HIP(h->pcv.ensure(h->pieces_cap * 32));
     CHECK_HIP(h->cut_base.ensure(std::max<size_t>(h->nfiles, 1) * 8));
     CHECK_HIP(h->cut_cap.ensure(std::max<size_t>(h->nfiles, 1) * 4));
     CHECK_HIP(h->cuts.ensure(std::max<uint64_t>(acc, 1) * sizeof(DevCut)));
@@ -225,6 +231,10 @@ HashTables make_hash_tables(syncr_cdc *h) {
     t.items_cap = h->items_cap;
     t.trees = h->trees.as<ulonglong2>();
     t.trees_cap = h->trees_cap;
+    t.tpieces = h->tpieces.as<uint64_t>();
+    t.pieces = h->pieces.as<ulonglong2>();
+    t.pcv = h->pcv.as<uint32_t>();
+    t.pieces_cap = h->pieces_cap;
     t.gcv = h->gcv.as<uint32_t>();
     t.hashes = h->hashes.as<uint32_t>();
     t.packed = h->packed.as<uint64_t>();
@@ -232,6 +242,7 @@ HashTables make_hash_tables(syncr_cdc *h) {
     t.ablate = h->b3_ablate;
     t.nt = h->b3_nt;
     t.coop = h->b3_coop;
+    t.nosplit = h->b3_nosplit;
     return t;
 }
 
@@ -399,6 +410,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_CDC_SERIAL")) h->serial_scans = atoi(a) != 0;
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
     if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
+    if (const char *sp = getenv("SYNCR_B3_SPLIT")) h->b3_nosplit = atoi(sp) == 0;          // A/B only
     if (const char *ld = getenv("SYNCR_B3_LOAD"))                                         // A/B only
         h->b3_coop = strcmp(ld, "plain") == 0  ? 0u
                      : strcmp(ld, "coop") == 0 ? 1u
@@ -460,7 +472,7 @@ void syncr_cdc_close(syncr_cdc *h) {
                       &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
                       &h->dense_cnt, &h->dense_bits, &h->super_off, &h->cand, &h->cuts,
                       &h->counts, &h->stage, &h->hctr, &h->items, &h->trees, &h->gcv,
-                      &h->hashes, &h->packed, &h->gpos, &h->gend, &h->gfix, &h->gbase};
+                      &h->hashes, &h->packed, &h->tpieces, &h->pieces, &h->pcv, &h->gpos, &h->gend, &h->gfix, &h->gbase};
     for (DevBuf *b : bufs) b->release();
     (void)hipStreamDestroy(h->stream);
     delete h;
@@ -655,7 +667,8 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
                 if (hashed) {
                     uint64_t hc[B3C_WORDS];
                     CHECK_HIP(hipMemcpy(hc, h->hctr.p, sizeof hc, hipMemcpyDeviceToHost));
-                    if (hc[B3C_FLAGS] || hc[B3C_ITEMS] > h->items_cap || hc[B3C_TREES] > h->trees_cap)
+                    if (hc[B3C_FLAGS] || hc[B3C_ITEMS] > h->items_cap || hc[B3C_TREES] > h->trees_cap ||
+                        hc[B3C_PIECES] > h->pieces_cap)
                         return SYNCR_CDC_EIO;          // capacities are exact bounds: cannot happen
                     hs.resize(h->total_cut_cap * 32);
                     CHECK_HIP(hipMemcpy(hs.data(), h->hashes.p, hs.size(), hipMemcpyDeviceToHost));

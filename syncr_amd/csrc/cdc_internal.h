@@ -118,12 +118,19 @@ struct Tables {
 // wave, each in an aligned run of 2^c lanes.  A chunk of T > 64 tasks (a BIG
 // chunk) is floor(T / 64) GROUP items of 64 tasks (one wave each) plus, when
 // T % 64 != 0, a TAIL unit of the last T % 64 tasks packed like a small chunk;
-// b3_tree_kernel merges the items' and the tail's subtree CVs.
+// b3_tree_kernel merges the items' and the tail's subtree CVs.  A unit whose
+// task count r is not a power of two (a small chunk or a tail) is split into
+// PIECES by the binary digits of r, largest first -- exactly the subtrees of
+// BLAKE3's left-balanced tree -- so each piece fills its 2^c lanes; the tree
+// kernel folds the piece CVs right to left.
 constexpr uint32_t B3_LANE_LEAVES = 4;                      // 1 KiB leaves per lane task
 constexpr uint32_t B3_GROUP_LEAVES = 64 * B3_LANE_LEAVES;   // leaves per group item (one wave)
 constexpr int B3_CLASSES = 7;                               // packed classes: <= 1, 2, 4, ..., 64 tasks
 constexpr uint64_t B3_TAIL = 1ull << 63;                  // packed entry: tail unit
-enum { B3C_ITEMS = 0, B3C_TREES = 1, B3C_NEXT = 2, B3C_FLAGS = 3, B3C_PK0 = 4, B3C_WORDS = 4 + B3_CLASSES };
+constexpr uint64_t B3_PIECE = 1ull << 62;                 // packed entry: piece (index into pieces[])
+constexpr uint32_t B3_MAX_PIECES = 7;                     // popcount of a task count <= 127
+enum { B3C_ITEMS = 0, B3C_TREES = 1, B3C_NEXT = 2, B3C_FLAGS = 3, B3C_PK0 = 4, B3C_PIECES = 4 + B3_CLASSES,
+       B3C_WORDS = 5 + B3_CLASSES };
 
 struct HashTables {
     uint64_t *ctr;                 // [B3C_WORDS] (zeroed per hashed launch)
@@ -131,8 +138,13 @@ struct HashTables {
     uint64_t items_cap;
     uint64_t *packed;              // [B3_CLASSES * packed_cap] by packed class: a chunk slot, or
     uint64_t packed_cap;           //   B3_TAIL | its placeholder item for a big chunk's tail unit
-    ulonglong2 *trees;             // [trees_cap] {slot, first item} of big chunks
+    ulonglong2 *trees;             // [trees_cap] {slot, first item or ~0} of big and of split chunks
+    uint64_t *tpieces;             // [trees_cap] first piece << 8 | pieces (0: none) of each tree
     uint64_t trees_cap;
+    ulonglong2 *pieces;            // [pieces_cap] {slot, first task}: a piece's chunk and position
+    uint32_t *pcv;                 // [pieces_cap * 8] CV of each piece
+    uint64_t pieces_cap;
+    uint32_t nosplit;              // dev A/B only (SYNCR_B3_SPLIT=0): one unit per power-of-two class, no pieces
     uint32_t *gcv;                 // [items_cap * 8] subtree CV of each item (or tail placeholder)
     uint32_t *hashes;              // [sum cut_cap * 8] BLAKE3 of each cut slot
     uint32_t ablate;               // timing-only (SYNCR_B3_ABLATE): 1 = loads only, 2 = no loads
