@@ -359,7 +359,8 @@ template <bool NT, int ABLATE, int LD>
 __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ data, uint64_t span, uint32_t stage,
                                                  uint32_t *stage_ptr, int lane, bool act, uint64_t tp,
                                                  uint32_t nbytes, uint32_t nblk, uint32_t nl, uint32_t nleaves,
-                                                 uint32_t j0, bool task_root, uint32_t x[8]) {
+                                                 uint32_t j0, bool task_root, bool uni, uint64_t tp0,
+                                                 uint32_t x[8]) {
     // leaf CVs are folded as they complete (left-balanced pairing of <= 4
     // leaves): x = leaf 0, then node(0,1); y = leaf 2, then node(2,3)
     uint32_t y[8];
@@ -375,6 +376,23 @@ __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ dat
     // compression cost 5 -> 4 waves/SIMD
     constexpr bool PAIR = LD == LD_PAIR;
     auto issue = [&](uint32_t t) {           // PAIR: t is even, blocks t and t+1
+        if constexpr (PAIR) {
+            if (uni) {
+                // a group item inside the batch (wave-uniform): task q starts at
+                // tp0 + 4096 q, so instruction i's source is the SGPR base
+                // tp0 + 64 t + 32768 i plus a per-lane offset fixed for the item
+                // ((q >> 1) & 3 == (lane >> 4) & 3 for every i) -- no shuffles, no
+                // per-piece branch; pieces past a partial last task are fetched
+                // from inside the batch and overwritten by the owner's fix-up
+                const uint32_t pos = (uint32_t)lane & 7u;
+                const uint32_t pc = (pos & 4u) | ((pos & 3u) ^ (((uint32_t)lane >> 4) & 3u));
+                const uint32_t voff = ((uint32_t)lane >> 3) * 4096u + pc * 16u;
+                const uint64_t b = (uint64_t)(data + tp0) + (uint64_t)t * 64u;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) dma16_s<NT>(voff, b + 32768ull * (uint64_t)i, stage + (uint32_t)i * 1024u);
+                return;
+            }
+        }
         // opaque copies: keep the shuffles here instead of hoisted out of the loop
         uint32_t tl = (uint32_t)tp, th = (uint32_t)(tp >> 32), pl = plim;
         asm volatile("" : "+v"(tl), "+v"(th), "+v"(pl));
@@ -699,8 +717,11 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
         const bool task_root = root && mm == 1;                  // the task is the whole chunk
         uint32_t x[8];
         if constexpr (COOP) {
+            // uniform fast loader: a group item whose 64 tasks (256 KiB) lie inside the batch
+            const uint64_t tp0 = group ? bcast64(cstart + ((uint64_t)k0 << 12)) : 0ull;
+            const bool uni = group && tp0 + (64ull << 12) + 16u <= T.span && !H.nouni;
             leaf_blocks_coop<NT, ABLATE, LD>(data, T.span, stage, stage_ptr, lane, act, cstart + lane_off, nbytes,
-                                         nblk, nl, nleaves, j0, task_root, x);
+                                         nblk, nl, nleaves, j0, task_root, uni, tp0, x);
         } else {
             uint32_t lc[LPL][8];                                 // leaf CVs
             // block t of the task (t < nblk) is at task offset 64*t; the next

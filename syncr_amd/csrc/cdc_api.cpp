@@ -76,7 +76,7 @@ struct syncr_cdc {
         dense_list, dense_cnt, dense_bits, super_off, cand, cuts, counts;
     // BLAKE3 of every chunk (launch_hashed)
     bool hash_on = false;
-    uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 3, b3_nosplit = 0;     // dev A/B knobs; coop 3 = the product (LD_PAIR + quad merges)
+    uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 3, b3_nosplit = 0, b3_nouni = 0;     // dev A/B knobs; coop 3 = the product (LD_PAIR + quad merges)
     uint64_t items_cap = 0, trees_cap = 0;
     DevBuf hctr, items, trees, gcv, hashes, packed, tpieces, pieces, pcv;
     uint64_t pieces_cap = 0;
@@ -243,6 +243,7 @@ HashTables make_hash_tables(syncr_cdc *h) {
     t.nt = h->b3_nt;
     t.coop = h->b3_coop;
     t.nosplit = h->b3_nosplit;
+    t.nouni = h->b3_nouni;
     return t;
 }
 
@@ -411,6 +412,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
     if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
     if (const char *sp = getenv("SYNCR_B3_SPLIT")) h->b3_nosplit = atoi(sp) == 0;          // A/B only
+    if (const char *un = getenv("SYNCR_B3_UNI")) h->b3_nouni = atoi(un) == 0;              // A/B only
     if (const char *ld = getenv("SYNCR_B3_LOAD"))                                         // A/B only
         h->b3_coop = strcmp(ld, "plain") == 0  ? 0u
                      : strcmp(ld, "coop") == 0 ? 1u

@@ -145,6 +145,7 @@ struct HashTables {
     uint32_t *pcv;                 // [pieces_cap * 8] CV of each piece
     uint64_t pieces_cap;
     uint32_t nosplit;              // dev A/B only (SYNCR_B3_SPLIT=0): one unit per power-of-two class, no pieces
+    uint32_t nouni;                // dev A/B only (SYNCR_B3_UNI=0): group items use the per-task loader
     uint32_t *gcv;                 // [items_cap * 8] subtree CV of each item (or tail placeholder)
     uint32_t *hashes;              // [sum cut_cap * 8] BLAKE3 of each cut slot
     uint32_t ablate;               // timing-only (SYNCR_B3_ABLATE): 1 = loads only, 2 = no loads

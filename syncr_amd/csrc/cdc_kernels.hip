@@ -251,33 +251,6 @@ __device__ __forceinline__ void publish_tile(const uint8_t *__restrict__ data, c
     }
 }
 
-// 16 B per lane from a wave-uniform SGPR base + per-lane VGPR offset into LDS.
-// NT: non-temporal policy (the bytes are read exactly once).
-template <bool NT>
-__device__ __forceinline__ void dma16_s(uint32_t voff, uint64_t sbase, uint32_t lds) {
-    uint32_t keep;
-    if constexpr (NT)
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %3\n\t"
-            "s_nop 4\n\t"
-            "global_load_lds_dwordx4 %1, %2 nt\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(voff), "s"(sbase), "s"(lds)
-            : "memory");
-    else
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %3\n\t"
-            "s_nop 4\n\t"
-            "global_load_lds_dwordx4 %1, %2\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(voff), "s"(sbase), "s"(lds)
-            : "memory");
-}
-
 // DMA of tile `tile`'s bytes [tile*TILE - HALO, tile*TILE + TILE) into the
 // wave's LDS landing buffer (BUF = HALO + TILE bytes).
 template <int BUF, int TILE, bool NT>

@@ -43,4 +43,31 @@ __device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds) {
             : "memory");
 }
 
+// 16 B per lane from a wave-uniform SGPR base + per-lane VGPR offset into LDS.
+// NT: non-temporal policy (the bytes are read exactly once).
+template <bool NT>
+__device__ __forceinline__ void dma16_s(uint32_t voff, uint64_t sbase, uint32_t lds) {
+    uint32_t keep;
+    if constexpr (NT)
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %3\n\t"
+            "s_nop 4\n\t"
+            "global_load_lds_dwordx4 %1, %2 nt\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(sbase), "s"(lds)
+            : "memory");
+    else
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %3\n\t"
+            "s_nop 4\n\t"
+            "global_load_lds_dwordx4 %1, %2\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(sbase), "s"(lds)
+            : "memory");
+}
+
 }  // namespace cdc
