@@ -1147,6 +1147,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     pm = __ballot(cand && x == (uint32_t)lane);
                 }
                 const bool on = (pm >> lane) & 1ull;
+                Off wup = 0;                                        // the previous lane's candidate
                 if (pm) {
                     const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
                     const int64_t capv = (int64_t)CAP, maxv = (int64_t)MAX;
@@ -1159,7 +1160,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     // (periodic data): a_m falls with m, so the prefix minimum is a_m
                     // itself and R_{m-1} follows from the previous lane's candidate --
                     // one shuffle instead of the 6-step scan and two more shuffles
-                    const Off wup = (Off)__shfl_up((int)wr, 1);
+                    wup = (Off)__shfl_up((int)wr, 1);
                     const bool mono = chain_contig &&
                                       __ballot(on && below && (int64_t)wr - (int64_t)wup >= capv) == 0ull;
                     if (mono) {
@@ -1217,7 +1218,8 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     }
                     const uint64_t below = (lane ? (~0ull >> (64 - lane)) : 0ull) & mk;
                     const uint32_t pl = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
-                    const Off pw = (Off)__shfl((int)wr, (int)pl);
+                    // a consecutive chain's previous cut lane is the previous lane
+                    const Off pw = chain_contig ? wup : (Off)__shfl((int)wr, (int)pl);
                     if ((mk >> lane) & 1ull) {
                         const Off st = below ? pw + 1 : s0;
                         const uint64_t idx = (uint64_t)n0 + (uint64_t)__builtin_popcountll(below);
