@@ -636,6 +636,18 @@ def main(argv=None):
         ch.set_timing(False)
         hcuts = ch.fetch(hashed=True)
         steph = dth / max(args.steps, 1)
+        hpipe = None
+        if depth > 1:                             # the same K hashed steps, `depth` batches in flight
+            for h, b in slots[1:]:
+                h.launch(b.ptr, hashed=True)
+                h.fetch(hashed=True)
+            run_steps(depth, max(args.warmup, depth), hashed=True)
+            d.barrier()
+            t0 = time.perf_counter()
+            run_steps(depth, args.steps, hashed=True)
+            dthp = d.reduce(time.perf_counter() - t0, "max")
+            d.barrier()
+            hpipe = round(total_bytes / (dthp / max(args.steps, 1)) / 2**30, 3)
         hash_ms = hms[3] / max(hn, 1)
         htr = load_traffic(args.workload, span, engine_info["run_bytes"], kernel="cdc::b3_leaf_kernel")
         hashed = {
@@ -645,6 +657,7 @@ def main(argv=None):
             "hash_rate_gbs": round(span / (hash_ms / 1e3) / 1e9, 1) if hash_ms > 0 else None,
             "cuts_agree_with_headline": all(np.array_equal(a[f], x[f]) for a, x in zip(hcuts, cuts)
                                             for f in ("offset", "len", "file")),
+            "pipelined_value": hpipe,
             "leaf_traffic_over_algorithmic": (round(htr["hbm_bytes_per_launch"] / span, 4) if htr else None),
             "leaf_traffic_source": (htr.get("source") if htr else None),
             "sample_check": "cpu_baseline.gpu_hashes_match_sample (rank 0, N=1)",
