@@ -185,7 +185,8 @@ int32_t syncr_ingest_open(int32_t device, const syncr_cdc_params *p, uint64_t ba
  * online form of LPT by size; no cross-device traffic).  Callbacks still arrive
  * in submission order, on the thread that called submit / flush.  Every
  * syncr_ingest_* call takes the returned handle; syncr_ingest_open is the
- * one-device case (no worker thread). */
+ * one-device case (no worker thread).  The copy_threads threads form one pool
+ * that the sub-pipelines take turns on. */
 int32_t syncr_ingest_open_multi(const int32_t *devices, uint32_t ndevices, const syncr_cdc_params *p,
                                 uint64_t batch_bytes, uint32_t depth, uint32_t copy_threads,
                                 syncr_ingest_cb cb, void *ctx, syncr_ingest **out);

@@ -61,12 +61,14 @@ class Pool {
         cv_.notify_all();
         for (auto &t : th_) t.join();
     }
-    // run fn(0..n-1) on the pool plus the calling thread; returns when all done
+    // run fn(0..n-1) on the pool plus the calling thread; returns when all done.
+    // Callers on several threads (sub-pipelines sharing the pool) take turns.
     void parallel(unsigned n, const std::function<void(unsigned)> &fn) {
         if (n <= 1 || th_.empty()) {
             for (unsigned i = 0; i < n; i++) fn(i);
             return;
         }
+        std::lock_guard<std::mutex> job(job_mu_);
         std::unique_lock<std::mutex> g(mu_);
         fn_ = &fn;
         next_ = 0;
@@ -110,6 +112,7 @@ class Pool {
         }
     }
     std::vector<std::thread> th_;
+    std::mutex job_mu_;                       // one parallel() job at a time
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     const std::function<void(unsigned)> *fn_ = nullptr;
@@ -154,6 +157,7 @@ struct Pipe {
     deliver_fn deliver = nullptr;
     void *owner = nullptr;
     Pool *pool = nullptr;
+    bool own_pool = true;            // false: the multi-device pipeline's shared pool
     bool reserved = false;           // reserve() outstanding on slots[cur]
     uint64_t reserved_len = 0;
     std::atomic<uint64_t> stats[4] = {{0}, {0}, {0}, {0}};   // files, bytes, batches, chunks
@@ -321,12 +325,12 @@ void pipe_close(Pipe *g) {
         }
         free_slot_buffers(g, s);
     }
-    delete g->pool;
+    if (g->own_pool) delete g->pool;
     delete g;
 }
 
 int32_t pipe_open(int32_t device, const syncr_cdc_params &p, uint64_t batch_bytes, uint32_t depth,
-                  uint32_t copy_threads, deliver_fn deliver, void *owner, Pipe **out) {
+                  uint32_t copy_threads, Pool *shared, deliver_fn deliver, void *owner, Pipe **out) {
     Pipe *g = new (std::nothrow) Pipe();
     if (!g) return SYNCR_CDC_ENOMEM;
     g->device = device;
@@ -344,7 +348,12 @@ int32_t pipe_open(int32_t device, const syncr_cdc_params &p, uint64_t batch_byte
                 return rc;
             }
         }
-        if (copy_threads > 1) g->pool = new Pool(std::min<uint32_t>(copy_threads, 64) - 1);
+        if (shared) {
+            g->pool = shared;
+            g->own_pool = false;
+        } else if (copy_threads > 1) {
+            g->pool = new Pool(std::min<uint32_t>(copy_threads, 64) - 1);
+        }
     } catch (...) {
         pipe_close(g);
         return SYNCR_CDC_ENOMEM;
@@ -538,6 +547,7 @@ struct syncr_ingest {
     uint32_t reserve_dev = 0;
     int32_t error = 0;
     syncr_cache *cache = nullptr;
+    Pool *pool = nullptr;             // multi: the copy pool the sub-pipelines share
 };
 
 namespace {
@@ -668,9 +678,11 @@ int32_t syncr_ingest_open_multi(const int32_t *devices, uint32_t ndevices, const
     g->ctx = ctx;
     g->multi = ndevices > 1;
     try {
+        // one copy pool for the whole pipeline: the sub-pipelines take turns on it
+        if (g->multi && copy_threads > 1) g->pool = new Pool(std::min<uint32_t>(copy_threads, 64) - 1);
         for (uint32_t k = 0; k < ndevices; k++) {
             Pipe *pp = nullptr;
-            const int32_t rc = pipe_open(devices[k], prm, batch_bytes, depth, copy_threads,
+            const int32_t rc = pipe_open(devices[k], prm, batch_bytes, depth, copy_threads, g->pool,
                                          g->multi ? deliver_multi : deliver_single, g, &pp);
             if (rc) {
                 syncr_ingest_close(g);
@@ -842,6 +854,7 @@ void syncr_ingest_close(syncr_ingest *g) {
     if (!g) return;
     close_multi(g);
     for (Pipe *p : g->pipes) pipe_close(p);
+    delete g->pool;
     delete g->assign;
     delete g;
 }
