@@ -120,33 +120,51 @@ struct DirtySlot {             // 80 bytes
     uint32_t flags;            // bit0: check A, bit1: check B
 };
 
+// Closed-form state before run position 16q (the window is the 64 bytes
+// A/B words q..q+15; weights 64..1, oldest first): the packed s1 sums and
+// the packed mask-test values tv.
+template <int RUN>
+__device__ __forceinline__ void window_state(const uint32_t (&A)[(HALO + RUN) / 4],
+                                             const uint32_t (&B)[(HALO + RUN) / 4], const KParams &P,
+                                             int q, uint32_t &S, u16x2 &Tv) {
+    uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const uint32_t w = 0x3D3E3F40u - 0x04040404u * (uint32_t)m;
+        SA = __builtin_amdgcn_udot4(A[q + m], 0x01010101u, SA, false);
+        WA = __builtin_amdgcn_udot4(A[q + m], w, WA, false);
+        SB = __builtin_amdgcn_udot4(B[q + m], 0x01010101u, SB, false);
+        WB = __builtin_amdgcn_udot4(B[q + m], w, WB, false);
+    }
+    S = SA | (SB << 16);
+    const uint32_t tA = ((124993u + WA) * P.k) & 0xffffu;
+    const uint32_t tB = ((124993u + WB) * P.k) & 0xffffu;
+    Tv = as_u16x2(tA | (tB << 16));
+}
+
 // ROLL2: the same values with single-op dependency chains per byte pair:
 // V = S - 64 d (one v_pk_mad_u16 off the T chain), then T += k V (one
 // v_pk_mad_u16 on it), instead of two dependent v_pk_mad_u16 on T.
+// The 16-byte group checks are two compares into lane masks each; the run
+// has no branch until its end, where a wave with any dirty group recomputes
+// each dirty group's entry state in closed form (window_state, from the
+// bytes still in registers) and hands it to the side slots.  (A branch per
+// group cost 4 more VALU per group to materialise the flags and split the
+// run into basic blocks the scheduler could not interleave across.)
 template <int RUN, bool ROLL2 = false>
 __device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
                                           const uint32_t (&B)[(HALO + RUN) / 4], const KParams &P,
                                           int lane, bool recA, bool recB, uint32_t *dcount,
                                           DirtySlot *dslots) {
-    // closed-form window sums at run start - 1 (weights 64..1, oldest first)
-    uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        const uint32_t w = 0x3D3E3F40u - 0x04040404u * (uint32_t)m;
-        SA = __builtin_amdgcn_udot4(A[m], 0x01010101u, SA, false);
-        WA = __builtin_amdgcn_udot4(A[m], w, WA, false);
-        SB = __builtin_amdgcn_udot4(B[m], 0x01010101u, SB, false);
-        WB = __builtin_amdgcn_udot4(B[m], w, WB, false);
-    }
-    uint32_t S = SA | (SB << 16);
-    const uint32_t tA = ((124993u + WA) * P.k) & 0xffffu;
-    const uint32_t tB = ((124993u + WB) * P.k) & 0xffffu;
-    u16x2 Tv = as_u16x2(tA | (tB << 16));
+    constexpr int NG = RUN / 16;
+    uint32_t S;
+    u16x2 Tv;
+    window_state<RUN>(A, B, P, 0, S, Tv);
     const uint32_t want = (recA ? 1u : 0u) | (recB ? 2u : 0u);
+    bool zg[NG];
+    bool anyz = false;
 #pragma unroll
-    for (int g = 0; g < RUN / 16; ++g) {
-        const uint32_t S0 = S;
-        const u16x2 T0 = Tv;
+    for (int g = 0; g < NG; ++g) {
         u16x2 acc = as_u16x2(0xffffffffu);
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) {
@@ -163,8 +181,61 @@ __device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
             acc = __builtin_elementwise_min(acc, Tv);
         }
         const uint32_t a = as_u32(acc);
+        zg[g] = (recA && (a & 0xffffu) == 0u) || (recB && (a >> 16) == 0u);
+        anyz = anyz || zg[g];
+    }
+    if (__builtin_expect(__ballot(anyz) != 0ull, 0)) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            if (zg[g]) {
+                const uint32_t idx = atomicAdd(dcount, 1u);
+                if (idx < (uint32_t)DIRTYCAP) {
+                    uint32_t S0;
+                    u16x2 T0;
+                    window_state<RUN>(A, B, P, 4 * g, S0, T0);
+                    DirtySlot &ds = dslots[idx];
+                    ds.xa = make_uint4(A[16 + 4 * g], A[17 + 4 * g], A[18 + 4 * g], A[19 + 4 * g]);
+                    ds.da = make_uint4(A[4 * g], A[1 + 4 * g], A[2 + 4 * g], A[3 + 4 * g]);
+                    ds.xb = make_uint4(B[16 + 4 * g], B[17 + 4 * g], B[18 + 4 * g], B[19 + 4 * g]);
+                    ds.db = make_uint4(B[4 * g], B[1 + 4 * g], B[2 + 4 * g], B[3 + 4 * g]);
+                    ds.S0 = S0;
+                    ds.T0 = as_u32(T0);
+                    ds.rel = (uint32_t)(lane * RUN + g * 16);
+                    ds.flags = want;         // the re-walk tests both halves exactly
+                }
+            }
+        }
+    }
+}
+
+#ifdef SYNCR_CDC_DEV
+// The round-2 roll (development A/B only, SYNCR_CDC_ABLATE=10): a branch per
+// 16-byte group that materialises the group's flags and captures its entry
+// state in registers.
+template <int RUN>
+__device__ __forceinline__ void roll_branchy(const uint32_t (&A)[(HALO + RUN) / 4],
+                                             const uint32_t (&B)[(HALO + RUN) / 4], const KParams &P,
+                                             int lane, uint32_t *dcount, DirtySlot *dslots) {
+    uint32_t S;
+    u16x2 Tv;
+    window_state<RUN>(A, B, P, 0, S, Tv);
+#pragma unroll
+    for (int g = 0; g < RUN / 16; ++g) {
+        const uint32_t S0 = S;
+        const u16x2 T0 = Tv;
+        u16x2 acc = as_u16x2(0xffffffffu);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const int i = g * 16 + jj;
+            const uint32_t x = pair_at<RUN>(A, B, HALO + i), d = pair_at<RUN>(A, B, i);
+            S = S + x - d;
+            const u16x2 V = pk_mad(d, 0xFFC0FFC0u, as_u16x2(S));
+            Tv = pk_mad(as_u32(V), P.kk, Tv);
+            acc = __builtin_elementwise_min(acc, Tv);
+        }
+        const uint32_t a = as_u32(acc);
         const uint32_t zf = (((a & 0xffffu) == 0u) ? 1u : 0u) | (((a >> 16) == 0u) ? 2u : 0u);
-        const bool z = (zf & want) != 0u;
+        const bool z = zf != 0u;
         if (__builtin_expect(__ballot(z) != 0ull, 0)) {
             if (z) {
                 const uint32_t idx = atomicAdd(dcount, 1u);
@@ -177,12 +248,13 @@ __device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
                     ds.S0 = S0;
                     ds.T0 = as_u32(T0);
                     ds.rel = (uint32_t)(lane * RUN + g * 16);
-                    ds.flags = zf & want;
+                    ds.flags = zf;
                 }
             }
         }
     }
 }
+#endif
 
 // Exact re-walk of the dirty groups (one lane per slot, bytes from LDS).
 template <int RUN>
@@ -312,7 +384,8 @@ __host__ __device__ constexpr bool scan_dynamic(uint32_t ntiles, uint32_t grid) 
     return (uint64_t)ntiles >= (uint64_t)grid * SCAN_DYN_MIN_TILES_PER_WAVE;
 }
 
-// MODE bit 5: ask for 3 waves per SIMD (VGPRs <= 168; development A/B only)
+// MODE bit 5: ask for 3 waves per SIMD (VGPRs <= 168; development A/B only).
+// MODE bit 6: the round-2 roll with a branch per group (development A/B only)
 template <int RUN, int MODE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((MODE & 32) ? 3 : 1)))
 void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
@@ -390,6 +463,9 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             continue;
         }
         const int64_t lim_rel = span - t0;                           // positions >= span are not bytes
+#ifdef SYNCR_CDC_DEV
+        if constexpr ((MODE & 64) != 0) roll_branchy<RUN>(A, B, P, lane, dcount, dslots); else
+#endif
         roll_fast<RUN, (MODE & 16) != 0>(A, B, P, lane, true, true, dcount, dslots);
         if constexpr ((MODE & 3) == 2) continue;                          // diagnostics: rolling only
         __builtin_amdgcn_wave_barrier();
@@ -1523,6 +1599,8 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 6u)                                         // timing only: roll, no DMA
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 7u)                                         // A/B: product + 3 waves per SIMD hint
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, d, p,
                            t);
