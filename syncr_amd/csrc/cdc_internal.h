@@ -44,6 +44,16 @@ __host__ __device__ constexpr int buf_bytes(int run) { return HALO + run * RUNS;
 // LDS per wave: one tile landing buffer + 16 dirty-group slots (80 B) +
 // candidate list + counters
 __host__ __device__ constexpr int lds_wave_bytes(int run) { return buf_bytes(run) + 16 * 80 + LISTCAP * 4 + 16; }
+// Three-waves-per-SIMD scan (cdc_scan3_kernel, RUN = W3_RUN): the landing
+// buffer + DIRTYCAP3 dirty-group positions (their bytes are re-read from HBM,
+// not kept in LDS) + candidate list + counters.  12 waves x 12 880 B <= 160 KiB.
+constexpr int W3_RUN = 96;
+constexpr int DIRTYCAP3 = 64;
+__host__ __device__ constexpr bool run_is_w3(int run) { return run == W3_RUN; }
+__host__ __device__ constexpr int lds3_wave_bytes(int run) { return buf_bytes(run) + DIRTYCAP3 * 4 + LISTCAP * 4 + 16; }
+__host__ __device__ constexpr int scan_lds_for_run(int run) {
+    return run_is_w3(run) ? lds3_wave_bytes(run) : lds_wave_bytes(run);
+}
 
 // ctr[] words (zeroed by the per-launch memset)
 enum { CTR_DENSE = 0, CTR_FLAGS = 1, CTR_CANDS_LO = 2, CTR_CANDS_HI = 3 };

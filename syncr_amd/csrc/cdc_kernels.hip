@@ -479,6 +479,232 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Three-waves-per-SIMD scan (cdc_scan3_kernel, RUN = W3_RUN = 96).
+//
+// At two waves per SIMD a wave issues a VALU instruction at most every ~8
+// cycles, so the roll's 2 VOP2 + 4 VOP3(P) per byte pair cost 3.85 / 6.05
+// SIMD-cycles each; at three waves they cost 2.72 / 4.70
+// (profiles/r02_ubench_valu.log): 32 -> 24 SIMD-cycles per 128 bytes, which
+// keeps the scan above the HBM read ceiling even at the 1.7 GHz the part
+// drops to when a scan load starts.  Three waves need
+// <= 168 VGPRs and <= 13.6 KB of LDS per wave:
+//   - a 12 KB tile (128 runs x 96 B): 12 waves x 12.35 KB keep the same
+//     148 KB per CU of tile bytes in flight as 8 waves x 18.5 KB;
+//   - dirty 16-byte groups keep no bytes in LDS or registers: the roll only
+//     records their positions; after the roll each dirty slot's lane re-reads
+//     the group's 80 bytes of both runs from HBM (the same clamped 16-byte
+//     pieces the tile DMA read) behind the next tile's DMA, and the next
+//     iteration's landing wait covers them, so the exact re-walk (closed-form
+//     entry state + 16 exact steps) and the tile's publication happen one
+//     iteration late without draining anything.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void window_state_n(const uint32_t (&A)[N], const uint32_t (&B)[N], const KParams &P,
+                                               uint32_t &S, u16x2 &Tv) {
+    uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const uint32_t w = 0x3D3E3F40u - 0x04040404u * (uint32_t)m;
+        SA = __builtin_amdgcn_udot4(A[m], 0x01010101u, SA, false);
+        WA = __builtin_amdgcn_udot4(A[m], w, WA, false);
+        SB = __builtin_amdgcn_udot4(B[m], 0x01010101u, SB, false);
+        WB = __builtin_amdgcn_udot4(B[m], w, WB, false);
+    }
+    S = SA | (SB << 16);
+    const uint32_t tA = ((124993u + WA) * P.k) & 0xffffu;
+    const uint32_t tB = ((124993u + WB) * P.k) & 0xffffu;
+    Tv = as_u16x2(tA | (tB << 16));
+}
+
+// The ROLL2 roll of one tile-lane; zg[g] = the 16-byte group g of run A or B
+// has a zero mask-test value (a superset of its edges).
+template <int RUN>
+__device__ __forceinline__ void roll_flags(const uint32_t (&A)[(HALO + RUN) / 4],
+                                           const uint32_t (&B)[(HALO + RUN) / 4], const KParams &P,
+                                           bool (&zg)[RUN / 16]) {
+    uint32_t S;
+    u16x2 Tv;
+    window_state<RUN>(A, B, P, 0, S, Tv);
+#pragma unroll
+    for (int g = 0; g < RUN / 16; ++g) {
+        u16x2 acc = as_u16x2(0xffffffffu);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const int i = g * 16 + jj;
+            const uint32_t x = pair_at<RUN>(A, B, HALO + i), d = pair_at<RUN>(A, B, i);
+            S = S + x - d;
+            const u16x2 V = pk_mad(d, 0xFFC0FFC0u, as_u16x2(S));   // S - 64 d (mod 2^16 per half)
+            Tv = pk_mad(as_u32(V), P.kk, Tv);                       // T += k (S - 64 d)
+            acc = __builtin_elementwise_min(acc, Tv);
+        }
+        const uint32_t a = as_u32(acc);
+        zg[g] = (a & 0xffffu) == 0u || (a >> 16) == 0u;
+    }
+}
+
+// One 16-byte piece of the batch at g, clamped as issue_buf clamps an edge
+// tile's pieces (so the re-walk sees exactly the bytes the roll saw).
+__device__ __forceinline__ uint4 reread_piece(const uint8_t *data, int64_t g, int64_t last) {
+    g = g < 0 ? 0 : (g > last ? last : g);
+    return *(const uint4 *)(data + g);
+}
+
+// Exact re-walk of one dirty group from its re-read bytes: ra / rb = bytes
+// [rel - 64, rel + 16) of runs A and B (tile-relative rel, rel + 64 RUN).
+template <int RUN>
+__device__ __forceinline__ void rewalk_reread(const KParams &P, uint32_t relA, const uint4 (&ra)[5],
+                                              const uint4 (&rb)[5], int64_t lim_rel, uint32_t *wcount,
+                                              uint32_t *wlist) {
+    uint32_t A[20], B[20];
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+        A[4 * m] = ra[m].x; A[4 * m + 1] = ra[m].y; A[4 * m + 2] = ra[m].z; A[4 * m + 3] = ra[m].w;
+        B[4 * m] = rb[m].x; B[4 * m + 1] = rb[m].y; B[4 * m + 2] = rb[m].z; B[4 * m + 3] = rb[m].w;
+    }
+    uint32_t s;
+    u16x2 t;
+    window_state_n<20>(A, B, P, s, t);
+    const u16x2 kk = as_u16x2(P.kk), km = as_u16x2(P.kmv);
+    const uint32_t relB = relA + 64u * RUN;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+        const uint32_t sel = 0x0C040C00u + (uint32_t)(jj & 3) * 0x00010001u;
+        const uint32_t x = __builtin_amdgcn_perm(B[16 + (jj >> 2)], A[16 + (jj >> 2)], sel);
+        const uint32_t d = __builtin_amdgcn_perm(B[jj >> 2], A[jj >> 2], sel);
+        s = s + x - d;
+        t = as_u16x2(s) * kk + t;
+        t = as_u16x2(d) * km + t;
+        if (t.x == 0 && ((1984u + (s & 0xffffu)) & P.m1) == P.m1 && (int64_t)(relA + jj) < lim_rel)
+            record(wcount, wlist, relA + jj);
+        if (t.y == 0 && ((1984u + (s >> 16)) & P.m1) == P.m1 && (int64_t)(relB + jj) < lim_rel)
+            record(wcount, wlist, relB + jj);
+    }
+}
+
+// MODE bit 2: non-temporal tile loads; bit 3: dynamic tile groups; bit 1
+// (development library only): no tile DMA after the first (roll timing).
+template <int RUN, int MODE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
+void cdc_scan3_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int TILE = tile_bytes(RUN);
+    constexpr int NQ = (HALO + RUN) / 16;
+    constexpr int NG = RUN / 16;
+    constexpr bool NT = (MODE & 4) != 0;
+    constexpr bool DYN = (MODE & 8) != 0;
+    const int lane = threadIdx.x;
+    uint8_t *wl = smem;
+    uint32_t *drel = (uint32_t *)(smem + buf_bytes(RUN));
+    uint32_t *wlist = drel + DIRTYCAP3;
+    uint32_t *wcount = wlist + LISTCAP;
+    uint32_t *dcount = wcount + 1;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
+    const uint32_t stride = gridDim.x;
+    // dynamic groups as in cdc_scan_kernel; 12 tiles of 12 KB per grab keep
+    // the counter below its ~69 M grabs/s
+    constexpr uint32_t DG = 12;
+    auto gbase = [&](uint32_t k) { return (k / stride) * stride * DG + (k % stride); };
+    uint32_t tile = blockIdx.x;
+    if (tile >= T.ntiles) return;
+    const int64_t span = (int64_t)T.span;
+    const int64_t last = (int64_t)((T.span - 1) & ~15ull);
+    issue_tile<RUN, NT>(data, T.span, tile, lds0, lane);
+    if (lane == 0) { *wcount = 0u; *dcount = 0u; }
+    uint32_t gj = 0, pend = 0;
+    // the previous tile's dirty groups: count, tile, this lane's slot and bytes
+    uint32_t pnd = 0, ptile = 0, prel = 0;
+    uint4 ra[5], rb[5];
+    for (uint32_t next; tile < T.ntiles; tile = next) {
+        bool grabbed = false;
+        uint32_t gjn = 0;
+        if constexpr (DYN) {
+            if (gj + 1 < DG && tile + stride < T.ntiles) {
+                next = tile + stride;
+                gjn = gj + 1;
+            } else {
+                if (gj == 0) {
+                    if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
+                    grabbed = true;
+                }
+                wait_vmcnt<0>();                                     // the grab
+                next = gbase(stride + (uint32_t)__builtin_amdgcn_readfirstlane(pend));
+                gjn = 0;
+            }
+        } else {
+            next = tile + stride;
+        }
+        const int64_t t0 = (int64_t)tile * TILE;
+        wait_vmcnt<0>();                         // this tile has landed, and the previous tile's re-reads
+        if (pnd) {
+            const int64_t pt0 = (int64_t)ptile * TILE;
+            if ((uint32_t)lane < pnd) rewalk_reread<RUN>(P, prel, ra, rb, span - pt0, wcount, wlist);
+            publish_tile(data, P, T, ptile, pt0, wlist, wcount, lane, false);
+            if (lane == 0) *wcount = 0u;
+        }
+        uint32_t A[NQ * 4], B[NQ * 4];
+        {
+            const uint4 *la = (const uint4 *)(wl + lane * RUN);          // = run start - 64
+            const uint4 *lb = (const uint4 *)(wl + (lane + 64) * RUN);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const uint4 a = la[q], b = lb[q];
+                A[4 * q + 0] = a.x; A[4 * q + 1] = a.y; A[4 * q + 2] = a.z; A[4 * q + 3] = a.w;
+                B[4 * q + 0] = b.x; B[4 * q + 1] = b.y; B[4 * q + 2] = b.z; B[4 * q + 3] = b.w;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");           // runs are in registers
+        if (next < T.ntiles && (MODE & 2) == 0) issue_tile<RUN, NT>(data, T.span, next, lds0, lane);
+        if constexpr (DYN) {
+            if (gj == 0 && !grabbed && lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
+            gj = gjn;
+        }
+        bool zg[NG];
+        roll_flags<RUN>(A, B, P, zg);
+        bool anyz = false;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) anyz = anyz || zg[g];
+        pnd = 0;
+        if (__builtin_expect(__ballot(anyz) != 0ull, 0)) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                if (zg[g]) {
+                    const uint32_t idx = atomicAdd(dcount, 1u);
+                    if (idx < (uint32_t)DIRTYCAP3) drel[idx] = (uint32_t)(lane * RUN + g * 16);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            const uint32_t nd = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)dcount, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WAVEFRONT));
+            if ((uint32_t)lane < nd && (uint32_t)lane < (uint32_t)DIRTYCAP3) prel = drel[lane];
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) *dcount = 0u;
+            if (nd > (uint32_t)DIRTYCAP3) {
+                publish_tile(data, P, T, tile, t0, wlist, wcount, lane, true);    // exact dense pass
+            } else {
+                pnd = nd;
+                ptile = tile;
+                if ((uint32_t)lane < nd) {
+                    const int64_t ga = t0 + (int64_t)prel - HALO, gb = ga + 64 * RUN;
+#pragma unroll
+                    for (int m = 0; m < 5; ++m) {
+                        ra[m] = reread_piece(data, ga + 16 * m, last);
+                        rb[m] = reread_piece(data, gb + 16 * m, last);
+                    }
+                }
+            }
+        }
+    }
+    if (pnd) {
+        wait_vmcnt<0>();
+        const int64_t pt0 = (int64_t)ptile * TILE;
+        if ((uint32_t)lane < pnd) rewalk_reread<RUN>(P, prel, ra, rb, span - pt0, wcount, wlist);
+        publish_tile(data, P, T, ptile, pt0, wlist, wcount, lane, false);
+    }
+}
+
 #ifdef SYNCR_CDC_DEV
 // ---------------------------------------------------------------------------
 // MFMA scan (development library only: north_star asks for integer VALU work,
@@ -1540,7 +1766,9 @@ hipError_t launch_read_probe(const uint8_t *d, uint64_t bytes, bool nt, uint32_t
 // selected by environment variables that the product never reads.
 // ---------------------------------------------------------------------------
 #ifdef SYNCR_CDC_DEV
-static bool valu_run_ok(int run) { return run == 48 || run == 80 || run == 112 || run == 144 || run == 176; }
+static bool valu_run_ok(int run) {
+    return run == 48 || run == 80 || run == W3_RUN || run == 112 || run == 144 || run == 176;
+}
 static bool mfma_nb_ok(int nb) { return nb == 4 || nb == 6 || nb == 8 || nb == 10 || nb == 12; }
 
 bool scan_supported(ScanGeom g) {
@@ -1548,7 +1776,7 @@ bool scan_supported(ScanGeom g) {
 }
 int scan_tile_bytes(ScanGeom g) { return g.kind == SCAN_VALU ? tile_bytes(g.param) : mf_tile_bytes(g.param); }
 int scan_lds_bytes(ScanGeom g) {
-    return g.kind == SCAN_VALU ? lds_wave_bytes(g.param) : mf_lds_bytes(g.param, (g.var & MFV_SINGLE) ? 1 : 2);
+    return g.kind == SCAN_VALU ? scan_lds_for_run(g.param) : mf_lds_bytes(g.param, (g.var & MFV_SINGLE) ? 1 : 2);
 }
 
 template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>; }
@@ -1575,6 +1803,7 @@ static const void *scan_kernel_ptr(ScanGeom g) {
     switch (g.param) {
         case 48: return scan_fn<48>();
         case 80: return scan_fn<80>();
+        case W3_RUN: return (const void *)&cdc_scan3_kernel<W3_RUN, 4 | 8>;
         case 112: return scan_fn<112>();
         case 144: return scan_fn<144>();
         case 176: return scan_fn<176>();
@@ -1610,6 +1839,16 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE & ~4>), dim3(grid), dim3(64), lds, s, d, p, t);
+}
+
+static void launch_scan3(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
+    const size_t lds = lds3_wave_bytes(W3_RUN);
+    if (p.ablate == 6u)                                              // timing only: roll, no DMA
+        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8 | 2>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (scan_dynamic(t.ntiles, grid))
+        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else
+        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4>), dim3(grid), dim3(64), lds, s, d, p, t);
 }
 
 template <int NB, int V>
@@ -1660,6 +1899,7 @@ hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParam
     switch (g.param) {
         case 48: launch_scan_t<48>(grid, d, p, t, s); break;
         case 80: launch_scan_t<80>(grid, d, p, t, s); break;
+        case W3_RUN: launch_scan3(grid, d, p, t, s); break;
         case 112: launch_scan_t<112>(grid, d, p, t, s); break;
         case 144: launch_scan_t<144>(grid, d, p, t, s); break;
         case 176: launch_scan_t<176>(grid, d, p, t, s); break;
