@@ -46,6 +46,7 @@ extern "C" {
  * alternative resolve (same cuts; for cross-checks only): */
 #define SYNCR_CDC_FLAG_RESOLVE_LANE 1u    /* one lane per file instead of one wave */
 #define SYNCR_CDC_FLAG_RESOLVE_NOBURST 2u /* wave resolve without the chained-hop burst */
+#define SYNCR_CDC_FLAG_RESOLVE_NOSPLIT 4u /* wave resolve without split walks of long files */
 typedef struct syncr_cdc_params {
     uint32_t chunk_bits; /* CHUNK_BITS, 1..31 (default 20; reference validates 8..32) */
     uint32_t flags;      /* 0, or SYNCR_CDC_FLAG_* (other bits: SYNCR_CDC_EINVAL)     */

@@ -65,6 +65,7 @@ E_BUSY = -16
 E_INVAL = -22
 FLAG_RESOLVE_LANE = 1       # exact alternative resolves (include/syncr_cdc.h SYNCR_CDC_FLAG_*)
 FLAG_RESOLVE_NOBURST = 2
+FLAG_RESOLVE_NOSPLIT = 4
 FMT_LIST_LINES = 1      # LIST reply "C" lines (src/protocol/v3_server.rs:146-182)
 FMT_HASHCHUNKS = 2      # profile FileData "ch" array (src/types.rs:117-129)
 

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <mutex>
@@ -17,6 +18,7 @@
 
 #include "../../include/syncr_cdc.h"
 #include "cdc_internal.h"
+#include <cstdio>
 
 using namespace cdc;
 
@@ -83,6 +85,14 @@ struct syncr_cdc {
     // read-boundary grid (Tables::gpos...): production semantics only
     uint32_t ngrid = 0;
     DevBuf gpos, gend, gfix, gbase;
+    // split walks of long files (Tables::segs...): files order[0 .. n_elig) may split
+    uint32_t n_elig = 0, seg_cap = 0;
+    DevBuf segs, seg_cuts;
+    // split only when a walk can be long: the last launch fetched held >= 2 x
+    // SPLIT_SEGC candidates (random data: ~1 per MiB, so never; periodic or
+    // low-entropy data: thousands per MiB).  Off until a fetch has seen that,
+    // so the common case launches no split workers at all.
+    bool split_hint = false;
 
     // launch
     bool launched = false;
@@ -119,7 +129,9 @@ int32_t hip_err(hipError_t e) {
 int32_t validate_params(const syncr_cdc_params *p) {
     if (!p) return SYNCR_CDC_EINVAL;
     if (p->chunk_bits < 1 || p->chunk_bits > 31) return SYNCR_CDC_EINVAL;
-    if (p->flags & ~(uint32_t)(SYNCR_CDC_FLAG_RESOLVE_LANE | SYNCR_CDC_FLAG_RESOLVE_NOBURST)) return SYNCR_CDC_EINVAL;
+    if (p->flags & ~(uint32_t)(SYNCR_CDC_FLAG_RESOLVE_LANE | SYNCR_CDC_FLAG_RESOLVE_NOBURST |
+                               SYNCR_CDC_FLAG_RESOLVE_NOSPLIT))
+        return SYNCR_CDC_EINVAL;
     if (p->max_chunk < 1 || p->max_chunk > 0xffffffffull) return SYNCR_CDC_EINVAL;
     return SYNCR_CDC_OK;
 }
@@ -140,6 +152,7 @@ KParams make_kparams(const syncr_cdc_params &p) {
     // exact alternative resolves, for cross-checks (include/syncr_cdc.h)
     k.resolve_lane = (p.flags & SYNCR_CDC_FLAG_RESOLVE_LANE) ? 1u : 0u;
     k.resolve_noburst = (p.flags & SYNCR_CDC_FLAG_RESOLVE_NOBURST) ? 1u : 0u;
+    k.resolve_nosplit = (p.flags & SYNCR_CDC_FLAG_RESOLVE_NOSPLIT) ? 1u : 0u;
     return k;
 }
 
@@ -150,6 +163,9 @@ uint32_t default_cut_cap(uint64_t len, uint32_t bits) {
     uint64_t c = (len >> sh) + 8;
     return (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
 }
+
+// the per-launch zeroed block: ctr[4] | nonempty[nwords] (u64) | super_cnt[nwords] (u32) | split[SPL_WORDS]
+size_t split_ctr_offset(const syncr_cdc *h) { return (16 + (size_t)h->nwords * 12 + 15) & ~size_t(15); }
 
 Tables make_tables(syncr_cdc *h) {
     Tables t{};
@@ -184,6 +200,17 @@ Tables make_tables(syncr_cdc *h) {
     t.gend = h->gend.as<uint64_t>();
     t.gfix = h->gfix.as<uint8_t>();
     t.gbase = h->gbase.as<uint64_t>();
+    t.n_elig = h->split_hint ? h->n_elig : 0u;
+    t.seg_cap = h->seg_cap;
+    t.segs = h->segs.as<SplitSeg>();
+    t.seg_cuts = h->seg_cuts.as<DevCut>();
+    t.split = reinterpret_cast<uint32_t *>(h->zeroed.as<uint8_t>() + split_ctr_offset(h));
+    // SplitSeg records outlive a launch: a record is ready for this launch only
+    // when its ready word holds this launch's id (records are zeroed when allocated)
+    static std::atomic<uint32_t> epochs{0};
+    uint32_t ep;
+    while ((ep = ++epochs) == 0u) {}
+    t.epoch = ep;
     return t;
 }
 
@@ -258,12 +285,20 @@ int32_t ensure_dense(syncr_cdc *h, uint32_t cap) {
 int32_t ensure_cand(syncr_cdc *h, uint64_t cap) {
     h->cand_cap = cap;
     CHECK_HIP(h->cand.ensure(std::max<uint64_t>(cap, 1) * 8));
+    // split-walk records: a file splits into segments of SPLIT_SEGC of its
+    // candidates, so cand_cap / SPLIT_SEGC records cover every split file
+    h->seg_cap = 0;
+    if (h->n_elig) {
+        const uint64_t segs = std::min<uint64_t>(cap / SPLIT_SEGC + 8, 0xffffffull);
+        CHECK_HIP(h->segs.ensure(segs * sizeof(SplitSeg)));
+        CHECK_HIP(hipMemset(h->segs.p, 0, segs * sizeof(SplitSeg)));     // no ready word from other memory
+        CHECK_HIP(h->seg_cuts.ensure(segs * SPLIT_SCAP * sizeof(DevCut)));
+        h->seg_cap = (uint32_t)segs;
+    }
     return SYNCR_CDC_OK;
 }
 
-size_t zeroed_bytes(const syncr_cdc *h) {
-    return (16 + (size_t)h->nwords * 12 + 15) & ~size_t(15);
-}
+size_t zeroed_bytes(const syncr_cdc *h) { return split_ctr_offset(h) + SPL_WORDS * 4; }
 
 void drain_timing(syncr_cdc *h) {
     for (auto &pt : h->pending) {
@@ -407,6 +442,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *rs = getenv("SYNCR_CDC_RESOLVE")) {
         h->kp.resolve_lane = strcmp(rs, "lane") == 0;
         h->kp.resolve_noburst = strcmp(rs, "noburst") == 0;
+        h->kp.resolve_nosplit = strcmp(rs, "nosplit") == 0;
     }
     if (const char *a = getenv("SYNCR_CDC_SERIAL")) h->serial_scans = atoi(a) != 0;
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
@@ -474,7 +510,8 @@ void syncr_cdc_close(syncr_cdc *h) {
                       &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
                       &h->dense_cnt, &h->dense_bits, &h->super_off, &h->cand, &h->cuts,
                       &h->counts, &h->stage, &h->hctr, &h->items, &h->trees, &h->gcv,
-                      &h->hashes, &h->packed, &h->tpieces, &h->pieces, &h->pcv, &h->gpos, &h->gend, &h->gfix, &h->gbase};
+                      &h->hashes, &h->packed, &h->tpieces, &h->pieces, &h->pcv, &h->gpos, &h->gend, &h->gfix, &h->gbase,
+                      &h->segs, &h->seg_cuts};
     for (DevBuf *b : bufs) b->release();
     (void)hipStreamDestroy(h->stream);
     delete h;
@@ -523,6 +560,8 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         std::iota(order.begin(), order.end(), 0u);
         std::stable_sort(order.begin(), order.end(),
                          [&](uint32_t a, uint32_t b) { return file_len[a] > file_len[b]; });
+        h->n_elig = 0;                  // files that may split their walk (a prefix of `order`)
+        while (h->n_elig < nfiles && file_len[order[h->n_elig]] >= SPLIT_MIN_BYTES) h->n_elig++;
         h->h_cut_cap.resize(nfiles);
         for (uint32_t i = 0; i < nfiles; i++) h->h_cut_cap[i] = default_cut_cap(file_len[i], h->params.chunk_bits);
 
@@ -621,9 +660,24 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
             uint32_t ctr[4];
             CHECK_HIP(hipMemcpy(ctr, h->zeroed.p, 16, hipMemcpyDeviceToHost));
             const uint64_t ncand = (uint64_t)ctr[CTR_CANDS_LO] | ((uint64_t)ctr[CTR_CANDS_HI] << 32);
+            h->split_hint = ncand >= 2ull * SPLIT_SEGC;        // for the next launch (also a re-run below)
             std::vector<uint64_t> counts(h->nfiles);
             if (h->nfiles)
                 CHECK_HIP(hipMemcpy(counts.data(), h->counts.p, h->nfiles * 8ull, hipMemcpyDeviceToHost));
+#ifdef SYNCR_CDC_DEV
+            if (getenv("SYNCR_CDC_DEBUG_FETCH")) {
+                uint32_t sp[SPL_WORDS];
+                CHECK_HIP(hipMemcpy(sp, h->zeroed.as<uint8_t>() + split_ctr_offset(h), sizeof sp, hipMemcpyDeviceToHost));
+                fprintf(stderr, "fetch attempt %d: flags %u ncand %llu dense %u cand_cap %llu dense_cap %u seg_cap %u | "
+                        "pub %u split %u reserved %u head %u done %u | counts",
+                        attempt, ctr[CTR_FLAGS], (unsigned long long)ncand, ctr[CTR_DENSE],
+                        (unsigned long long)h->cand_cap, h->dense_cap, h->seg_cap, sp[0], sp[1], sp[SPL_RESERVED],
+                        sp[SPL_HEAD], sp[SPL_DONE]);
+                for (uint32_t i = 0; i < h->nfiles && i < 8; i++)
+                    fprintf(stderr, " %llu/%u", (unsigned long long)counts[i], h->h_cut_cap[i]);
+                fprintf(stderr, "\n");
+            }
+#endif
             bool rerun = false;
             if (ctr[CTR_FLAGS] & FLAG_DENSE_OVERFLOW) {
                 uint32_t want = std::min<uint32_t>(std::max<uint32_t>(h->ntiles, 1u),

@@ -77,6 +77,40 @@ struct KParams {
     uint32_t nt;       // 1: non-temporal tile loads (SYNCR_CDC_NT=1)
     uint32_t resolve_lane;  // 1: lane-per-file resolve (SYNCR_CDC_FLAG_RESOLVE_LANE); 0: wave-per-file
     uint32_t resolve_noburst;  // 1: no burst of chained hops in the wave resolve (SYNCR_CDC_FLAG_RESOLVE_NOBURST)
+    uint32_t resolve_nosplit;  // 1: no split walks of long files (SYNCR_CDC_FLAG_RESOLVE_NOSPLIT)
+};
+
+// ---- split walks of long files (wave resolve) -------------
+// A file whose walk would be long (>= 2 SPLIT_SEGC candidates) is cut into
+// segments of SPLIT_SEGC candidates.  Segment k >= 1 is walked speculatively by
+// an extra resolve wave from the state "a cut at its first candidate c, buffer
+// full": s = c + 1, R = min(F, s + MAX).  A walk whose own cut lands on
+// segment b's start with exactly that R continues identically to segment b's
+// walk (the walk's future is a function of (s, R) only), so the file's walker
+// adopts segment b's cuts and jumps to where that walk linked in turn.
+constexpr uint32_t SPLIT_SEGC = 16384;                  // candidates per segment
+constexpr uint32_t SPLIT_SCAP = 3 * SPLIT_SEGC + 64;    // scratch cuts per segment walk
+constexpr uint64_t SPLIT_MIN_BYTES = 4ull << 20;         // smaller files never split
+constexpr uint32_t SPLIT_BLOCKS = 128;                  // extra resolve blocks (4 waves each)
+constexpr uint32_t SPLIT_END = 0xffffffffu;             // SplitSeg::link: walked to the file end
+constexpr uint32_t SPLIT_ABORT = 0xfffffffeu;           // (segment walk state: gave up)
+// split[] words: a 64-bit count (split files << 32 | eligible walkers
+// published), so one relaxed read gives both; segment records reserved;
+// queue head; split walkers done
+enum { SPL_PUB64 = 0, SPL_RESERVED = 2, SPL_HEAD = 3, SPL_DONE = 4, SPL_WORDS = 8 };
+struct SplitSeg {            // 64 bytes
+    uint64_t cidx;           // candidate index of the segment's first candidate
+    uint64_t out_off;        // adopted: first cut slot within the file's output
+    uint32_t file;           // file index
+    uint32_t k;              // boundary number within the file (>= 1); 0: unusable record
+    uint32_t s0, R0;         // walk state at the segment start
+    uint32_t first, nseg;    // record of the file's boundary 1; the file's segment count
+    uint32_t n;              // cuts the segment walk produced
+    uint32_t link;           // record of the boundary the walk linked at, or SPLIT_END
+    uint32_t status;         // 0 pending, 1 done, 2 aborted (release)
+    uint32_t verdict;        // 1: adopted by the file's walker
+    uint32_t ready;          // == Tables::epoch: initialised in this launch (release)
+    uint32_t pad;
 };
 
 struct DevCut {        // == syncr_cut
@@ -120,6 +154,13 @@ struct Tables {
     const uint64_t *gend;          // [ngrid] batch offset of that file's end
     uint8_t *gfix;                 // [ngrid] first chunk-local hit in [p, p+63): offset + 1, 0 = none
     const uint64_t *gbase;         // [nfiles] first grid index of each file
+    // split walks of long files
+    uint32_t n_elig;               // order[0 .. n_elig): files of >= SPLIT_MIN_BYTES (largest first)
+    uint32_t seg_cap;              // SplitSeg records
+    SplitSeg *segs;                // [seg_cap]
+    DevCut *seg_cuts;              // [seg_cap * SPLIT_SCAP]
+    uint32_t *split;               // [SPL_WORDS] counters                    (zeroed per launch)
+    uint32_t epoch;                // this launch's id (!= 0, unique in the process): SplitSeg::ready
 };
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------

@@ -1276,6 +1276,105 @@ __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restri
 // scalar/vector ops per cut instead of a dependent memory round trip.
 // ---------------------------------------------------------------------------
 
+// First index in [lo, hi) whose candidate position is >= key (cand sorted), by
+// 64 probes per round: two or three dependent loads for a 64-tile group.
+__device__ __forceinline__ uint64_t wave_lower_bound(const uint64_t *cand, uint64_t lo, uint64_t hi, uint64_t key,
+                                                     int lane) {
+    if (lo > hi) lo = hi;
+    while (hi - lo > 64) {
+        const uint64_t n = hi - lo;
+        const uint64_t idx = lo + n * (uint64_t)(lane + 1) / 65;          // 64 increasing probes in [lo, hi)
+        const uint32_t c = (uint32_t)__builtin_popcountll(__ballot((cand[idx] & CAND_POS_MASK) < key));
+        const uint64_t nlo = c ? lo + n * c / 65 + 1 : lo;               // past the last probe below key
+        const uint64_t nhi = c < 64 ? lo + n * (c + 1) / 65 : hi;         // the first probe at or above key
+        lo = nlo;
+        hi = nhi;
+    }
+    const uint64_t idx = lo + (uint64_t)lane;
+    const uint64_t r = lo + (uint64_t)__builtin_popcountll(__ballot(idx < hi && (cand[idx] & CAND_POS_MASK) < key));
+    return readlane64(r, 0);                     // wave-uniform to the compiler
+}
+
+// SplitSeg fields written by another wave are read with agent-scope atomic
+// loads: a plain load with a wave-uniform address may be a scalar load through
+// the scalar cache, which the acquire does not make coherent (stale fields
+// from an earlier launch were read that way).
+__device__ __forceinline__ uint32_t seg_ld(const uint32_t &f) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ uint64_t seg_ld(const uint64_t &f) {
+    const uint64_t v = __hip_atomic_load(&f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
+__device__ __forceinline__ unsigned long long *split_pub(const Tables &T) {
+    return reinterpret_cast<unsigned long long *>(&T.split[SPL_PUB64]);
+}
+
+// Split setup by the walker of an eligible file (Tables::n_elig): when the file
+// holds >= 2 SPLIT_SEGC candidates, reserve and initialise the SplitSeg records
+// of its boundaries 1 .. nseg-1 (boundary k = its k * SPLIT_SEGC-th candidate)
+// for the extra resolve waves to walk.  Returns the record of boundary 1 and
+// the segment count (nseg = 0: not split).  Every eligible walker then counts
+// itself in the SPL_PUB64 count exactly once, after its reservation.
+__device__ __forceinline__ void split_setup(const KParams &P, const Tables &T, uint32_t i, uint64_t F, uint64_t g0,
+                                            uint64_t ncand, int lane, uint32_t &first, uint32_t &nseg) {
+    first = 0;
+    nseg = 0;
+    if (!P.resolve_nosplit && F && F <= 0xFFFFFF00ull && T.seg_cap) {
+        const uint32_t w0 = (uint32_t)((g0 / T.tile) >> 6), w1 = (uint32_t)(((g0 + F - 1) / T.tile) >> 6);
+        const uint64_t a0 = T.super_off[w0], a1 = T.super_off[w0 + 1], b0 = T.super_off[w1], b1 = T.super_off[w1 + 1];
+        if (b1 - a0 >= 2ull * SPLIT_SEGC) {                       // upper bound on the file's candidates
+            const uint64_t j0 = wave_lower_bound(T.cand, min(a0, ncand), min(a1, ncand), g0, lane);
+            const uint64_t j1 = wave_lower_bound(T.cand, min(b0, ncand), min(b1, ncand), g0 + F, lane);
+            const uint64_t ns = j1 > j0 ? (j1 - j0) / SPLIT_SEGC : 0;
+            if (ns >= 2 && ns < 0x10000ull) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&T.split[SPL_RESERVED], (uint32_t)ns - 1u);
+                base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
+                const bool fits = (uint64_t)base + ns - 1 <= (uint64_t)T.seg_cap;
+                const uint64_t MAX = P.max_chunk;
+                for (uint32_t r = (uint32_t)lane; r + 1 < (uint32_t)ns; r += 64) {
+                    const uint32_t q = base + r;
+                    if (q >= T.seg_cap) continue;
+                    SplitSeg &g = T.segs[q];
+                    g.k = 0;                                          // unusable unless it fits
+                    if (fits) {
+                        const uint64_t cidx = j0 + (uint64_t)(r + 1) * SPLIT_SEGC;
+                        const uint64_t s0 = (T.cand[cidx] & CAND_POS_MASK) - g0 + 1;
+                        g.cidx = cidx;
+                        g.out_off = 0;
+                        g.file = i;
+                        g.k = r + 1;
+                        g.s0 = (uint32_t)s0;
+                        g.R0 = (uint32_t)min(F, s0 + MAX);
+                        g.first = base;
+                        g.nseg = (uint32_t)ns;
+                        g.n = 0;
+                        g.link = 0;
+                        g.status = 0;
+                        g.verdict = 0;
+                    }
+                }
+                __threadfence();
+                for (uint32_t r = (uint32_t)lane; r + 1 < (uint32_t)ns; r += 64)
+                    if (base + r < T.seg_cap)
+                        __hip_atomic_store(&T.segs[base + r].ready, T.epoch, __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                if (fits) {                                       // (uniform again after the lane loops)
+                    first = (uint32_t)__builtin_amdgcn_readfirstlane(base);
+                    nseg = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ns);
+                }
+            }
+        }
+    }
+    // (a reservation precedes the fence before the records' ready stores, so it
+    // is ordered before this count)
+    if (lane == 0) atomicAdd(split_pub(T), (nseg ? 1ull << 32 : 0ull) + 1ull);
+}
+
 // The walk of one file, in file-relative offsets of type Off (uint32_t for
 // files below 4 GiB: every comparison and min stays in the scalar unit, which
 // has no 64-bit unsigned compare).  Per window lane: wr = candidate position
@@ -1283,18 +1382,46 @@ __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restri
 // monotone, so the window stays sorted), wk = head fix-up | known << 8.
 // Cuts are gathered into two VGPRs (lane k = k-th cut of a batch of 64) and
 // stored 64 at a time.
+//
+// Split walks (Off = uint32_t): `elig` = the walker of an eligible file (it may
+// split the file, then adopts segment walks at its boundaries); spec >= 0 = the
+// walk of segment record `spec`, from that segment's start state into scratch,
+// until it lands on a later boundary with that boundary's start state (link),
+// reaches the file end, or passes two boundaries without landing (abort).
 template <typename Off>
 __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, const KParams &P,
-                                             const Tables &T, uint32_t i, uint64_t F, uint64_t g0, int lane) {
+                                             const Tables &T, uint32_t i, uint64_t F, uint64_t g0, int lane,
+                                             bool elig, uint32_t spec) {
     constexpr Off OMAX = (Off)~(Off)0;
-    DevCut *out = T.cuts + T.cut_base[i];
-    const uint64_t cap = T.cut_cap[i];
+    const bool is_spec = spec != SPLIT_END;
+    DevCut *out = is_spec ? T.seg_cuts + (uint64_t)spec * SPLIT_SCAP : T.cuts + T.cut_base[i];
+    const uint64_t cap = is_spec ? (uint64_t)SPLIT_SCAP : (uint64_t)T.cut_cap[i];
     const Off Fo = (Off)F;
     const Off MAX = (Off)min<uint64_t>(P.max_chunk, (uint64_t)OMAX);
     const Off CAP = P.read_cap ? (Off)min<uint64_t>(P.read_cap, (uint64_t)OMAX) : OMAX;
     const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
     const uint64_t ncand = min(total, T.cand_cap);
-    uint64_t wb = F ? T.super_off[(uint32_t)((g0 / T.tile) >> 6)] : 0;   // the file's 64-tile group
+    // split state: the file's remaining boundaries are records [brec, bend);
+    // sb = the next one's start (OMAX: none)
+    uint32_t brec = 0, bend = 0;
+    if (elig) {
+        uint32_t first, nseg;
+        split_setup(P, T, i, F, g0, ncand, lane, first, nseg);
+        if (nseg) {
+            brec = first;
+            bend = first + nseg - 1;
+        }
+    }
+    if (is_spec) {
+        brec = spec + 1;
+        bend = seg_ld(T.segs[spec].first) + seg_ld(T.segs[spec].nseg) - 1;
+    }
+    if constexpr (sizeof(Off) != 4) bend = 0;
+    Off sb = OMAX;
+    auto load_bnd = [&]() { sb = brec < bend ? (Off)seg_ld(T.segs[brec].s0) : OMAX; };
+    load_bnd();
+    uint64_t wb = is_spec ? seg_ld(T.segs[spec].cidx)
+                          : (F ? T.super_off[(uint32_t)((g0 / T.tile) >> 6)] : 0);   // the file's 64-tile group
     Off wr = OMAX;
     uint32_t wk = 0, nx = 64;
     // the window after the current one is loaded ahead (a slide then costs no
@@ -1392,7 +1519,69 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
     int head = 2;            // 1: fix known, 2: unknown (head scan / grid; also at the file start)
     uint32_t fix = 0;
     int jlast = -1;          // window index of the candidate the last cut was made at
+    // a cut at window lane 0's candidate, buffer full (a segment's start state)
+    auto start_at_lane0 = [&](Off s0, Off R0) {
+        s = s0;
+        R = R0;
+        const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)wk, 0);
+        head = (k0 & 0x100u) ? 1 : 2;
+        fix = k0 & 0xffu;
+        jlast = 0;
+    };
+    if (is_spec) start_at_lane0((Off)seg_ld(T.segs[spec].s0), (Off)seg_ld(T.segs[spec].R0));
+    uint32_t link = SPLIT_END;          // segment walk: the record it linked at / SPLIT_END / SPLIT_ABORT
     while (s < R) {                                          // :747
+        if (s >= sb) {
+            // at or past boundary brec: a landing with the boundary's start state
+            // links (segment walk) or adopts the boundary's segment walk (file walker)
+            bool stop = false;
+            while (s >= sb) {
+                if (s == sb && R == (Off)seg_ld(T.segs[brec].R0)) {
+                    if (is_spec) {
+                        link = brec;
+                        stop = true;
+                        break;
+                    }
+                    SplitSeg &g = T.segs[brec];
+                    // (an atomic's result is divergent to the compiler: readfirstlane keeps
+                    // the walk state in scalar registers)
+                    const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(&g.status, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
+                    const uint32_t lk = st == 1u ? seg_ld(g.link) : 0u;
+                    // (a link always names a later boundary of this file)
+                    if (st == 1u && (lk == SPLIT_END || (lk > brec && lk < bend))) {
+                        const uint32_t pend = (uint32_t)cnt & 63u;   // gathered cuts before the adopted ones
+                        if (pend > bstart) flush(pend);
+                        if (lane == 0) {
+                            g.out_off = (uint64_t)cnt;
+                            g.verdict = 1u;
+                        }
+                        cnt += (Off)seg_ld(g.n);
+                        bstart = (uint32_t)cnt & 63u;              // slots below: the copy phase's
+                        if (lk == SPLIT_END) {
+                            stop = true;
+                            break;
+                        }
+                        brec = lk;                                 // continue where that walk linked
+                        load_bnd();
+                        wb = seg_ld(T.segs[brec].cidx);
+#pragma unroll
+                        for (int k = 0; k < PF; ++k) pf[k] = fetch(wb + 64ull * k);
+                        load_window();
+                        start_at_lane0(sb, (Off)seg_ld(T.segs[brec].R0));
+                        continue;
+                    }
+                }
+                ++brec;                                            // passed without adopting
+                if (is_spec && brec > spec + 2) {                  // two boundaries without a landing
+                    link = SPLIT_ABORT;
+                    stop = true;
+                    break;
+                }
+                load_bnd();
+            }
+            if (stop) break;
+        }
         if constexpr (sizeof(Off) == 4) {
             // Burst of chained hops: while every cut lands on a window candidate
             // with no head hit after it (fix 0), the next cut is the candidate
@@ -1499,6 +1688,13 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     const bool ok = on && (int64_t)wr < Rprev && (int64_t)wr >= wprev + 64;
                     const unsigned long long bad = __ballot(on && !ok);
                     mk = bad ? pm & ((1ull << __builtin_ctzll(bad)) - 1ull) : pm;
+                    if (mk) {                                      // stop at the next split boundary
+                        const unsigned long long past = __ballot(((mk >> lane) & 1ull) && (Off)(wr + 1) >= sb);
+                        if (past) {
+                            const uint32_t fl = (uint32_t)__builtin_ctzll(past);
+                            mk &= fl >= 63u ? ~0ull : ((2ull << fl) - 1ull);
+                        }
+                    }
                     if (mk) {
                         j = 63 - __builtin_clzll(mk);
                         s = rl(wr, (uint32_t)j) + 1;                 // cut = edge + 1 (:754-755, :771)
@@ -1536,6 +1732,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     bstart = (uint32_t)cnt & 63u;
                 }
                 if (s >= R) break;
+                if (s >= sb) continue;                              // the boundary first
             }
         }
         const Off lim = R;                                   // :749-752
@@ -1634,24 +1831,117 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
         R += rd;
     }
     if (cnt & 63u) flush((uint32_t)(cnt & 63u));
+    if (is_spec) {                                           // results, then the status (release)
+        SplitSeg &g = T.segs[spec];
+        if (lane == 0) {
+            g.n = (uint32_t)min<uint64_t>((uint64_t)cnt, 0xffffffffull);
+            g.link = link;
+        }
+        const uint32_t st = (link == SPLIT_ABORT || (uint64_t)cnt > cap) ? 2u : 1u;
+        __threadfence();
+        if (lane == 0) __hip_atomic_store(&g.status, st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (lane == 0) {
         T.counts[i] = (uint64_t)cnt;
         if ((uint64_t)cnt > cap) atomicOr(&T.ctr[CTR_FLAGS], FLAG_CUT_OVERFLOW);
     }
+    if (elig && bend) {                                      // adoptions before the done count
+        __threadfence();
+        if (lane == 0) atomicAdd(&T.split[SPL_DONE], 1u);
+    }
 }
 
-// One wave per file; files below 4 GiB walk in 32-bit offsets.
+// The extra resolve waves (split workers): walk segments as the file walkers
+// publish them, then copy every adopted segment's cuts into its file's
+// output.  They never hold up a file walker (which walks a segment itself when
+// that segment's walk is not done), and they only wait for file walkers,
+// which are dispatched first.  split_next: the next segment record to walk, or
+// SPLIT_END once every eligible walker has published and the queue is empty.
+// Polls are relaxed: an agent-scope acquire invalidates the XCD's L2 on gfx950,
+// so it is taken once, only before reading what another wave published.
+__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t ld64_relaxed(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t split_next(const Tables &T, int lane) {
+    uint32_t q = 0;
+    if (lane == 0) q = atomicAdd(&T.split[SPL_HEAD], 1u);
+    q = (uint32_t)__builtin_amdgcn_readfirstlane(q);
+    for (;;) {
+        if (q < min(ld_relaxed(&T.split[SPL_RESERVED]), T.seg_cap)) break;
+        if ((uint32_t)ld64_relaxed(split_pub(T)) >= T.n_elig) {
+            // every reservation precedes its walker's count (split_setup); a stale
+            // read here only leaves a segment to its file's walker
+            if (q < min(ld_relaxed(&T.split[SPL_RESERVED]), T.seg_cap)) break;
+            return SPLIT_END;
+        }
+        __builtin_amdgcn_s_sleep(16);
+    }
+    while (ld_relaxed(&T.segs[q].ready) != T.epoch) __builtin_amdgcn_s_sleep(4);   // not a stale record
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");        // the record's fields
+    return q;
+}
+
+// Once every split file's walker is done: copy the adopted segments' cuts.
+__device__ void split_copy(const Tables &T, int lane, uint32_t wid, uint32_t nw) {
+    uint64_t pub;
+    while ((uint32_t)(pub = ld64_relaxed(split_pub(T))) < T.n_elig) __builtin_amdgcn_s_sleep(16);
+    const uint32_t nsplit = (uint32_t)(pub >> 32);          // final with the last count
+    if (nsplit == 0u) return;                               // nothing split: nothing to copy
+    while (ld_relaxed(&T.split[SPL_DONE]) < nsplit) __builtin_amdgcn_s_sleep(16);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");        // verdicts, offsets and segment cuts
+    const uint32_t nrec = min(ld_relaxed(&T.split[SPL_RESERVED]), T.seg_cap);
+    for (uint32_t q = wid; q < nrec; q += nw) {
+        const SplitSeg &g = T.segs[q];
+        if (seg_ld(g.k) == 0u || seg_ld(g.verdict) != 1u) continue;
+        const uint32_t i = seg_ld(g.file);
+        const uint64_t cap = T.cut_cap[i], o = seg_ld(g.out_off), n = seg_ld(g.n);
+        const DevCut *src = T.seg_cuts + (uint64_t)q * SPLIT_SCAP;
+        DevCut *dst = T.cuts + T.cut_base[i];
+        for (uint64_t t = (uint64_t)lane; t < n && o + t < cap; t += 64) dst[o + t] = src[t];
+    }
+}
+
+__device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P, const Tables &T, int lane,
+                             uint32_t wid, uint32_t nw) {
+    for (;;) {
+        const uint32_t q = split_next(T, lane);
+        if (q == SPLIT_END) break;
+        if (seg_ld(T.segs[q].k) == 0u) continue;
+        const uint32_t i = seg_ld(T.segs[q].file);
+        resolve_walk<uint32_t>(data, P, T, i, T.flen[i], T.foff[i], lane, false, q);
+    }
+    split_copy(T, lane, wid, nw);
+}
+
+// One wave per file; files below 4 GiB walk in 32-bit offsets.  Blocks past
+// the file walkers' (launched only when a file is eligible) are split workers.
+// (Their walk is a separate inlined copy: sharing one with the file walkers
+// made the file walk spill scalar registers.)
 __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__restrict__ data,
                                                                KParams P, Tables T) {
     const int lane = threadIdx.x & 63;
+    const uint32_t nmain = (T.nfiles + 3u) / 4u;
+    if (blockIdx.x >= nmain) {
+        split_worker(data, P, T, lane, (blockIdx.x - nmain) * 4u + (threadIdx.x >> 6), (gridDim.x - nmain) * 4u);
+        return;
+    }
     const uint32_t kf = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (kf >= T.nfiles) return;
     const uint32_t i = T.order[kf];
     const uint64_t F = T.flen[i], g0 = T.foff[i];
-    if (F <= 0xFFFFFF00ull)
-        resolve_walk<uint32_t>(data, P, T, i, F, g0, lane);
-    else
-        resolve_walk<uint64_t>(data, P, T, i, F, g0, lane);
+    const bool elig = kf < T.n_elig;
+    if (F <= 0xFFFFFF00ull) {
+        resolve_walk<uint32_t>(data, P, T, i, F, g0, lane, elig, SPLIT_END);
+    } else {
+        if (elig && lane == 0) atomicAdd(split_pub(T), 1ull);            // counted, never split
+        resolve_walk<uint64_t>(data, P, T, i, F, g0, lane, false, SPLIT_END);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1953,8 +2243,11 @@ hipError_t launch_resolve(const uint8_t *d, const KParams &p, const Tables &t, h
     if (!t.nfiles) return hipSuccess;
     if (p.resolve_lane)
         hipLaunchKernelGGL(cdc_resolve_kernel, dim3((t.nfiles + 63) / 64), dim3(64), 0, s, d, p, t);
-    else
-        hipLaunchKernelGGL(cdc_resolve_wave_kernel, dim3((t.nfiles + 3) / 4), dim3(256), 0, s, d, p, t);
+    else {
+        const bool split = t.n_elig && t.seg_cap && !p.resolve_nosplit;
+        hipLaunchKernelGGL(cdc_resolve_wave_kernel, dim3((t.nfiles + 3) / 4 + (split ? SPLIT_BLOCKS : 0u)),
+                           dim3(256), 0, s, d, p, t);
+    }
     return hipGetLastError();
 }
 

@@ -14,6 +14,9 @@ GOLDEN = os.path.join(TESTS, "golden")
 
 
 def pytest_configure(config):
+    if os.environ.get("SYNCR_TEST_DEV_LIBRARY"):       # diagnostics: run the suite on libsyncr_cdc_dev.so
+        import syncr_amd
+        syncr_amd.use_dev_library()
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); parity tests of the HIP engine")
     config.addinivalue_line("markers", "slow: long-running (full BASELINE sizes)")
 

@@ -517,3 +517,49 @@ def test_long_resolve_chains(chunkers, bits, mx, cap):
     cuts = ch.cut_array(data)
     assert ends_of(cuts) == oracle_ends(data, bits, mx, cap)
     check_contiguous(cuts, data.size, mx)
+
+
+@pytest.mark.parametrize("bits,mx,cap", [(8, 4096, 3000), (8, 1 << 16, 0), (10, 1 << 14, 2 << 20),
+                                         (20, 16 << 20, 2 << 20), (20, 16 << 20, 0)])
+def test_split_walks(bits, mx, cap):
+    """Split walks of long files: files of >= 4 MiB holding
+    >= 2 x 16384 candidates are walked in segments by extra resolve waves and
+    stitched where a walk lands on a segment's start with its start state.
+    Mixed content makes segment starts that are not cuts, read-limit
+    mismatches and aborted segment walks; every file must equal the oracle
+    and the unsplit walk (SYNCR_CDC_FLAG_RESOLVE_NOSPLIT)."""
+    import bench
+    pat = bench.periodic_pattern() if bits == 20 else None
+    rng = np.random.default_rng(bits * 7919 + cap)
+    files = []
+    lo, hi = (34 * M, 44 * M) if bits == 10 else (5 * M, 14 * M)     # >= 2 x 16384 candidates for most
+    for k in range(3 if bits == 10 else 4):
+        n = int(rng.integers(lo, hi))
+        if pat is not None:                         # periodic with random glitches every ~1-3 MiB
+            f = np.resize(pat, n)
+            for g in rng.integers(0, n - 4096, 6).tolist():
+                f[g: g + int(rng.integers(1, 3000))] = rng.integers(0, 256, 1, dtype=np.uint8)
+        else:                                       # random: a candidate every ~2^bits bytes, many not cuts
+            f = rng.integers(0, 256, n, dtype=np.uint8)
+            f[n // 3: n // 3 + 200000] = 9          # a constant stretch: max-chunk cuts
+        files.append(f)
+    files.append(rng.integers(0, 256, 3 * M, dtype=np.uint8))       # below the split threshold
+    lens = np.array([f.size for f in files], np.uint64)
+    offs = np.zeros_like(lens)
+    offs[1:] = np.cumsum(lens + 48)[:-1]
+    span = int(offs[-1] + lens[-1]) + 16
+    data = np.zeros(span, np.uint8)
+    for o, f in zip(offs.tolist(), files):
+        data[o:o + f.size] = f
+    got = {}
+    for flags in (0, syncr_amd.FLAG_RESOLVE_NOSPLIT):
+        with syncr_amd.Chunker(bits, mx, cap, flags=flags) as ch:
+            # the handle splits once a fetch has seen >= 2 x 16384 candidates:
+            # the second call (and the re-runs of the first) walk split
+            got[flags] = [ends_of(r) for r in ch.batch_arrays(data, offs, lens)]
+            got[flags + 100] = [ends_of(r) for r in ch.batch_arrays(data, offs, lens)]
+    for i, (o, n) in enumerate(zip(offs.tolist(), lens.tolist())):
+        f = data[o:o + n]
+        want = (O.chunk_production_window(f, bits, mx, cap) if cap else O.chunk_ideal(f, bits, mx)).tolist()
+        for k in got:
+            assert got[k][i] == want, (i, n, bits, mx, cap, k)
