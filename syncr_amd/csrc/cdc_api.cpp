@@ -88,10 +88,10 @@ struct syncr_cdc {
     // split walks of long files (Tables::segs...): files order[0 .. n_elig) may split
     uint32_t n_elig = 0, seg_cap = 0;
     DevBuf segs, seg_cuts;
-    // split only when a walk can be long: the last launch fetched held >= 2 x
-    // SPLIT_SEGC candidates (random data: ~1 per MiB, so never; periodic or
-    // low-entropy data: thousands per MiB).  Off until a fetch has seen that,
-    // so the common case launches no split workers at all.
+    // split only when walks can be long: the last launch fetched held >= 64 Ki
+    // candidates at >= 1 per 16 KiB (random data: ~1 per MiB, so never;
+    // periodic or low-entropy data: thousands per MiB).  Off until a fetch has
+    // seen that, so the common case launches no split workers at all.
     bool split_hint = false;
 
     // launch
@@ -660,7 +660,9 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
             uint32_t ctr[4];
             CHECK_HIP(hipMemcpy(ctr, h->zeroed.p, 16, hipMemcpyDeviceToHost));
             const uint64_t ncand = (uint64_t)ctr[CTR_CANDS_LO] | ((uint64_t)ctr[CTR_CANDS_HI] << 32);
-            h->split_hint = ncand >= 2ull * SPLIT_SEGC;        // for the next launch (also a re-run below)
+            // for the next launch (also a re-run below): >= 64 Ki candidates at >= 1
+            // per 16 KiB (random data: ~1 per MiB at chunk_bits 20)
+            h->split_hint = ncand >= std::max<uint64_t>(65536ull, h->span >> 14);
             std::vector<uint64_t> counts(h->nfiles);
             if (h->nfiles)
                 CHECK_HIP(hipMemcpy(counts.data(), h->counts.p, h->nfiles * 8ull, hipMemcpyDeviceToHost));

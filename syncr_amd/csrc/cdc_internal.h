@@ -88,10 +88,10 @@ struct KParams {
 // segment b's start with exactly that R continues identically to segment b's
 // walk (the walk's future is a function of (s, R) only), so the file's walker
 // adopts segment b's cuts and jumps to where that walk linked in turn.
-constexpr uint32_t SPLIT_SEGC = 16384;                  // candidates per segment
+constexpr uint32_t SPLIT_SEGC = 4096;                   // candidates per segment
 constexpr uint32_t SPLIT_SCAP = 3 * SPLIT_SEGC + 64;    // scratch cuts per segment walk
-constexpr uint64_t SPLIT_MIN_BYTES = 4ull << 20;         // smaller files never split
-constexpr uint32_t SPLIT_BLOCKS = 128;                  // extra resolve blocks (4 waves each)
+constexpr uint64_t SPLIT_MIN_BYTES = 256ull << 10;       // smaller files never split
+constexpr uint32_t SPLIT_BLOCKS = 256;                  // extra resolve blocks (4 waves each)
 constexpr uint32_t SPLIT_END = 0xffffffffu;             // SplitSeg::link: walked to the file end
 constexpr uint32_t SPLIT_ABORT = 0xfffffffeu;           // (segment walk state: gave up)
 // split[] words: a 64-bit count (split files << 32 | eligible walkers

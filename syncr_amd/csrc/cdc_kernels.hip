@@ -1542,34 +1542,57 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                         stop = true;
                         break;
                     }
-                    SplitSeg &g = T.segs[brec];
-                    // (an atomic's result is divergent to the compiler: readfirstlane keeps
-                    // the walk state in scalar registers)
-                    const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane(
-                        __hip_atomic_load(&g.status, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
-                    const uint32_t lk = st == 1u ? seg_ld(g.link) : 0u;
-                    // (a link always names a later boundary of this file)
-                    if (st == 1u && (lk == SPLIT_END || (lk > brec && lk < bend))) {
-                        const uint32_t pend = (uint32_t)cnt & 63u;   // gathered cuts before the adopted ones
-                        if (pend > bstart) flush(pend);
-                        if (lane == 0) {
-                            g.out_off = (uint64_t)cnt;
-                            g.verdict = 1u;
+                    // Adopt a chain of done segment walks at once: lane k reads record
+                    // brec + k, and the chain brec -> link -> link ... is followed on
+                    // lane indices (one memory round trip per 64 records, not per hop).
+                    const uint32_t rq = brec + (uint32_t)lane;
+                    const bool in = rq < bend;
+                    const uint32_t st = in ? __hip_atomic_load(&T.segs[rq].status, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                    // (atomic results are divergent to the compiler: readlane keeps the
+                    // walk state in scalar registers)
+                    if ((uint32_t)__builtin_amdgcn_readlane((int)st, 0) == 1u) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // the walks' results
+                        const bool done = st == 1u;
+                        const uint32_t nn = done ? __hip_atomic_load(&T.segs[rq].n, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                        const uint32_t lkv = done ? __hip_atomic_load(&T.segs[rq].link, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                        unsigned long long adopted = 0;
+                        uint32_t cur = 0, last = 0;
+                        for (;;) {                                 // chain order = increasing lanes
+                            if ((uint32_t)__builtin_amdgcn_readlane((int)st, (int)cur) != 1u) break;
+                            const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)lkv, (int)cur);
+                            if (lk != SPLIT_END && (lk <= brec + cur || lk >= bend)) break;   // (never)
+                            adopted |= 1ull << cur;
+                            last = lk;
+                            if (lk == SPLIT_END || lk - brec >= 64u) break;
+                            cur = lk - brec;
                         }
-                        cnt += (Off)seg_ld(g.n);
-                        bstart = (uint32_t)cnt & 63u;              // slots below: the copy phase's
-                        if (lk == SPLIT_END) {
-                            stop = true;
-                            break;
-                        }
-                        brec = lk;                                 // continue where that walk linked
-                        load_bnd();
-                        wb = seg_ld(T.segs[brec].cidx);
+                        if (adopted) {
+                            const uint32_t pend = (uint32_t)cnt & 63u;   // gathered cuts before the adopted ones
+                            if (pend > bstart) flush(pend);
+                            const bool mine = (adopted >> lane) & 1ull;
+                            const uint32_t incl = wave_incl_scan(mine ? nn : 0u, lane);
+                            if (mine) {
+                                T.segs[rq].out_off = (uint64_t)cnt + (incl - nn);
+                                T.segs[rq].verdict = 1u;
+                            }
+                            cnt += (Off)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                            bstart = (uint32_t)cnt & 63u;          // slots below: the copy phase's
+                            if (last == SPLIT_END) {
+                                stop = true;
+                                break;
+                            }
+                            brec = last;                           // continue where the chain linked
+                            load_bnd();
+                            wb = seg_ld(T.segs[brec].cidx);
 #pragma unroll
-                        for (int k = 0; k < PF; ++k) pf[k] = fetch(wb + 64ull * k);
-                        load_window();
-                        start_at_lane0(sb, (Off)seg_ld(T.segs[brec].R0));
-                        continue;
+                            for (int k = 0; k < PF; ++k) pf[k] = fetch(wb + 64ull * k);
+                            load_window();
+                            start_at_lane0(sb, (Off)seg_ld(T.segs[brec].R0));
+                            continue;
+                        }
                     }
                 }
                 ++brec;                                            // passed without adopting
