@@ -282,20 +282,25 @@ int32_t ensure_dense(syncr_cdc *h, uint32_t cap) {
     return SYNCR_CDC_OK;
 }
 
-int32_t ensure_cand(syncr_cdc *h, uint64_t cap) {
-    h->cand_cap = cap;
-    CHECK_HIP(h->cand.ensure(std::max<uint64_t>(cap, 1) * 8));
-    // split-walk records: a file splits into segments of SPLIT_SEGC of its
-    // candidates, so cand_cap / SPLIT_SEGC records cover every split file
+// Split-walk records and scratch, only while the handle splits (split_hint):
+// a file splits into segments of SPLIT_SEGC of its candidates, so
+// cand_cap / SPLIT_SEGC records cover every split file.
+int32_t ensure_split(syncr_cdc *h) {
     h->seg_cap = 0;
-    if (h->n_elig) {
-        const uint64_t segs = std::min<uint64_t>(cap / SPLIT_SEGC + 8, 0xffffffull);
+    if (h->n_elig && h->split_hint) {
+        const uint64_t segs = std::min<uint64_t>(h->cand_cap / SPLIT_SEGC + 8, 0xffffffull);
         CHECK_HIP(h->segs.ensure(segs * sizeof(SplitSeg)));
         CHECK_HIP(hipMemset(h->segs.p, 0, segs * sizeof(SplitSeg)));     // no ready word from other memory
         CHECK_HIP(h->seg_cuts.ensure(segs * SPLIT_SCAP * sizeof(DevCut)));
         h->seg_cap = (uint32_t)segs;
     }
     return SYNCR_CDC_OK;
+}
+
+int32_t ensure_cand(syncr_cdc *h, uint64_t cap) {
+    h->cand_cap = cap;
+    CHECK_HIP(h->cand.ensure(std::max<uint64_t>(cap, 1) * 8));
+    return ensure_split(h);
 }
 
 size_t zeroed_bytes(const syncr_cdc *h) { return split_ctr_offset(h) + SPL_WORDS * 4; }
@@ -662,7 +667,12 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
             const uint64_t ncand = (uint64_t)ctr[CTR_CANDS_LO] | ((uint64_t)ctr[CTR_CANDS_HI] << 32);
             // for the next launch (also a re-run below): >= 64 Ki candidates at >= 1
             // per 16 KiB (random data: ~1 per MiB at chunk_bits 20)
-            h->split_hint = ncand >= std::max<uint64_t>(65536ull, h->span >> 14);
+            const bool hint = ncand >= std::max<uint64_t>(65536ull, h->span >> 14);
+            if (hint != h->split_hint) {
+                h->split_hint = hint;
+                int32_t rc = ensure_split(h);
+                if (rc) return rc;
+            }
             std::vector<uint64_t> counts(h->nfiles);
             if (h->nfiles)
                 CHECK_HIP(hipMemcpy(counts.data(), h->counts.p, h->nfiles * 8ull, hipMemcpyDeviceToHost));

@@ -262,3 +262,32 @@ def test_first_read_failure_is_empty(tmp_path):
         assert [t for t, _, _ in got] == list(range(len(paths)))
         assert got[2][1] == -errno.EISDIR and got[2][2].size == 0
         check([(i, s, a) for i, (_, s, a) in enumerate(got[:2] + got[3:])], files)
+
+
+def test_periodic_files_split_walks():
+    """Low-entropy input through the pipeline: bits-20 periodic files (a cut
+    every 64 bytes) of up to 6 MiB between random ones.  A slot's handle turns
+    on split walks once a batch of it held many candidates,
+    so later batches walk split; every ChunkInfo (boundaries + BLAKE3) must
+    still equal the oracle's, in submission order."""
+    import bench
+    pat = bench.periodic_pattern()
+    rng = np.random.default_rng(31)
+    files = []
+    for i in range(24):
+        n = int(rng.integers(300 << 10, 6 * M))
+        files.append(np.resize(pat, n) if i % 2 == 0 else O.xorshift_bytes(7000 + i, n))
+    with syncr_amd.Ingest(batch_bytes=8 * M, depth=2, copy_threads=4) as g:
+        for i, f in enumerate(files):
+            g.submit(f, i)
+        g.flush()
+        res = g.results
+    assert [t for t, _, _ in res] == list(range(len(files)))
+    for (tag, status, got), data in zip(res, files):
+        assert status == 0, tag
+        ends = O.chunk_production_window(data, 20, 16 * M, 2 * M).astype(np.uint64)
+        starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64)[:ends.size]
+        assert np.array_equal(got["offset"], starts), tag
+        assert np.array_equal(got["len"].astype(np.uint64), ends - starts), tag
+        hs = O.blake3_batch(data, starts, ends - starts, nthreads=8)
+        assert np.array_equal(got["hash"], hs), tag
