@@ -80,7 +80,8 @@ struct syncr_cdc {
     bool hash_on = false;
     uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 3, b3_nosplit = 0, b3_nouni = 0;     // dev A/B knobs; coop 3 = the product (LD_PAIR + quad merges)
     uint64_t items_cap = 0, trees_cap = 0;
-    DevBuf hctr, items, trees, gcv, hashes, packed, tpieces, pieces, pcv;
+    DevBuf hctr, items, trees, gcv, hashes, packed, tpieces, pieces, pcv, iblocks;
+    uint32_t n_iblocks = 0;
     uint64_t pieces_cap = 0;
     // read-boundary grid (Tables::gpos...): production semantics only
     uint32_t ngrid = 0;
@@ -241,6 +242,19 @@ int32_t upload_cut_tables(syncr_cdc *h) {
     CHECK_HIP(h->tpieces.ensure(h->trees_cap * 8));
     CHECK_HIP(h->pieces.ensure(h->pieces_cap * 16));
     CHECK_HIP(h->pcv.ensure(h->pieces_cap * 32));
+    // b3_items_kernel blocks: each group of 256 files is split into parts of
+    // ~B3_ITEMS_CUTS of its output slots, so one file with millions of chunks
+    // (periodic data) is planned by many blocks, not one
+    std::vector<uint64_t> ib;
+    for (uint32_t g = 0; g * 256u < h->nfiles; g++) {
+        uint64_t caps = 0;
+        for (uint32_t i = g * 256u; i < std::min<uint32_t>(h->nfiles, g * 256u + 256u); i++) caps += h->h_cut_cap[i];
+        const uint64_t parts = std::min<uint64_t>(std::max<uint64_t>((caps + B3_ITEMS_CUTS - 1) / B3_ITEMS_CUTS, 1), 0xfffff);
+        for (uint64_t k = 0; k < parts; k++) ib.push_back(((uint64_t)g << 40) | (k << 20) | parts);
+    }
+    h->n_iblocks = (uint32_t)ib.size();
+    CHECK_HIP(h->iblocks.ensure(std::max<size_t>(ib.size(), 1) * 8));
+    if (!ib.empty()) CHECK_HIP(hipMemcpy(h->iblocks.p, ib.data(), ib.size() * 8, hipMemcpyHostToDevice));
     CHECK_HIP(h->cut_base.ensure(std::max<size_t>(h->nfiles, 1) * 8));
     CHECK_HIP(h->cut_cap.ensure(std::max<size_t>(h->nfiles, 1) * 4));
     CHECK_HIP(h->cuts.ensure(std::max<uint64_t>(acc, 1) * sizeof(DevCut)));
@@ -269,6 +283,8 @@ HashTables make_hash_tables(syncr_cdc *h) {
     t.ablate = h->b3_ablate;
     t.nt = h->b3_nt;
     t.coop = h->b3_coop;
+    t.iblocks = h->iblocks.as<uint64_t>();
+    t.n_iblocks = h->n_iblocks;
     t.nosplit = h->b3_nosplit;
     t.nouni = h->b3_nouni;
     return t;
@@ -516,7 +532,7 @@ void syncr_cdc_close(syncr_cdc *h) {
                       &h->dense_cnt, &h->dense_bits, &h->super_off, &h->cand, &h->cuts,
                       &h->counts, &h->stage, &h->hctr, &h->items, &h->trees, &h->gcv,
                       &h->hashes, &h->packed, &h->tpieces, &h->pieces, &h->pcv, &h->gpos, &h->gend, &h->gfix, &h->gbase,
-                      &h->segs, &h->seg_cuts};
+                      &h->segs, &h->seg_cuts, &h->iblocks};
     for (DevBuf *b : bufs) b->release();
     (void)hipStreamDestroy(h->stream);
     delete h;

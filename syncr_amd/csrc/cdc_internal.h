@@ -180,6 +180,7 @@ constexpr int B3_CLASSES = 7;                               // packed classes: <
 constexpr uint64_t B3_TAIL = 1ull << 63;                  // packed entry: tail unit
 constexpr uint64_t B3_PIECE = 1ull << 62;                 // packed entry: piece (index into pieces[])
 constexpr uint32_t B3_MAX_PIECES = 7;                     // popcount of a task count <= 127
+constexpr uint64_t B3_ITEMS_CUTS = 16384;                 // output slots per b3_items_kernel block
 enum { B3C_ITEMS = 0, B3C_TREES = 1, B3C_NEXT = 2, B3C_FLAGS = 3, B3C_PK0 = 4, B3C_PIECES = 4 + B3_CLASSES,
        B3C_WORDS = 5 + B3_CLASSES };
 
@@ -201,6 +202,8 @@ struct HashTables {
     uint32_t *hashes;              // [sum cut_cap * 8] BLAKE3 of each cut slot
     uint32_t ablate;               // timing-only (SYNCR_B3_ABLATE): 1 = loads only, 2 = no loads
     uint32_t nt;                   // 1: non-temporal chunk loads (SYNCR_B3_NT)
+    const uint64_t *iblocks;       // [n_iblocks] b3_items_kernel blocks: group << 40 | part << 20 | parts
+    uint32_t n_iblocks;
     uint32_t coop;                 // 3 (product): cooperative LDS-DMA loader, two blocks per round, quad
                                    //   merges; 2: shuffle merges (SYNCR_B3_LOAD=pair); 1: one block per
                                    //   round (=coop); 0: per-lane loads (=plain)

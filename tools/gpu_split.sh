@@ -6,7 +6,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -3 gpurun_out/split_tests.log
 for wl in dense1 dense; do
   timeout -k 10 300 python -u bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --sustained-steps 0 --no-read-probe > gpurun_out/bench_$wl.json 2> gpurun_out/bench_$wl.err || { tail -20 gpurun_out/bench_$wl.err; exit 12; }
-  python3 -c "import json,sys; d=json.load(open('gpurun_out/bench_$wl.json')); r=d['roofline']; print('$wl', d['value'], d['ms_per_step'], r['kernel_ms'], r['dense_ms'], r['resolve_ms'], d['pipelined'] and d['pipelined']['value'])"
+  python3 -c "import json,sys; d=json.load(open('gpurun_out/bench_$wl.json')); r=d['roofline']; print('$wl', d['value'], d['ms_per_step'], r['kernel_ms'], r['dense_ms'], r['resolve_ms'], d['pipelined'] and d['pipelined']['value'], 'hashed', d['hashed'] and (d['hashed']['value'], d['hashed']['hash_ms']))"
 done
 timeout -k 10 300 python -u tools/ab_bench.py "SYNCR_CDC_ABLATE=8" "SYNCR_CDC_ABLATE=8,SYNCR_CDC_RESOLVE=nosplit" --rounds 4 > gpurun_out/ab_split.log 2>&1 || { tail -20 gpurun_out/ab_split.log; exit 13; }
 cat gpurun_out/ab_split.log
