@@ -204,7 +204,19 @@ class Dist:
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            # Gloo reports its connections on stdout ("[Gloo] Rank r is connected
+            # to ..."), which would mix into the one JSON line rank 0 prints:
+            # send fd 1 to stderr while the group connects
+            import ctypes
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            finally:
+                ctypes.CDLL(None).fflush(None)
+                os.dup2(saved, 1)
+                os.close(saved)
             self.pg = dist
 
     def barrier(self):
