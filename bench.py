@@ -4,15 +4,25 @@
 Metric (BASELINE.json): GiB/s of file bytes chunked (bytes -> cut offsets),
 inputs already resident in HBM, bit-exact vs the reference chunker.
 
-One step = one pass of the hot path (scan kernel + dense pass + per-file
-resolve, cuts written to HBM) over this rank's whole batch.  Workload at N=1:
-SURVEY.md §8d config 3 -- 10 000 Zipf(1.5) files (4 KiB..128 MiB, 9.73 GiB).
-With N GPUs the corpus is N such file sets (N x 10 000 files, distinct seeds),
-LPT-sharded per file across ranks: fixed work per GPU ("weak" scaling), no
-data-path collective (files are independent).  torch.distributed
-(gloo) is used only for the barrier and the max-over-ranks of the step time.
+One step = one pass of the hot path (scan kernel + dense pass + compaction +
+per-file resolve, cuts written to HBM) over this rank's whole batch.  Workload
+at N=1: SURVEY.md §8d config 3 -- 10 000 Zipf(1.5) files (4 KiB..128 MiB,
+9.73 GiB).  With N GPUs (BASELINE config 4) the SAME 10 000-file corpus is
+LPT-sharded per file across the ranks (`--scaling strong`, the default): the
+aggregate is the corpus bytes / the max per-rank step time.  `--scaling weak`
+gives every rank its own 10 000 files instead.  No data-path collective: files
+are independent; torch.distributed (gloo) carries only the
+barrier and the max / sum / gather of per-rank numbers.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload zipf10k|uniform1k|dense|big1]
+After the timed headline (untimed, N=1 only, on the same GPU): the parity leg
+-- every file of the headline corpus in both semantics and with hashes against
+golden digests, every KAT case, the BLAKE3 vectors, an adversarial subset, the
+multi-device ingest -- and the other single-GPU BASELINE configs: uniform1k
+(config 2), dedup (config 5), the adversarial dense workload, and the
+end-to-end ingest rate from host memory.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
+                    [--workload zipf10k|uniform1k|dense|big1|dense1|dedup]
 
 `--gpus N` with N > 1 launches the N ranks itself (one process per GPU, before
 anything touches HIP) unless a launcher (torchrun) already set WORLD_SIZE, in
@@ -22,7 +32,6 @@ device: it prints the shard plan (files / bytes per rank, disjointness).
 from __future__ import annotations
 
 import argparse
-import heapq
 import json
 import os
 import socket
@@ -35,166 +44,19 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from benchlib.workloads import (DENSE_CONSTANT, DENSE_PERIODIC, WORKLOADS, dedup_plan, dense_kind,  # noqa: E402,F401
+                                lpt_shard, offsets_of, periodic_pattern, workload, zipf_sizes)
+
 METRIC = "GiB/s chunked device-resident (bytes→cut offsets); bit-exact vs ref"
 METRIC_HASHED = "GiB/s chunked+BLAKE3-hashed device-resident (bytes→ChunkInfo); bit-exact vs ref"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 M = 1 << 20
-
-
-def zipf_sizes(n: int = 10000, seed: int = 20251212) -> np.ndarray:
-    """size_i = min(4 KiB * Z_i, 128 MiB), Z = rng.zipf(1.5)."""
-    z = np.random.default_rng(seed).zipf(1.5, n).astype(np.float64)
-    return np.minimum(4096.0 * z, float(128 * M)).astype(np.uint64)
-
-
-# --workload dense: the zipf10k file table with adversarial contents in some
-# files (VERDICT r1 "What's missing" #4; the reference's own tests chunk
-# constant data, tests/chunking_test.rs:95-108, and 50 MiB of 'A',
-# tests/protocol_list_test.rs:360-378).  Kind per corpus index i:
-DENSE_PERIODIC, DENSE_CONSTANT = 5, 11          # i % 16 == 5: 64-byte period; i % 16 == 11: one byte value
-
-
-def dense_kind(i: int) -> int:
-    """0 random, 1 periodic (a 64-byte pattern that hits at bits 20 once per
-    period: a candidate every 64 bytes, 288 per scan tile = dense tiles), 2
-    constant byte (never hits: forced MAX / read-cap cuts only)."""
-    r = i % 16
-    return 1 if r == DENSE_PERIODIC else (2 if r == DENSE_CONSTANT else 0)
-
-
-def periodic_pattern(seed: int = 20251212) -> np.ndarray:
-    """64 bytes whose periodic extension hits the Bup edge test at chunk_bits
-    20 (S = sum of the window = 15 mod 16 and W = sum of (age+1)*byte = 0x17BF
-    mod 2^16, Appendix A) at the phase where the window is exactly the pattern
-    (age 0 = pattern[63]).  Built by fixing 62 random bytes and solving the last
-    two (weights 1 and 2) for the W target, then checking S."""
-    rng = np.random.default_rng(seed)
-    w = np.arange(64, 0, -1, dtype=np.int64)          # pattern[k] has age 63-k: weight 64-k
-    for _ in range(1 << 20):
-        p = rng.integers(0, 256, 64).astype(np.int64)
-        rest = int((w[:62] * p[:62]).sum())
-        t = (0x17BF - rest) % 65536                   # W = 0x17BF mod 2^16: (124992 + W) & 0xffff == 0xffff
-        for x1 in range(256):                          # pattern[62]: weight 2, pattern[63]: weight 1
-            x0 = t - 2 * x1
-            if 0 <= x0 < 256:
-                p[62], p[63] = x1, x0
-                S = int(p.sum())
-                if (1984 + S) % 16 == 15 and ((124992 + int((w * p).sum())) & 0xFFFF) == 0xFFFF:
-                    return p.astype(np.uint8)
-    raise RuntimeError("no periodic pattern found")
-
-
-def workload(name: str, world: int):
-    """Global file table (sizes, corpus indices) for `world` GPUs."""
-    if name in ("zipf10k", "dense"):
-        one = zipf_sizes()
-        desc = ("SURVEY §8d config 3: 10 000 Zipf(1.5) files, 4 KiB-128 MiB, 9.73 GiB per GPU; "
-                "N GPUs chunk N x 10 000 files (distinct seeds) LPT-sharded per file (config 4)")
-        if name == "dense":
-            desc = ("adversarial: the zipf10k file table; files i%16==5 are a 64-byte period that hits at "
-                    "chunk_bits 20 every 64 bytes (dense tiles, long serial resolve chains), files i%16==11 are "
-                    "one constant byte (no hits: MAX / read-cap cuts), the rest random")
-    elif name == "big1":
-        one = np.full(1, 128 * M, np.uint64)
-        desc = "diagnostic: one 128 MiB file (the longest resolve walk of zipf10k)"
-    elif name == "dense1":
-        one = np.full(1, 128 * M, np.uint64)
-        desc = "diagnostic: one 128 MiB periodic-64 file (2 M chained cuts: the dense workload's longest walk)"
-    elif name == "dedup":
-        one = np.array([p[4] for p in dedup_plan()], np.uint64)
-        desc = ("SURVEY §8d config 5: 1000 files per GPU, each one 1-256 byte edit (50 % overwrite, 25 % insert, "
-                "25 % delete) of one random 32 MiB base, ~32 GiB (boundary stability in config.dedup)")
-    elif name == "uniform1k":
-        one = np.full(1024, M, np.uint64)
-        desc = "SURVEY §8d config 2: 1024 x 1 MiB files per GPU, LPT-sharded per file"
-    elif name in ("uniform2k", "uniform4k"):
-        n = 2048 if name == "uniform2k" else 4096
-        one = np.full(n, M, np.uint64)
-        desc = f"diagnostic: {n} x 1 MiB files per GPU (batch-size sweep between uniform1k and zipf10k)"
-    else:
-        raise SystemExit(f"unknown workload {name}")
-    sizes = np.tile(one, world)
-    return sizes, np.arange(sizes.size, dtype=np.uint64), desc
-
-
-DEDUP_BASE = 32 * M
-
-
-def dedup_plan(n: int = 1000, seed: int = 20251212):
-    """(kind, pos, len, inserted bytes, file size) of the dedup corpus's variants."""
-    rng = np.random.default_rng(seed)
-    plan = []
-    for _ in range(n):
-        pos = int(rng.integers(0, DEDUP_BASE))
-        ln = int(rng.integers(1, 257))
-        kind = ("overwrite", "overwrite", "insert", "delete")[int(rng.integers(0, 4))]
-        ins = rng.integers(0, 256, ln, dtype=np.uint8)
-        d = min(ln, DEDUP_BASE - pos)
-        size = DEDUP_BASE + (ln if kind == "insert" else (-d if kind == "delete" else 0))
-        plan.append((kind, pos, ln, ins, size))
-    return plan
-
-
-def dedup_base() -> np.ndarray:
-    return np.random.default_rng(31337).integers(0, 256, DEDUP_BASE, dtype=np.uint8)
-
-
-def dedup_file(base: np.ndarray, entry) -> tuple[np.ndarray, int, int]:
-    """One variant's bytes and its edit (position, size delta)."""
-    kind, pos, ln, ins, _ = entry
-    if kind == "overwrite":
-        f = base.copy()
-        k = max(0, min(ln, base.size - pos))
-        f[pos:pos + k] = ins[:k]
-        return f, pos, 0
-    if kind == "insert":
-        return np.concatenate([base[:pos], ins, base[pos:]]), pos, ln
-    d = min(ln, base.size - pos)
-    return np.concatenate([base[:pos], base[pos + d:]]), pos, -d
-
-
-def fill_dedup(dbuf, offs, lens, idx):
-    """Upload the dedup variants (file j is variant idx[j] % 1000 of the plan)."""
-    plan, base = dedup_plan(), dedup_base()
-    for j in range(lens.size):
-        f, _, _ = dedup_file(base, plan[int(idx[j]) % len(plan)])
-        assert f.size == int(lens[j])
-        dbuf.upload(f, offset=int(offs[j]))
-
-
-def dedup_stability(cuts, idx) -> dict:
-    """Fraction of the base's cut positions each variant keeps (shift-adjusted)."""
-    plan, base = dedup_plan(), dedup_base()
-    import syncr_amd
-    with syncr_amd.Chunker() as c:
-        bc = c.batch_arrays(base, np.zeros(1, np.uint64), np.array([base.size], np.uint64))[0]
-    base_cuts = set((bc["offset"].astype(np.int64) + bc["len"].astype(np.int64)).tolist())
-    kept = []
-    for c, i in zip(cuts, idx.tolist()):
-        kind, pos, ln, _, _ = plan[int(i) % len(plan)]
-        delta = ln if kind == "insert" else (-min(ln, DEDUP_BASE - pos) if kind == "delete" else 0)
-        ends = (c["offset"].astype(np.int64) + c["len"].astype(np.int64)).tolist()
-        adj = {e - delta if e > pos else e for e in ends}
-        kept.append(len(adj & base_cuts) / max(len(base_cuts), 1))
-    return {"base_cuts": len(base_cuts), "kept_median": round(float(np.median(kept)), 4),
-            "kept_min": round(float(np.min(kept)), 4),
-            "note": "share of the base file's cut offsets present in each variant (offsets past the edit shifted back)"}
-
-
-def lpt_shard(sizes: np.ndarray, world: int) -> list[np.ndarray]:
-    """Longest-processing-time-first assignment of files to ranks."""
-    order = np.argsort(-sizes.astype(np.int64), kind="stable")
-    heap = [(0, r) for r in range(world)]
-    parts: list[list[int]] = [[] for _ in range(world)]
-    for i in order.tolist():
-        load, r = heapq.heappop(heap)
-        parts[r].append(i)
-        heapq.heappush(heap, (load + int(sizes[i]), r))
-    return [np.array(sorted(p), dtype=np.int64) for p in parts]
+# golden digest fixture of each workload's corpus (tests/golden/<name>_digests.npz)
+GOLDEN_OF = {"zipf10k": "zipf10k", "dense": "dense", "dedup": "dedup"}
 
 
 class Dist:
-    """Control plane only (barrier, max, sum) -- no data-path collective."""
+    """Control plane only (barrier, max, sum, gather) -- no data-path collective."""
 
     def __init__(self):
         self.rank = int(os.environ.get("RANK", 0))
@@ -367,6 +229,7 @@ def cpu_baseline(dbuf, offs, lens, cuts, hcuts, sample_gib: float, skip=None):
         e = (c["offset"].astype(np.uint64) + c["len"].astype(np.uint64)).tolist()
         mism += e != ref[j].tolist()
     gib = tot / 2**30
+    nproc = hw["nproc"] or nthr
     out = {
         "value": round(gib / dt1, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
         "sample": f"first {take.size} files of rank 0's batch ({gib:.2f} GiB), production semantics, "
@@ -374,6 +237,10 @@ def cpu_baseline(dbuf, offs, lens, cuts, hcuts, sample_gib: float, skip=None):
                   f"`value` single thread (the reference chunks one file at a time, file_operations.rs:599-605), "
                   f"`threads_value` one file per thread on `threads` threads",
         "threads_value": round(gib / dtn, 4), "threads": nthr, **hw,
+        "all_cores_estimate": round(gib / dtn * nproc / max(nthr, 1), 3),
+        "all_cores_note": (f"SURVEY §8d's 'one file per thread on all nproc cores' leg, NOT measured: the GPU box "
+                           f"grants one GPU's job a {nthr}-CPU share of its {nproc} CPUs (OMP_NUM_THREADS); "
+                           f"this is threads_value x nproc / threads, a linear-scaling upper bound"),
         "gpu_cuts_match_sample": mism == 0, "sample_files_mismatched": int(mism),
     }
     if skip is not None:
@@ -394,30 +261,16 @@ def cpu_baseline(dbuf, offs, lens, cuts, hcuts, sample_gib: float, skip=None):
     return out
 
 
-def fill_dense(dbuf, offs, lens, idx):
-    """Overwrite the adversarial files of --workload dense (see dense_kind)."""
-    pat = periodic_pattern()
-    for j in range(lens.size):
-        k = dense_kind(int(idx[j]))
-        n = int(lens[j])
-        if k == 0 or n == 0:
-            continue
-        if k == 1:
-            a = np.resize(pat, n)
-        else:
-            a = np.full(n, int(idx[j]) & 0xFF, np.uint8)
-        dbuf.upload(a, offset=int(offs[j]))
-
-
 def dry_run(d: Dist, args) -> None:
-    sizes, idx, desc = workload(args.workload, d.world)
+    sizes, idx, desc = workload(args.workload, d.world, args.scaling)
     mine = lpt_shard(sizes, d.world)[d.rank]
     plan = d.gather({"rank": d.rank, "files": mine.tolist()})
     if d.rank == 0:
         allf = np.concatenate([np.array(p["files"], np.int64) for p in plan]) if plan else np.zeros(0, np.int64)
         loads = [int(sizes[np.array(p["files"], np.int64)].sum()) for p in plan]
         print(json.dumps({
-            "dry_run": True, "n_gpus": d.world, "workload": args.workload,
+            "dry_run": True, "n_gpus": d.world, "workload": args.workload, "scaling": args.scaling,
+            "total_files": int(sizes.size), "total_bytes": int(sizes.sum()),
             "shards": [{"rank": p["rank"], "files": len(p["files"]), "bytes": l} for p, l in zip(plan, loads)],
             "disjoint": bool(np.unique(allf).size == allf.size),
             "covers_all": bool(np.array_equal(np.sort(allf), np.arange(sizes.size))),
@@ -426,17 +279,74 @@ def dry_run(d: Dist, args) -> None:
         }), flush=True)
 
 
+def run_legs(args, dev_id: int, dbuf, offs, lens, idx, rank_span: int, out: dict) -> None:
+    """N=1 only, after the headline: parity legs and the other single-GPU configs."""
+    from benchlib import legs as L
+    t_all = time.perf_counter()
+    parity = out.setdefault("parity", {})
+    timing = {}
+
+    def timed(name, fn, *a):
+        t = time.perf_counter()
+        try:
+            r = fn(*a)
+        except Exception as e:                                   # reported, never hidden
+            r = {"error": f"{type(e).__name__}: {e}"}
+        timing[name] = round(time.perf_counter() - t, 2)
+        return r
+
+    if args.workload == "zipf10k":
+        parity["ideal"] = timed("ideal", L.ideal_leg, dbuf, offs, lens, idx, dev_id)
+        host = dbuf.download(rank_span)
+    else:
+        host = None
+    for h, b in out.pop("_slots"):
+        b.free()
+        h.close()
+    parity["kat"] = timed("kat", L.kat_leg, dev_id)
+    parity["blake3_vectors"] = timed("blake3_vectors", L.blake3_vectors_leg, dev_id)
+    parity["dense_subset"] = timed("dense_subset", L.dense_subset_leg, dev_id)
+    k, w = args.steps, max(args.warmup, 2)
+    if args.workload != "uniform1k":
+        out["uniform1k"] = timed("uniform1k", L.uniform1k_leg, dev_id, k, w)
+    if args.workload != "dedup":
+        out["dedup"] = timed("dedup", L.dedup_leg, dev_id, k, w)
+    if args.workload != "dense":
+        out["dense"] = timed("dense", L.dense_leg, dev_id, k, w)
+    if host is not None:
+        out["ingest"] = timed("ingest", L.ingest_leg, host, offs, lens, idx, dev_id)
+        parity["ingest_multi_device"] = out["ingest"].get("multi_device", {}).get("parity")
+    del host
+    # one summary: every parity check of the line
+    checks = []
+    for name, p in list(parity.items()) + [(f"{s}.parity", out.get(s, {}).get("parity")) for s in
+                                            ("uniform1k", "dedup", "dense", "ingest")] + \
+            [(f"{s}.parity_hashed", out.get(s, {}).get("parity_hashed")) for s in ("dedup", "dense")]:
+        if isinstance(p, dict) and "mismatches" in p:
+            checks.append((name, p.get("files", p.get("cases", 0)), p["mismatches"] + p.get("hash_mismatches", 0)))
+        elif isinstance(p, dict):
+            checks.append((name, 0, 1))                          # error / missing fixture: counted as a failure
+    parity["summary"] = {"checks": len(checks), "files_or_cases": int(sum(c[1] for c in checks)),
+                         "mismatches": int(sum(c[2] for c in checks)),
+                         "failed": [c[0] for c in checks if c[2]]}
+    out["legs_seconds"] = dict(timing, total=round(time.perf_counter() - t_all, 2))
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "uniform2k", "uniform4k", "dense", "big1", "dense1",
-                                                           "dedup"])
+    ap.add_argument("--workload", default="zipf10k", choices=list(WORKLOADS))
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="N>1: strong = one file set sharded across the ranks (BASELINE config 4, default); "
+                         "weak = one file set per rank")
     ap.add_argument("--mode", default="production", choices=["production", "ideal"])
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the untimed parity leg and the other BASELINE configs (N=1)")
     ap.add_argument("--no-read-probe", action="store_true",
                     help="skip the streaming-read microbenchmark reported as roofline.measured_read_peak")
     ap.add_argument("--pipeline-depth", type=int, default=2,
@@ -473,6 +383,8 @@ def main(argv=None):
         return 0
 
     import syncr_amd
+    from benchlib import golden as G
+    from benchlib import legs as L
     if args.dev_lib:
         syncr_amd.use_dev_library()
     read_cap = syncr_amd.TOKIO_READ_CAP if args.mode == "production" else 0
@@ -484,29 +396,33 @@ def main(argv=None):
         dev_id = dmap[d.local_rank]
     ch = syncr_amd.Chunker(syncr_amd.CHUNK_BITS, syncr_amd.MAX_CHUNK_SIZE, read_cap, device=dev_id)
 
-    sizes, indices, desc = workload(args.workload, world)
+    sizes, indices, desc = workload(args.workload, world, args.scaling)
     mine = lpt_shard(sizes, world)[d.rank]
     lens = sizes[mine]
     idx = indices[mine]
-    offs = np.zeros_like(lens)
-    if lens.size:
-        offs[1:] = np.cumsum(lens)[:-1]
+    offs = offsets_of(lens)
     span = int(lens.sum())
     depth = max(1, args.pipeline_depth)
-    slots = []                                # (handle, corpus copy): one batch in flight each
-    for k in range(depth):
-        h = ch if k == 0 else syncr_amd.Chunker(syncr_amd.CHUNK_BITS, syncr_amd.MAX_CHUNK_SIZE, read_cap,
-                                                 device=dev_id)
-        b = syncr_amd.DeviceBuffer(h, span)   # own buffer: no slot reads another's bytes from cache
-        b.gen_corpus(offs, lens, indices=idx)
+
+    def make_slot(h):
+        """A handle with its own copy of the corpus (one batch in flight each)."""
+        b = syncr_amd.DeviceBuffer(h, max(span, 16))   # own buffer: no slot reads another's bytes from cache
+        if args.workload == "dedup":
+            plan = dedup_plan()
+            L.build_dedup(h, b, offs, [plan[int(i) % len(plan)] for i in idx.tolist()])
+        else:
+            b.gen_corpus(offs, lens, indices=idx)
         if args.workload == "dense":
-            fill_dense(b, offs, lens, idx)
+            L.fill_dense(b, offs, lens, idx)
         elif args.workload == "dense1":
             b.upload(np.resize(periodic_pattern(), span))
-        elif args.workload == "dedup":
-            fill_dedup(b, offs, lens, idx)
         h.plan(offs, lens, span)
-        slots.append((h, b))
+        return (h, b)
+
+    # the headline runs with ONE handle open on the device (one batch in
+    # flight, like a single chunking thread); the pipelined section below adds
+    # the other slots' handles
+    slots = [make_slot(ch)]
     ch, dbuf = slots[0]
     head_hashed = args.hashed
 
@@ -551,7 +467,7 @@ def main(argv=None):
 
     # sustained rate: the same one-in-flight steps after ~150 ms of back-to-back
     # chunking.  On MI355X the shader clock dips for the first ~30 ms of a
-    # sustained scan (2.1 -> 1.7 GHz by rocprofv3 GRBM_GUI_ACTIVE, DESIGN.md §7)
+    # sustained scan (2.1 -> 1.7 GHz by rocprofv3 GRBM_GUI_ACTIVE, DESIGN.md §4.2)
     # and the timed K steps above usually start inside that dip; a continuously
     # running ingest pipeline sees this rate.
     sustained = None
@@ -576,6 +492,9 @@ def main(argv=None):
 
     pipelined = None
     if depth > 1:                             # the same K steps with `depth` batches in flight
+        for _ in range(depth - 1):
+            slots.append(make_slot(syncr_amd.Chunker(syncr_amd.CHUNK_BITS, syncr_amd.MAX_CHUNK_SIZE, read_cap,
+                                                     device=dev_id)))
         for h, b in slots[1:]:                # settle capacity re-runs before timing
             h.launch(b.ptr, hashed=head_hashed)
             h.fetch(hashed=head_hashed)
@@ -672,8 +591,30 @@ def main(argv=None):
             "pipelined_value": hpipe,
             "leaf_traffic_over_algorithmic": (round(htr["hbm_bytes_per_launch"] / span, 4) if htr else None),
             "leaf_traffic_source": (htr.get("source") if htr else None),
-            "sample_check": "cpu_baseline.gpu_hashes_match_sample (rank 0, N=1)",
+            "sample_check": "cpu_baseline.gpu_hashes_match_sample (rank 0, N=1) and parity.headline_hashed",
         }
+
+    # parity of the headline corpus: every file of this rank against the golden
+    # digests of the CPU oracle (weak-scaled copies with other seeds are skipped)
+    parity = {}
+    gname = GOLDEN_OF.get(args.workload)
+    if gname is not None:
+        rows = idx.astype(np.int64) % (1000 if gname == "dedup" else 1 << 62)
+        sem = "production" if read_cap else "ideal"
+        parity["headline"] = G.check_files(gname, cuts, rows, semantics=sem, hashed=head_hashed)
+        if hcuts is not None:
+            parity["headline_hashed"] = G.check_files(gname, hcuts, rows, semantics=sem, hashed=True)
+    ranks = d.gather({"rank": d.rank, "device": dev_id, "files": int(lens.size), "bytes": span,
+                      "ms_per_step": round(dt / max(args.steps, 1) * 1e3, 4), "scan_ms": round(scan_ms, 4),
+                      "scan_frac": round(achieved / HBM_PEAK_GBS, 4), "parity": parity})
+    if world > 1:
+        for key in ("headline", "headline_hashed"):
+            ps = [r["parity"].get(key) for r in ranks if r["parity"].get(key)]
+            if ps:
+                parity[key] = {"files": sum(p.get("files", 0) for p in ps),
+                               "chunks": sum(p.get("chunks", 0) for p in ps),
+                               "mismatches": sum(p.get("mismatches", 0) for p in ps),
+                               "fixture": ps[0].get("fixture"), "ranks": len(ps)}
 
     cpu = None
     # dense1 is one periodic file: the literal loop would memmove 16 MiB per 64-byte chunk
@@ -687,47 +628,61 @@ def main(argv=None):
         cpu = cpu_baseline(dbuf, offs, lens, cuts, hcuts, args.cpu_sample_gib, skip=skip)
         if skip is not None:
             cpu["sample"] += "; periodic files over 1 MiB skipped (the literal loop's memmove per 64-byte chunk)"
-    for h, b in slots:
-        b.free()
-        h.close()
 
+    out = {
+        "metric": METRIC_HASHED if head_hashed else METRIC, "value": round(value, 3), "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4),
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u8",
+        "data": ("synthetic: one random 32 MiB base (corpus file DEDUP_BASE_INDEX, generated in HBM) and its "
+                 "single-edit variants, copied together in HBM" if args.workload == "dedup" else
+                 "synthetic: per-file xorshift64 corpus generated in HBM (SURVEY §8d seed rule)"
+                 + ("; adversarial files uploaded from the host (dense_kind)" if args.workload == "dense" else "")),
+        "config": {
+            "workload": f"{args.workload}: {desc}", "files_per_gpu": int(lens.size),
+            "bytes_per_gpu": span, "total_files": int(sizes.size), "total_bytes": int(total_bytes),
+            "chunk_bits": 20, "max_chunk": syncr_amd.MAX_CHUNK_SIZE, "read_cap": read_cap, "mode": args.mode,
+            "parallelism": (f"file-sharded x{world} (LPT, {args.scaling} scaling), one process + HIP stream per "
+                            "GPU, no collective"),
+            "launcher": os.environ.get("SYNCR_BENCH_LAUNCHER", "torchrun/env" if world > 1 else "none"),
+            "device_map": args.device_map or "device = LOCAL_RANK",
+            "warmup_fetch": f"results fetched after warm-up step {1 if args.fetch_at == 'first' else args.warmup} "
+                            f"of {args.warmup}",
+            "slots_agree_rank0": slots_agree,
+            "cuts_rank0": ncuts, "coverage_ok_rank0": covered,
+            "candidates_rank0": int(stats["candidates"]), "dense_tiles_rank0": int(stats["dense_tiles"]),
+            "engine": engine_info,
+        },
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "pipelined": pipelined,
+        "sustained": sustained,
+        "hashed": hashed,
+        "parity": parity,
+    }
+    if world > 1:
+        loads = [r["bytes"] for r in ranks]
+        out["ranks"] = [{k: r[k] for k in ("rank", "device", "files", "bytes", "ms_per_step", "scan_ms",
+                                           "scan_frac")} for r in ranks]
+        out["load_balance"] = {"max_over_mean_bytes": round(max(loads) / (sum(loads) / len(loads)), 5),
+                               "max_over_mean_ms": round(max(r["ms_per_step"] for r in ranks) /
+                                                         (sum(r["ms_per_step"] for r in ranks) / len(ranks)), 5)}
+    if args.workload == "dedup":
+        plan = dedup_plan()
+        out["config"]["dedup"] = L.dedup_stability(cuts, [plan[int(i) % len(plan)] for i in idx.tolist()])
+    if args.workload == "dense":
+        kinds = np.array([dense_kind(int(i)) for i in idx.tolist()])
+        out["config"]["adversarial_bytes_frac"] = {
+            "periodic64": round(float(lens[kinds == 1].sum()) / max(span, 1), 4),
+            "constant": round(float(lens[kinds == 2].sum()) / max(span, 1), 4)}
+    if world == 1 and not args.no_legs:
+        out["_slots"] = slots
+        run_legs(args, dev_id, dbuf, offs, lens, idx, span, out)
+    else:
+        for h, b in slots:
+            b.free()
+            h.close()
     if d.rank == 0:
-        out = {
-            "metric": METRIC_HASHED if head_hashed else METRIC, "value": round(value, 3), "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": ("synthetic: one random 32 MiB base (numpy PCG64, seed 31337) and its single-edit variants, "
-                     "uploaded from the host" if args.workload == "dedup" else
-                     "synthetic: per-file xorshift64 corpus generated in HBM (SURVEY §8d seed rule)"
-                     + ("; adversarial files uploaded from the host (dense_kind)" if args.workload == "dense" else "")),
-            "config": {
-                "workload": f"{args.workload}: {desc}", "files_per_gpu": int(lens.size),
-                "bytes_per_gpu": span, "total_bytes": int(total_bytes), "chunk_bits": 20,
-                "max_chunk": syncr_amd.MAX_CHUNK_SIZE, "read_cap": read_cap, "mode": args.mode,
-                "parallelism": f"file-sharded x{world} (LPT), one process + HIP stream per GPU, no collective",
-                "launcher": os.environ.get("SYNCR_BENCH_LAUNCHER", "torchrun/env" if world > 1 else "none"),
-                "device_map": args.device_map or "device = LOCAL_RANK",
-                "warmup_fetch": f"results fetched after warm-up step {1 if args.fetch_at == 'first' else args.warmup} "
-                                f"of {args.warmup}",
-                "slots_agree_rank0": slots_agree,
-                "cuts_rank0": ncuts, "coverage_ok_rank0": covered,
-                "candidates_rank0": int(stats["candidates"]), "dense_tiles_rank0": int(stats["dense_tiles"]),
-                "engine": engine_info,
-            },
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            "pipelined": pipelined,
-            "sustained": sustained,
-            "hashed": hashed,
-        }
-        if args.workload == "dedup":
-            out["config"]["dedup"] = dedup_stability(cuts, idx)
-        if args.workload == "dense":
-            kinds = np.array([dense_kind(int(i)) for i in idx.tolist()])
-            out["config"]["adversarial_bytes_frac"] = {
-                "periodic64": round(float(lens[kinds == 1].sum()) / max(span, 1), 4),
-                "constant": round(float(lens[kinds == 2].sum()) / max(span, 1), 4)}
         print(json.dumps(out), flush=True)
     d.close()
     return 0

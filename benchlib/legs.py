@@ -1,0 +1,402 @@
+"""GPU legs of bench.py outside its timed headline region, and of smoke():
+parity of the product HIP path against committed golden fixtures and the CPU
+oracle, and the single-GPU BASELINE configs other than the headline.
+
+Every leg runs the product library (syncr_amd -> libsyncr_cdc.so); the oracle
+(oracle/) is only the checker, exactly as in bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import numpy as np
+
+from benchlib import golden as G
+from benchlib import workloads as WL
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+M = 1 << 20
+
+
+def _tests_path():
+    t = os.path.join(G.ROOT, "tests")
+    if t not in sys.path:
+        sys.path.insert(0, t)
+
+
+def time_steps(ch, ptr: int, span: int, steps: int, warmup: int, hashed: bool = False) -> dict:
+    """K one-in-flight steps after W warm-up steps (results fetched after the
+    first), wall clock bracketed by device synchronisation; the scan kernel's
+    mean time from HIP events on its stream; then a few steps with every phase
+    bracketed by events (outside the timed steps)."""
+    ch.launch(ptr, hashed=hashed)
+    ch.fetch(hashed=hashed)
+    for _ in range(max(warmup - 1, 0)):
+        ch.launch(ptr, hashed=hashed)
+    ch.synchronize()
+    ch.set_timing(True, scan_only=True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ch.launch(ptr, hashed=hashed)
+    ch.synchronize()
+    dt = (time.perf_counter() - t0) / max(steps, 1)
+    kms, nl = ch.kernel_times()
+    ch.set_timing(False)
+    ch.set_timing(True)
+    for _ in range(min(steps, 5)):
+        ch.launch(ptr, hashed=hashed)
+    ch.synchronize()
+    pms, pn = ch.kernel_times()
+    ch.set_timing(False)
+    scan_ms = kms[0] / max(nl, 1)
+    out = {"value": round(span / dt / 2**30, 3), "unit": "GiB/s", "ms_per_step": round(dt * 1e3, 4),
+           "scan_ms": round(scan_ms, 4),
+           "scan_frac": round(span / (scan_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if scan_ms > 0 else None,
+           "dense_ms": round(pms[1] / max(pn, 1), 4), "resolve_ms": round(pms[2] / max(pn, 1), 4)}
+    if hashed:
+        out["hash_ms"] = round(pms[3] / max(pn, 1), 4)
+    return out
+
+
+# --------------------------------------------------------------------------
+# parity legs against fixtures / the oracle (small inputs)
+# --------------------------------------------------------------------------
+def kat_leg(device: int = 0) -> dict:
+    """Every case of tests/golden/kat_cases.json (SURVEY App. A known answers,
+    tests/chunking_test.rs inputs, random data at bits 8..24 and read caps, and
+    the adversarial inputs where skipping the chunk-head fix-up changes the cuts
+    -- a fresh Bup per chunk, file_operations.rs:748) through the product's
+    host entry point, cut ends compared with the fixture; each case's chunks
+    are also hashed on the GPU and checked against the BLAKE3 oracle."""
+    import syncr_amd
+    from oracle import oracle as O
+    _tests_path()
+    from golden_inputs import make_input
+    cases = G.load_json("kat_cases.json")["cases"]
+    handles: dict = {}
+    bad, hbad, nhash, names = 0, 0, 0, []
+    try:
+        for c in cases:
+            key = (c["chunk_bits"], c["max_chunk"], c["read_cap"])
+            if key not in handles:
+                handles[key] = syncr_amd.Chunker(*key, device=device)
+            ch = handles[key]
+            data = make_input(c["recipe"])
+            got = ch.batch_arrays(data, [0], [data.size], hashed=True)[0]
+            if G.ends_of(got).tolist() != list(c["ends"]):
+                bad += 1
+                names.append(c["name"])
+            if data.size <= 8 * M:
+                nhash += got.size
+                want = O.blake3_batch(data, got["offset"].astype(np.uint64), got["len"].astype(np.uint64),
+                                      nthreads=8) if got.size else np.zeros((0, 32), np.uint8)
+                hbad += int((got["hash"] != want).any(axis=1).sum()) if got.size else 0
+    finally:
+        for h in handles.values():
+            h.close()
+    out = {"cases": len(cases), "adversarial_head_cases": sum(c["name"].startswith("adversarial_head")
+                                                              for c in cases),
+           "mismatches": bad, "chunk_hashes_checked": nhash, "hash_mismatches": hbad,
+           "fixture": "tests/golden/kat_cases.json"}
+    if names:
+        out["failed"] = names[:8]
+    return out
+
+
+def blake3_vectors_leg(device: int = 0) -> dict:
+    """The official BLAKE3 vectors (tests/golden/blake3_vectors.json), each input
+    one chunk (chunk_bits 31, no read cap), hashed by the product's GPU hasher."""
+    import syncr_amd
+    v = G.load_json("blake3_vectors.json")
+    lens = np.array([n for n, _ in v["cases"]], np.uint64)
+    offs = np.zeros_like(lens)
+    pos = 0
+    for i, n in enumerate(lens.tolist()):
+        offs[i] = pos
+        pos += n + 13                           # unaligned file starts
+    buf = np.zeros(max(pos, 1), np.uint8)
+    for o, n in zip(offs.tolist(), lens.tolist()):
+        buf[o:o + n] = (np.arange(n) % 251).astype(np.uint8)
+    with syncr_amd.Chunker(31, 1 << 31, 0, device=device) as ch:
+        got = ch.batch_arrays(buf, offs, lens, hashed=True)
+    bad = 0
+    for (n, want), cuts in zip(v["cases"], got):
+        if n == 0:
+            bad += cuts.size != 0
+        else:
+            bad += not (cuts.size == 1 and cuts["hash"][0].tobytes().hex() == want)
+    return {"cases": len(v["cases"]), "mismatches": bad, "fixture": "tests/golden/blake3_vectors.json"}
+
+
+def dense_subset_files() -> list[np.ndarray]:
+    """Adversarial files after the reference's own test data: constant bytes
+    (tests/chunking_test.rs:95-108; 50 MiB of 'A' and 100 000 x 'X',
+    tests/protocol_list_test.rs:360-400, scaled), and 64-byte periodic data
+    (a candidate every 64 bytes: dense scan tiles, chained cuts, and files
+    long enough to be walked split)."""
+    pat = WL.periodic_pattern()
+    rng = np.random.default_rng(77)
+    glitchy = np.resize(pat, 6 * M + 5)
+    for g in rng.integers(0, glitchy.size - 4096, 8).tolist():
+        glitchy[g: g + int(rng.integers(1, 3000))] = rng.integers(0, 256, 1, dtype=np.uint8)
+    return [np.resize(pat, 5 * M + 3), np.full(5 * M, ord("A"), np.uint8), np.resize(pat, 2 * M),
+            np.full(100000, ord("X"), np.uint8), glitchy, np.resize(pat, 700 * 1024 + 11),
+            np.full(20 * M + 7, 0xAB, np.uint8), rng.integers(0, 256, 3 * M, dtype=np.uint8),
+            np.resize(pat, 64 * 1024), np.resize(np.roll(pat, 17), 4 * M + 1)]
+
+
+def dense_subset_leg(device: int = 0) -> dict:
+    """dense_subset_files() through the product path in both semantics, each
+    twice (the second launch walks long files split, once the first fetch has
+    seen their candidate density), against the oracle."""
+    import syncr_amd
+    from oracle import oracle as O
+    files = dense_subset_files()
+    lens = np.array([f.size for f in files], np.uint64)
+    offs = WL.offsets_of(lens)
+    buf = np.concatenate(files)
+    out = {"files": len(files), "bytes": int(lens.sum())}
+    bad = 0
+    for sem, cap in (("production", syncr_amd.TOKIO_READ_CAP), ("ideal", 0)):
+        want = [(O.chunk_production_window(f) if cap else O.chunk_ideal(f)).tolist() for f in files]
+        with syncr_amd.Chunker(read_cap=cap, device=device) as ch:
+            for rep in range(2):
+                got = ch.batch_arrays(buf, offs, lens)
+                bad += sum(G.ends_of(g).tolist() != w for g, w in zip(got, want))
+            out[f"{sem}_chunks"] = int(sum(g.size for g in got))
+            out[f"{sem}_dense_tiles"] = int(ch.last_stats()["dense_tiles"])
+            out[f"{sem}_split"] = ch.split_stats()
+    out["mismatches"] = bad
+    out["checked"] = "oracle (literal loops; orc_chunk_production_window for production), both semantics, 2 launches each"
+    return out
+
+
+# --------------------------------------------------------------------------
+# single-GPU BASELINE configs beside the headline (each with its parity)
+# --------------------------------------------------------------------------
+def uniform1k_leg(device: int, steps: int, warmup: int) -> dict:
+    """1024 x 1 MiB files generated in HBM, one batch;
+    parity: the committed full cut lists (tests/golden/corpus_uniform_1024x1MiB.json)."""
+    import syncr_amd
+    g = G.load_json("corpus_uniform_1024x1MiB.json")
+    lens = np.full(int(g["files"]), int(g["file_len"]), np.uint64)
+    offs = WL.offsets_of(lens)
+    span = int(lens.sum())
+    with syncr_amd.Chunker(device=device) as ch:
+        b = syncr_amd.DeviceBuffer(ch, span)
+        try:
+            b.gen_corpus(offs, lens)
+            ch.plan(offs, lens, span)
+            out = time_steps(ch, b.ptr, span, steps, warmup)
+            cuts = ch.fetch()
+        finally:
+            b.free()
+    bad = sum(G.ends_of(c).tolist() != e for c, e in zip(cuts, g["ends"]))
+    out.update({"config": "SURVEY §8d config 2: 1024 x 1 MiB random files, 1 GiB, production semantics",
+                "parity": {"files": len(cuts), "chunks": int(sum(c.size for c in cuts)), "mismatches": int(bad),
+                           "fixture": "tests/golden/corpus_uniform_1024x1MiB.json (every cut)"}})
+    return out
+
+
+def build_dedup(ch, dbuf, offs, plan) -> None:
+    """The dedup corpus on the device: the base is corpus file DEDUP_BASE_INDEX
+    (syncr_cdc_gen_corpus), each variant is copied together from base pieces and
+    its edit's bytes (syncr_cdc_memcpy_d2d): no 32 GiB host upload."""
+    import syncr_amd
+    base = syncr_amd.DeviceBuffer(ch, WL.DEDUP_BASE)
+    ins_all = np.concatenate([e[3] for e in plan])
+    ins_off = WL.offsets_of(np.array([e[3].size for e in plan], np.uint64))
+    ins = syncr_amd.DeviceBuffer(ch, max(int(ins_all.size), 16))
+    try:
+        base.gen_corpus(np.zeros(1, np.uint64), np.array([WL.DEDUP_BASE], np.uint64),
+                        indices=np.array([WL.DEDUP_BASE_INDEX], np.uint64))
+        ins.upload(ins_all)
+        for j, e in enumerate(plan):
+            dst = int(offs[j])
+            for src, o, n in WL.dedup_pieces(e):
+                sp = base.ptr + o if src == "base" else ins.ptr + int(ins_off[j]) + o
+                dbuf.copy_from(sp, n, dst)
+                dst += n
+        ch.synchronize()
+    finally:
+        base.free()
+        ins.free()
+
+
+def dedup_stability(cuts, plan) -> dict:
+    """Share of the base file's cut offsets each variant keeps (offsets past the
+    edit shifted back), and a chunk-level dedup ratio."""
+    from oracle import oracle as O
+    base, _ = O.corpus_fill_threads(np.array([WL.DEDUP_BASE], np.uint64), np.array([WL.DEDUP_BASE_INDEX], np.uint64))
+    base_cuts = set(O.chunk_production(base).astype(np.int64).tolist())
+    kept = []
+    for c, e in zip(cuts, plan):
+        pos, delta = e[1], WL.dedup_shift(e)
+        ends = G.ends_of(c).astype(np.int64).tolist()
+        adj = {x - delta if x > pos else x for x in ends}
+        kept.append(len(adj & base_cuts) / max(len(base_cuts), 1))
+    return {"base_cuts": len(base_cuts), "kept_median": round(float(np.median(kept)), 4),
+            "kept_min": round(float(np.min(kept)), 4),
+            "note": "share of the base file's cut offsets present in each variant (offsets past the edit shifted back)"}
+
+
+def dedup_leg(device: int, steps: int, warmup: int) -> dict:
+    """SURVEY §8d config 5 (~32 GiB, one batch), built on the device; parity of
+    every variant's cuts and chunk hashes against the golden digests
+    (tests/golden/dedup_digests.npz), boundary stability."""
+    import syncr_amd
+    plan = WL.dedup_plan()
+    lens = np.array([e[4] for e in plan], np.uint64)
+    offs = WL.offsets_of(lens)
+    span = int(lens.sum())
+    with syncr_amd.Chunker(device=device) as ch:
+        b = syncr_amd.DeviceBuffer(ch, span)
+        try:
+            t0 = time.perf_counter()
+            build_dedup(ch, b, offs, plan)
+            t_build = time.perf_counter() - t0
+            ch.plan(offs, lens, span)
+            out = time_steps(ch, b.ptr, span, steps, warmup)
+            cuts = ch.fetch()
+            ch.launch(b.ptr, hashed=True)
+            hcuts = ch.fetch(hashed=True)
+        finally:
+            b.free()
+    rows = np.arange(len(plan))
+    out.update({"config": "SURVEY §8d config 5: 1000 single-edit variants of one 32 MiB random base "
+                          f"({span / 2**30:.2f} GiB), production semantics; built in HBM in {t_build:.2f} s",
+                "parity": G.check_files("dedup", cuts, rows),
+                "parity_hashed": G.check_files("dedup", hcuts, rows, hashed=True),
+                "stability": dedup_stability(cuts, plan)})
+    return out
+
+
+def fill_dense(dbuf, offs, lens, idx) -> None:
+    """Overwrite the adversarial files of the dense workload (WL.dense_kind)."""
+    pat = WL.periodic_pattern()
+    for j in range(lens.size):
+        f = WL.dense_file(int(idx[j]), int(lens[j]), pat)
+        if f is not None and f.size:
+            dbuf.upload(f, offset=int(offs[j]))
+
+
+def dense_leg(device: int, steps: int, warmup: int) -> dict:
+    """The adversarial `dense` workload (zipf10k table; periodic files i%16==5,
+    constant files i%16==11) as one batch; parity of every file (cuts and chunk
+    hashes) against tests/golden/dense_digests.npz."""
+    import syncr_amd
+    lens = WL.zipf_sizes()
+    idx = np.arange(lens.size, dtype=np.uint64)
+    offs = WL.offsets_of(lens)
+    span = int(lens.sum())
+    with syncr_amd.Chunker(device=device) as ch:
+        b = syncr_amd.DeviceBuffer(ch, span)
+        try:
+            b.gen_corpus(offs, lens, indices=idx)
+            fill_dense(b, offs, lens, idx)
+            ch.plan(offs, lens, span)
+            out = time_steps(ch, b.ptr, span, steps, warmup)
+            cuts = ch.fetch()
+            out["split"] = ch.split_stats()
+            out["dense_tiles"] = int(ch.last_stats()["dense_tiles"])
+            out["candidates"] = int(ch.last_stats()["candidates"])
+            hashed = time_steps(ch, b.ptr, span, max(steps // 2, 3), 2, hashed=True)
+            hcuts = ch.fetch(hashed=True)
+        finally:
+            b.free()
+    kinds = np.array([WL.dense_kind(int(i)) for i in idx.tolist()])
+    out.update({"config": "adversarial: zipf10k table, periodic-64 files (i%16==5) and constant files (i%16==11)",
+                "adversarial_bytes_frac": {"periodic64": round(float(lens[kinds == 1].sum()) / span, 4),
+                                           "constant": round(float(lens[kinds == 2].sum()) / span, 4)},
+                "hashed": {k: hashed[k] for k in ("value", "ms_per_step", "hash_ms")},
+                "parity": G.check_files("dense", cuts, idx),
+                "parity_hashed": G.check_files("dense", hcuts, idx, hashed=True)})
+    return out
+
+
+def ideal_leg(dbuf, offs, lens, idx, device: int) -> dict:
+    """Ideal semantics (chunk_data, tests/chunking_test.rs:170-192: read_cap 0)
+    on the headline corpus already in HBM, every file against the golden ideal
+    digests."""
+    import syncr_amd
+    with syncr_amd.Chunker(read_cap=0, device=device) as ch:
+        ch.plan(offs, lens, int(lens.sum()))
+        ch.launch(dbuf.ptr)
+        cuts = ch.fetch()
+    return G.check_files("zipf10k", cuts, idx, semantics="ideal")
+
+
+def ingest_leg(host: np.ndarray, offs, lens, idx, device: int, reps: int = 2, multi_files: int = 2000) -> dict:
+    """End to end (north_star: the path starts and ends in host memory): the
+    zipf10k corpus's files in ordinary host memory -> syncr_ingest_submit
+    (copied into pinned staging) -> H2D -> scan + resolve + BLAKE3 -> one
+    ChunkInfo list per file back on the host, in submission order.  Every
+    file is checked against the golden digests (cuts and hashes).  Then the
+    multi-device front end (syncr_ingest_open_multi, devices {d, d}) on the
+    first `multi_files` files, checked the same way."""
+    import syncr_amd
+    files = [host[int(o): int(o + n)] for o, n in zip(offs.tolist(), lens.tolist())]
+    span = int(lens.sum())
+    res: dict = {}
+
+    def on_file(tag, status, a):
+        res[tag] = (status, a)
+
+    out = {}
+    with syncr_amd.Ingest(device=device, batch_bytes=256 << 20, depth=3, copy_threads=16, on_file=on_file) as g:
+        best = None
+        for _ in range(reps):
+            res.clear()
+            t0 = time.perf_counter()
+            for i, f in enumerate(files):
+                g.submit(f, i)
+            g.flush()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        st = g.stats()
+    got = [res[i][1] for i in range(len(files))]
+    out.update({"value": round(span / best / 2**30, 3), "unit": "GiB/s", "seconds": round(best, 4),
+                "bytes": span, "files": len(files), "batches_per_pass": st["batches"] // reps,
+                "path": "syncr_ingest_submit from pageable host memory (16 copy threads into pinned staging, "
+                        "256 MiB batches, depth 3) -> hipMemcpyAsync H2D -> chunk + BLAKE3 -> per-file "
+                        "ChunkInfo callbacks; best of %d passes" % reps,
+                "status_nonzero": int(sum(res[i][0] != 0 for i in range(len(files)))),
+                "parity": G.check_files("zipf10k", got, idx, hashed=True)})
+    nm = min(multi_files, len(files))
+    res.clear()
+    with syncr_amd.Ingest(devices=[device, device], batch_bytes=64 << 20, depth=2, copy_threads=8,
+                          on_file=on_file) as g:
+        for i in range(nm):
+            g.submit(files[i], i)
+        g.flush()
+        ds = g.device_stats()
+    got = [res[i][1] for i in range(nm)]
+    out["multi_device"] = {"devices": [device, device], "per_device_files": [d["files"] for d in ds],
+                           "parity": G.check_files("zipf10k", got, idx[:nm], hashed=True)}
+    return out
+
+
+def ingest_multi_leg(device: int = 0, max_file: int = 4 * M, nfiles: int = 1500) -> dict:
+    """smoke()-sized check of the multi-device ingest front end
+    (syncr_ingest_open_multi, devices {d, d}): the zipf10k files among the first
+    `nfiles` that are at most `max_file` bytes, generated on the host (the
+    corpus's xorshift rule), submitted from host memory, chunked + hashed, each
+    compared with the golden digests."""
+    import syncr_amd
+    from oracle import oracle as O
+    sizes = WL.zipf_sizes()
+    rows = np.array([i for i in range(min(nfiles, sizes.size)) if int(sizes[i]) <= max_file], np.int64)
+    host, offs = O.corpus_fill_threads(sizes[rows], indices=rows.astype(np.uint64))
+    lens = sizes[rows]
+    res: dict = {}
+    with syncr_amd.Ingest(devices=[device, device], batch_bytes=16 << 20, depth=2, copy_threads=4,
+                          on_file=lambda t, s, a: res.__setitem__(t, a)) as g:
+        for j in range(rows.size):
+            g.submit(host[int(offs[j]): int(offs[j] + lens[j])], j)
+        g.flush()
+        ds = g.device_stats()
+    got = [res[j] for j in range(rows.size)]
+    return {"devices": [device, device], "per_device_files": [d["files"] for d in ds],
+            "parity": G.check_files("zipf10k", got, rows, hashed=True)}

@@ -47,6 +47,8 @@ extern "C" {
 #define SYNCR_CDC_FLAG_RESOLVE_LANE 1u    /* one lane per file instead of one wave */
 #define SYNCR_CDC_FLAG_RESOLVE_NOBURST 2u /* wave resolve without the chained-hop burst */
 #define SYNCR_CDC_FLAG_RESOLVE_NOSPLIT 4u /* wave resolve without split walks of long files */
+#define SYNCR_CDC_FLAG_SPLIT_NOWAIT 8u    /* testing: split-walk workers give up at once, so
+                                             every file walker walks its whole file itself */
 typedef struct syncr_cdc_params {
     uint32_t chunk_bits; /* CHUNK_BITS, 1..31 (default 20; reference validates 8..32) */
     uint32_t flags;      /* 0, or SYNCR_CDC_FLAG_* (other bits: SYNCR_CDC_EINVAL)     */
@@ -219,8 +221,10 @@ void syncr_ingest_close(syncr_ingest *g);
  * `path` (NULL = in memory only) that records them in its header; opening a log
  * written under other parameters gives SYNCR_CDC_EINVAL, a file that is not a
  * cache log SYNCR_CDC_EIO, a log locked by another open handle SYNCR_CDC_EBUSY.
- * An empty file (or one torn while its header was written) is a new cache; a
- * torn tail is dropped on open; a failed append is rolled back and makes later
+ * An empty file (or one torn while its header was written) is a new cache, and
+ * so is a log of the ABI-v2 format (magic SYNCRCC1, which did not record the
+ * parameters, so none of its lists can be trusted): it is rewritten with the
+ * current header on open; a torn tail is dropped on open; a failed append is rolled back and makes later
  * puts fail with SYNCR_CDC_EIO.  get: 0 on a hit, SYNCR_CDC_ENOENT on a miss,
  * SYNCR_CDC_ERANGE (n_out = needed) if cap is short.  Attached to an ingest
  * pipeline (same parameters, else SYNCR_CDC_EINVAL), submit_file serves
@@ -246,6 +250,9 @@ int32_t syncr_cdc_host_alloc_pinned(syncr_cdc *h, uint64_t bytes, void **ptr);
 int32_t syncr_cdc_host_free_pinned(syncr_cdc *h, void *ptr);
 int32_t syncr_cdc_memcpy_h2d(syncr_cdc *h, void *d_dst, const void *src, uint64_t bytes, void *stream);
 int32_t syncr_cdc_memcpy_d2h(syncr_cdc *h, void *dst, const void *d_src, uint64_t bytes, void *stream);
+/* Device-to-device copy on the handle's device (building device-resident
+ * batches from shared pieces, e.g. the dedup corpus of SURVEY.md §8d config 5). */
+int32_t syncr_cdc_memcpy_d2d(syncr_cdc *h, void *d_dst, const void *d_src, uint64_t bytes, void *stream);
 int32_t syncr_cdc_synchronize(syncr_cdc *h);
 void *syncr_cdc_stream(syncr_cdc *h);
 /* Fill [d_bytes + file_off[i], +file_len[i]) with corpus file number
@@ -272,6 +279,12 @@ int32_t syncr_cdc_kernel_times(syncr_cdc *h, double *ms3, uint64_t *launches);
 int32_t syncr_cdc_kernel_times_ex(syncr_cdc *h, double *ms, uint32_t n, uint64_t *launches);
 /* Diagnostics of the last fetched launch: [candidates, dense_tiles, tiles, overflow]. */
 int32_t syncr_cdc_last_stats(syncr_cdc *h, uint64_t *stats4);
+/* Split walks of long files (wave resolve) in the last fetched launch:
+ * [workers_launched (0/1), files_split, segments, segments walked by the split
+ * workers, segments adopted by their file's walker, worker give-ups].  A worker
+ * waits only for file walkers to publish their segments; it gives up (and
+ * leaves the rest to the file walkers, which never wait) after ~100 ms. */
+int32_t syncr_cdc_split_stats(syncr_cdc *h, uint64_t *stats6);
 /* Engine geometry: [run_bytes, tile_bytes, scan_grid, compute_units,
  * scan_blocks_per_cu, lds_bytes_per_scan_block, device, abi_version]. */
 int32_t syncr_cdc_get_info(const syncr_cdc *h, uint64_t *info8);

@@ -368,7 +368,8 @@ typedef struct {
     uint64_t nfiles;
     uint32_t bits;
     uint64_t max_chunk, read_cap;
-    int mode;               /* 0 production (literal), 1 ideal (literal), 2 closed form */
+    int mode;               /* 0 production (literal), 1 ideal (literal), 2 closed form,
+                               3 production without copy_within's memmove (window) */
     uint64_t next;          /* work queue (atomic) */
 } batch_t;
 
@@ -384,6 +385,8 @@ static void *batch_worker(void *arg) {
             c = orc_chunk_ideal(f, B->lens[i], B->bits, B->max_chunk, e, B->out_cap[i]);
         else if (B->mode == 2)
             c = orc_chunk_closed_form(f, B->lens[i], B->bits, B->max_chunk, B->read_cap, e, B->out_cap[i]);
+        else if (B->mode == 3)
+            c = orc_chunk_production_window(f, B->lens[i], B->bits, B->max_chunk, B->read_cap, e, B->out_cap[i]);
         else
             c = orc_chunk_production(f, B->lens[i], B->bits, B->max_chunk, B->read_cap, e, B->out_cap[i]);
         B->counts[i] = c;

@@ -27,7 +27,7 @@ CHUNK_BITS = 20                       # src/chunking.rs:7
 MAX_CHUNK_SIZE = (1 << 20) * 16       # src/chunking.rs:10-13
 TOKIO_READ_CAP = 2 * 1024 * 1024      # tokio DEFAULT_MAX_BUF_SIZE (Cargo.toml:29)
 
-MODE_PRODUCTION, MODE_IDEAL, MODE_CLOSED_FORM = 0, 1, 2
+MODE_PRODUCTION, MODE_IDEAL, MODE_CLOSED_FORM, MODE_PRODUCTION_WINDOW = 0, 1, 2, 3
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -174,9 +174,39 @@ def corpus_fill(lens, first_index: int = 0) -> tuple[np.ndarray, np.ndarray]:
     return buf[:total], offs
 
 
+def corpus_fill_threads(lens, indices=None, nthreads: int = 8) -> tuple[np.ndarray, np.ndarray]:
+    """corpus_fill with file j = corpus file indices[j] (default j), on threads."""
+    from concurrent.futures import ThreadPoolExecutor
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    idx = np.arange(lens.size, dtype=np.uint64) if indices is None else np.ascontiguousarray(indices, np.uint64)
+    offs = np.zeros_like(lens)
+    if lens.size:
+        offs[1:] = np.cumsum(lens)[:-1]
+    total = int(lens.sum())
+    buf = np.empty(max(total, 1), np.uint8)
+    L = lib()
+
+    def one(j):
+        o, n = offs[j:j + 1], lens[j:j + 1]
+        L.orc_corpus_fill(_p64(o), _p64(n), 1, int(idx[j]), _p8(buf))
+
+    order = np.argsort(-lens.astype(np.int64), kind="stable").tolist()
+    with ThreadPoolExecutor(nthreads) as ex:
+        list(ex.map(one, order))
+    return buf[:total], offs
+
+
 def fnv_ends(ends) -> int:
     e = np.ascontiguousarray(ends, dtype=np.uint64)
     return int(lib().orc_fnv_ends(_p64(e if e.size else np.zeros(1, np.uint64)), e.size))
+
+
+def fnv_hashes(hashes) -> int:
+    """FNV-1a-64 (orc_fnv_ends) over a file's chunk hashes, [n, 32] uint8, read
+    as 4 little-endian u64 words per hash: the per-file hash digest of the
+    golden corpus fixtures (tests/golden/make_corpus_digests.py)."""
+    h = np.ascontiguousarray(hashes, dtype=np.uint8).reshape(-1)
+    return fnv_ends(h.view("<u8") if h.size else np.zeros(0, np.uint64))
 
 
 def chunk_batch(base, offs, lens, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE,
@@ -206,7 +236,8 @@ def chunk_batch(base, offs, lens, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE,
         c = int(counts[i])
         if c > int(caps[i]):  # rare: re-run this file alone with exact capacity
             f = base[int(offs[i]): int(offs[i]) + int(lens[i])]
-            fn = {MODE_PRODUCTION: chunk_production, MODE_CLOSED_FORM: chunk_closed_form}.get(mode)
+            fn = {MODE_PRODUCTION: chunk_production, MODE_CLOSED_FORM: chunk_closed_form,
+                  MODE_PRODUCTION_WINDOW: chunk_production_window}.get(mode)
             out.append(chunk_ideal(f, bits, max_chunk) if mode == MODE_IDEAL else fn(f, bits, max_chunk, read_cap))
         else:
             out.append(ends[int(ob[i]): int(ob[i]) + c].copy())

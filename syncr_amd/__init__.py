@@ -45,9 +45,9 @@ EXPORTED_SYMBOLS = (
     "syncr_cdc_chunk_host", "syncr_cdc_chunk_batch_host", "syncr_cdc_plan", "syncr_cdc_launch",
     "syncr_cdc_fetch", "syncr_cdc_chunk_batch_device", "syncr_cdc_device_alloc",
     "syncr_cdc_device_free", "syncr_cdc_host_alloc_pinned", "syncr_cdc_host_free_pinned",
-    "syncr_cdc_memcpy_h2d", "syncr_cdc_memcpy_d2h", "syncr_cdc_synchronize", "syncr_cdc_stream",
+    "syncr_cdc_memcpy_h2d", "syncr_cdc_memcpy_d2h", "syncr_cdc_memcpy_d2d", "syncr_cdc_synchronize", "syncr_cdc_stream",
     "syncr_cdc_gen_corpus", "syncr_cdc_read_probe", "syncr_cdc_set_timing", "syncr_cdc_kernel_times",
-    "syncr_cdc_last_stats", "syncr_cdc_get_info",
+    "syncr_cdc_last_stats", "syncr_cdc_split_stats", "syncr_cdc_get_info",
     "syncr_cdc_chunk_host_hashed", "syncr_cdc_chunk_batch_host_hashed", "syncr_cdc_launch_hashed",
     "syncr_cdc_fetch_hashed", "syncr_cdc_kernel_times_ex",
     "syncr_cdc_format_chunks",
@@ -66,6 +66,7 @@ E_INVAL = -22
 FLAG_RESOLVE_LANE = 1       # exact alternative resolves (include/syncr_cdc.h SYNCR_CDC_FLAG_*)
 FLAG_RESOLVE_NOBURST = 2
 FLAG_RESOLVE_NOSPLIT = 4
+FLAG_SPLIT_NOWAIT = 8       # testing: split-walk workers give up at once
 FMT_LIST_LINES = 1      # LIST reply "C" lines (src/protocol/v3_server.rs:146-182)
 FMT_HASHCHUNKS = 2      # profile FileData "ch" array (src/types.rs:117-129)
 
@@ -138,6 +139,7 @@ def library():
             "syncr_cdc_host_free_pinned": ([_vp, _vp], _i32),
             "syncr_cdc_memcpy_h2d": ([_vp, _vp, _vp, _u64, _vp], _i32),
             "syncr_cdc_memcpy_d2h": ([_vp, _vp, _vp, _u64, _vp], _i32),
+            "syncr_cdc_memcpy_d2d": ([_vp, _vp, _vp, _u64, _vp], _i32),
             "syncr_cdc_synchronize": ([_vp], _i32),
             "syncr_cdc_stream": ([_vp], _vp),
             "syncr_cdc_gen_corpus": ([_vp, _vp, _vp, _vp, _vp, _u32, _u64, _vp], _i32),
@@ -145,6 +147,7 @@ def library():
             "syncr_cdc_set_timing": ([_vp, _i32], _i32),
             "syncr_cdc_kernel_times": ([_vp, ctypes.POINTER(ctypes.c_double), _pu64], _i32),
             "syncr_cdc_last_stats": ([_vp, _pu64], _i32),
+            "syncr_cdc_split_stats": ([_vp, _pu64], _i32),
             "syncr_cdc_get_info": ([_vp, _pu64], _i32),
             "syncr_cdc_chunk_host_hashed": ([_vp, _vp, _u64, _vp, _u64, _pu64], _i32),
             "syncr_cdc_chunk_batch_host_hashed": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u64, _vp, _pu64], _i32),
@@ -340,6 +343,13 @@ class Chunker:
         _check(library().syncr_cdc_last_stats(self._h, st), "syncr_cdc_last_stats")
         return {"candidates": st[0], "dense_tiles": st[1], "tiles": st[2], "flags": st[3]}
 
+    def split_stats(self) -> dict:
+        """Split walks of long files in the last fetched launch (syncr_cdc_split_stats)."""
+        st = (ctypes.c_uint64 * 6)()
+        _check(library().syncr_cdc_split_stats(self._h, st), "syncr_cdc_split_stats")
+        return dict(zip(("workers_launched", "files_split", "segments", "walked", "adopted", "giveups"),
+                        (int(x) for x in st)))
+
     def info(self) -> dict:
         v = (ctypes.c_uint64 * 8)()
         _check(library().syncr_cdc_get_info(self._h, v), "syncr_cdc_get_info")
@@ -381,6 +391,13 @@ class DeviceBuffer:
                                                   None), "memcpy_d2h")
             self._c.synchronize()
         return out[:n]
+
+    def copy_from(self, src_ptr: int, nbytes: int, offset: int = 0) -> None:
+        """Asynchronous device-to-device copy of nbytes at src_ptr to offset
+        (on the chunker's stream; synchronize() before reading the result)."""
+        if nbytes:
+            _check(library().syncr_cdc_memcpy_d2d(self._c.handle, self.ptr + offset, src_ptr, nbytes, None),
+                   "memcpy_d2d")
 
     def gen_corpus(self, offsets, lengths, first_index: int = 0, indices=None) -> None:
         """Synthetic corpus on the device: file i gets corpus file number

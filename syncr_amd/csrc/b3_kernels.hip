@@ -953,7 +953,8 @@ static hipError_t launch_leaf_v(int device, const uint8_t *d, const Tables &t, c
 #endif
 
 hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(ht.ctr, 0, B3C_WORDS * sizeof(uint64_t), s);
+    hipError_t e = hipSuccess;
+    if (!t.hzero) e = hipMemsetAsync(ht.ctr, 0, B3C_WORDS * sizeof(uint64_t), s);   // else: the resolve zeroed them
     if (e != hipSuccess) return e;
     if (!t.nfiles) return hipSuccess;
     hipLaunchKernelGGL(b3_items_kernel, dim3(ht.n_iblocks), dim3(256), 0, s, t, ht);

@@ -43,6 +43,9 @@
 namespace {
 
 constexpr char MAGIC[8] = {'S', 'Y', 'N', 'C', 'R', 'C', 'C', '2'};
+// the ABI-v2 log format: no parameter header, so its chunk lists cannot be
+// trusted under any parameters; such a log is a stale cache, started afresh
+constexpr char MAGIC_V1[8] = {'S', 'Y', 'N', 'C', 'R', 'C', 'C', '1'};
 constexpr size_t HDR = 32;              // MAGIC | chunk_bits u32 | flags u32 | max_chunk u64 | read_cap u64
 
 struct Entry {
@@ -85,6 +88,7 @@ struct syncr_cache {
     int fd = -1;
     uint64_t end = 0;                  // bytes of valid log (next record goes here)
     bool broken = false;               // a write failed: no more appends
+    bool upgraded = false;             // an old-format (SYNCRCC1) log was started afresh
     syncr_cdc_params params{};
     std::unordered_map<std::string, Entry> map;
     uint64_t records = 0;              // records in the log (live + superseded)
@@ -128,6 +132,12 @@ int32_t load(syncr_cache *c) {
     buf.resize(got);
     uint8_t want[HDR];
     header(c->params, want);
+    if (buf.size() >= 8 && memcmp(buf.data(), MAGIC_V1, 8) == 0) {        // stale format: a new cache
+        if (ftruncate(c->fd, 0) != 0 || !write_all(c->fd, want, HDR, 0) || fsync(c->fd) != 0) return SYNCR_CDC_EIO;
+        c->end = HDR;
+        c->upgraded = true;
+        return SYNCR_CDC_OK;
+    }
     if (buf.size() < HDR) {
         // empty or torn while the header was being written (a prefix of the
         // magic, or of our own header): a new cache

@@ -95,11 +95,18 @@ struct syncr_cdc {
     // seen that, so the common case launches no split workers at all.
     bool split_hint = false;
 
+    // two per-launch zeroed blocks (Tables::znext): launch k uses block zpar; the
+    // resolve of launch k zeroes the other one for launch k+1
+    uint32_t zpar = 0, zlast = 0;
+    bool zclean[2] = {false, false};
+
     // launch
     bool launched = false;
     const uint8_t *last_bytes = nullptr;
     hipStream_t last_stream = nullptr;
     uint64_t stats[4] = {0, 0, 0, 0};
+    bool split_launched = false;        // the last launch started split workers
+    uint64_t split_stats[6] = {0, 0, 0, 0, 0, 0};
 
     // host-path staging
     DevBuf stage;
@@ -131,7 +138,7 @@ int32_t validate_params(const syncr_cdc_params *p) {
     if (!p) return SYNCR_CDC_EINVAL;
     if (p->chunk_bits < 1 || p->chunk_bits > 31) return SYNCR_CDC_EINVAL;
     if (p->flags & ~(uint32_t)(SYNCR_CDC_FLAG_RESOLVE_LANE | SYNCR_CDC_FLAG_RESOLVE_NOBURST |
-                               SYNCR_CDC_FLAG_RESOLVE_NOSPLIT))
+                               SYNCR_CDC_FLAG_RESOLVE_NOSPLIT | SYNCR_CDC_FLAG_SPLIT_NOWAIT))
         return SYNCR_CDC_EINVAL;
     if (p->max_chunk < 1 || p->max_chunk > 0xffffffffull) return SYNCR_CDC_EINVAL;
     return SYNCR_CDC_OK;
@@ -167,6 +174,9 @@ uint32_t default_cut_cap(uint64_t len, uint32_t bits) {
 
 // the per-launch zeroed block: ctr[4] | nonempty[nwords] (u64) | super_cnt[nwords] (u32) | split[SPL_WORDS]
 size_t split_ctr_offset(const syncr_cdc *h) { return (16 + (size_t)h->nwords * 12 + 15) & ~size_t(15); }
+size_t zeroed_bytes(const syncr_cdc *h) { return split_ctr_offset(h) + SPL_WORDS * 4; }
+size_t zstride(const syncr_cdc *h) { return (zeroed_bytes(h) + 255) & ~size_t(255); }
+uint8_t *zblock(const syncr_cdc *h, uint32_t par) { return h->zeroed.as<uint8_t>() + par * zstride(h); }
 
 Tables make_tables(syncr_cdc *h) {
     Tables t{};
@@ -184,9 +194,10 @@ Tables make_tables(syncr_cdc *h) {
     t.cut_cap = h->cut_cap.as<uint32_t>();
     t.tile_meta = h->tile_meta.as<uint32_t>();
     t.slots = h->slots.as<uint2>();
-    t.ctr = h->zeroed.as<uint32_t>();
-    t.nonempty = reinterpret_cast<unsigned long long *>(h->zeroed.as<uint8_t>() + 16);
-    t.super_cnt = reinterpret_cast<uint32_t *>(h->zeroed.as<uint8_t>() + 16 + (size_t)h->nwords * 8);
+    uint8_t *zb = zblock(h, h->zpar);
+    t.ctr = reinterpret_cast<uint32_t *>(zb);
+    t.nonempty = reinterpret_cast<unsigned long long *>(zb + 16);
+    t.super_cnt = reinterpret_cast<uint32_t *>(zb + 16 + (size_t)h->nwords * 8);
     t.super_off = h->super_off.as<uint64_t>();
     t.dense_list = h->dense_list.as<uint32_t>();
     t.dense_cnt = h->dense_cnt.as<uint32_t>();
@@ -205,7 +216,10 @@ Tables make_tables(syncr_cdc *h) {
     t.seg_cap = h->seg_cap;
     t.segs = h->segs.as<SplitSeg>();
     t.seg_cuts = h->seg_cuts.as<DevCut>();
-    t.split = reinterpret_cast<uint32_t *>(h->zeroed.as<uint8_t>() + split_ctr_offset(h));
+    t.split = reinterpret_cast<uint32_t *>(zb + split_ctr_offset(h));
+    t.znext = reinterpret_cast<uint4 *>(zblock(h, h->zpar ^ 1u));
+    t.znext_vec = (uint32_t)(zstride(h) / 16);
+    t.hzero = nullptr;
     // SplitSeg records outlive a launch: a record is ready for this launch only
     // when its ready word holds this launch's id (records are zeroed when allocated)
     static std::atomic<uint32_t> epochs{0};
@@ -319,8 +333,6 @@ int32_t ensure_cand(syncr_cdc *h, uint64_t cap) {
     return ensure_split(h);
 }
 
-size_t zeroed_bytes(const syncr_cdc *h) { return split_ctr_offset(h) + SPL_WORDS * 4; }
-
 void drain_timing(syncr_cdc *h) {
     for (auto &pt : h->pending) {
         (void)hipEventSynchronize(pt.ev[pt.nev - 1]);
@@ -348,6 +360,7 @@ struct ScanOrder {
     std::mutex mu;
     const syncr_cdc *owner = nullptr;   // handle whose scan was enqueued last
     hipEvent_t ev = nullptr;            // its scan_done event
+    std::atomic<int> open{0};           // handles open on the device: ordering only when > 1
 };
 ScanOrder &scan_order(int device) {
     static std::mutex reg_mu;
@@ -364,18 +377,24 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     pt.nev = h->timing_scan_only ? 2 : h->hash_on ? 5 : 4;
     if (h->timing) {
         if (h->pending.size() >= 256) drain_timing(h);
-        for (int k = 0; k < pt.nev; k++) CHECK_HIP(hipEventCreate(&pt.ev[k]));
+        // timing only: no system-scope release (a cache writeback + invalidate per
+        // event would stall the queue and perturb the kernels being timed)
+        for (int k = 0; k < pt.nev; k++) CHECK_HIP(hipEventCreateWithFlags(&pt.ev[k], hipEventDisableSystemFence));
     }
-    CHECK_HIP(hipMemsetAsync(h->zeroed.p, 0, zeroed_bytes(h), s));
+    const uint32_t par = h->zpar;
+    if (!h->zclean[par]) CHECK_HIP(hipMemsetAsync(zblock(h, par), 0, zeroed_bytes(h), s));
+    h->zclean[par] = false;
+    if (h->hash_on && t.nfiles) t.hzero = h->hctr.as<uint64_t>();     // zeroed by the resolve
     ScanOrder &so = scan_order(h->device);
-    if (h->serial_scans) {
+    const bool order = h->serial_scans && so.open.load() > 1;          // another handle on this device
+    if (order) {
         std::lock_guard<std::mutex> g(so.mu);        // held: the owner cannot close its event meanwhile
         if (so.owner && so.owner != h) CHECK_HIP(hipStreamWaitEvent(s, so.ev, 0));
     }
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[0], s));
     CHECK_HIP(launch_scan(h->geom, h->scan_grid, d_bytes, kp, t, s));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[1], s));
-    if (h->serial_scans) {
+    if (order) {
         std::lock_guard<std::mutex> g(so.mu);
         CHECK_HIP(hipEventRecord(h->scan_done, s));
         so.owner = h;
@@ -384,9 +403,13 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     // an event record costs ~6 us of queue idle: the scan-only mode records
     // just the two around the scan
     const bool phases = h->timing && !h->timing_scan_only;
-    CHECK_HIP(launch_post(d_bytes, kp, t, s, nullptr));
+    CHECK_HIP(launch_post(d_bytes, kp, t, s, scan_dense_inline(h->geom, kp)));
     if (phases) CHECK_HIP(hipEventRecord(pt.ev[2], s));
     CHECK_HIP(launch_resolve(d_bytes, kp, t, s));
+    h->split_launched = resolve_splits(kp, t);
+    if (t.nfiles) h->zclean[par ^ 1u] = true;        // the resolve zeroed the next launch's block
+    h->zlast = par;
+    h->zpar = par ^ 1u;
     if (phases) CHECK_HIP(hipEventRecord(pt.ev[3], s));
     if (h->hash_on) {
         CHECK_HIP(launch_hash(h->device, d_bytes, t, make_hash_tables(h), s));
@@ -453,6 +476,12 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     h->device = device;
     h->params = prm;
     h->kp = make_kparams(prm);
+    {   // split workers wait at most ~100 ms of wall clock for file walkers (cdc_kernels.hip split_next)
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
+            khz = 100000;
+        h->kp.split_patience = (prm.flags & SYNCR_CDC_FLAG_SPLIT_NOWAIT) ? 0ull : 100ull * (uint64_t)khz;
+    }
 #ifdef SYNCR_CDC_DEV
     // Development library only (libsyncr_cdc_dev.so, used by tools/): variants
     // and timing-only ablations chosen by environment variables.  The product
@@ -504,11 +533,12 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
         delete h;
         return SYNCR_CDC_EIO;
     }
-    if (hipEventCreateWithFlags(&h->scan_done, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&h->scan_done, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
         (void)hipStreamDestroy(h->stream);
         delete h;
         return SYNCR_CDC_EIO;
     }
+    scan_order(device).open++;
     *out = h;
     return SYNCR_CDC_OK;
 }
@@ -525,6 +555,7 @@ void syncr_cdc_close(syncr_cdc *h) {
             so.owner = nullptr;
             so.ev = nullptr;
         }
+        so.open--;
         (void)hipEventDestroy(h->scan_done);
     }
     DevBuf *bufs[] = {&h->fstart, &h->foff, &h->flen, &h->order, &h->cut_base, &h->cut_cap,
@@ -593,7 +624,9 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         CHECK_HIP(h->counts.ensure(std::max<size_t>(nfiles, 1) * 8));
         CHECK_HIP(h->tile_meta.ensure(std::max<size_t>(h->ntiles, 1) * 4));
         CHECK_HIP(h->slots.ensure(std::max<size_t>(h->ntiles, 1) * LISTCAP * sizeof(uint2)));
-        CHECK_HIP(h->zeroed.ensure(zeroed_bytes(h)));
+        CHECK_HIP(h->zeroed.ensure(2 * zstride(h)));
+        h->zclean[0] = h->zclean[1] = false;
+        h->zpar = h->zlast = 0;
         CHECK_HIP(h->super_off.ensure(((size_t)h->nwords + 1) * 8));
         // dense tiles are rare (adversarial data); grow on demand in fetch()
         uint32_t dcap = std::max<uint32_t>(64u, h->ntiles / 256u);
@@ -679,7 +712,7 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
         for (int attempt = 0; attempt < 8; attempt++) {
             CHECK_HIP(hipStreamSynchronize(h->last_stream));
             uint32_t ctr[4];
-            CHECK_HIP(hipMemcpy(ctr, h->zeroed.p, 16, hipMemcpyDeviceToHost));
+            CHECK_HIP(hipMemcpy(ctr, zblock(h, h->zlast), 16, hipMemcpyDeviceToHost));
             const uint64_t ncand = (uint64_t)ctr[CTR_CANDS_LO] | ((uint64_t)ctr[CTR_CANDS_HI] << 32);
             // for the next launch (also a re-run below): >= 64 Ki candidates at >= 1
             // per 16 KiB (random data: ~1 per MiB at chunk_bits 20)
@@ -695,7 +728,7 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
 #ifdef SYNCR_CDC_DEV
             if (getenv("SYNCR_CDC_DEBUG_FETCH")) {
                 uint32_t sp[SPL_WORDS];
-                CHECK_HIP(hipMemcpy(sp, h->zeroed.as<uint8_t>() + split_ctr_offset(h), sizeof sp, hipMemcpyDeviceToHost));
+                CHECK_HIP(hipMemcpy(sp, zblock(h, h->zlast) + split_ctr_offset(h), sizeof sp, hipMemcpyDeviceToHost));
                 fprintf(stderr, "fetch attempt %d: flags %u ncand %llu dense %u cand_cap %llu dense_cap %u seg_cap %u | "
                         "pub %u split %u reserved %u head %u done %u | counts",
                         attempt, ctr[CTR_FLAGS], (unsigned long long)ncand, ctr[CTR_DENSE],
@@ -738,6 +771,17 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
             h->stats[1] = ctr[CTR_DENSE];
             h->stats[2] = h->ntiles;
             h->stats[3] = ctr[CTR_FLAGS];
+            {
+                uint32_t sp[SPL_WORDS];
+                CHECK_HIP(hipMemcpy(sp, zblock(h, h->zlast) + split_ctr_offset(h), sizeof sp,
+                                    hipMemcpyDeviceToHost));
+                h->split_stats[0] = h->split_launched ? 1u : 0u;
+                h->split_stats[1] = sp[SPL_PUB64 + 1];          // split files (high half of the 64-bit count)
+                h->split_stats[2] = std::min<uint32_t>(sp[SPL_RESERVED], h->seg_cap);
+                h->split_stats[3] = sp[SPL_WALKED];
+                h->split_stats[4] = sp[SPL_ADOPTED];
+                h->split_stats[5] = sp[SPL_GIVEUP];
+            }
             uint64_t total = 0;
             for (uint32_t i = 0; i < h->nfiles; i++) total += counts[i];
             if (per_file_count)
@@ -892,6 +936,14 @@ int32_t syncr_cdc_memcpy_d2h(syncr_cdc *h, void *dst, const void *d_src, uint64_
     return SYNCR_CDC_OK;
 }
 
+int32_t syncr_cdc_memcpy_d2d(syncr_cdc *h, void *d_dst, const void *d_src, uint64_t bytes, void *stream) {
+    if (!h || (bytes && (!d_dst || !d_src))) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    if (bytes) CHECK_HIP(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, s));
+    return SYNCR_CDC_OK;
+}
+
 int32_t syncr_cdc_synchronize(syncr_cdc *h) {
     if (!h) return SYNCR_CDC_EINVAL;
     CHECK_HIP(hipSetDevice(h->device));
@@ -971,8 +1023,8 @@ int32_t syncr_cdc_read_probe(syncr_cdc *h, const uint8_t *d_bytes, uint64_t byte
     double best = 1e30, sum = 0;
     do {
         if ((e = sink.ensure((size_t)grid * 4)) != hipSuccess) break;
-        if ((e = hipEventCreate(&e0)) != hipSuccess) break;
-        if ((e = hipEventCreate(&e1)) != hipSuccess) break;
+        if ((e = hipEventCreateWithFlags(&e0, hipEventDisableSystemFence)) != hipSuccess) break;
+        if ((e = hipEventCreateWithFlags(&e1, hipEventDisableSystemFence)) != hipSuccess) break;
         if ((e = launch_read_probe(d_bytes, bytes, nt != 0, grid, sink.as<uint32_t>(), h->stream)) != hipSuccess) break;
         for (uint32_t r = 0; r < reps && e == hipSuccess; ++r) {
             if ((e = hipEventRecord(e0, h->stream)) != hipSuccess) break;
@@ -1020,6 +1072,12 @@ int32_t syncr_cdc_kernel_times_ex(syncr_cdc *h, double *ms, uint32_t n, uint64_t
     drain_timing(h);
     for (uint32_t k = 0; k < n; k++) ms[k] = k < (uint32_t)NPHASE ? h->ms[k] : 0.0;
     if (launches) *launches = h->timed_launches;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_split_stats(syncr_cdc *h, uint64_t *stats6) {
+    if (!h || !stats6) return SYNCR_CDC_EINVAL;
+    for (int k = 0; k < 6; k++) stats6[k] = h->split_stats[k];
     return SYNCR_CDC_OK;
 }
 

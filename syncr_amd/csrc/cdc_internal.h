@@ -78,6 +78,8 @@ struct KParams {
     uint32_t resolve_lane;  // 1: lane-per-file resolve (SYNCR_CDC_FLAG_RESOLVE_LANE); 0: wave-per-file
     uint32_t resolve_noburst;  // 1: no burst of chained hops in the wave resolve (SYNCR_CDC_FLAG_RESOLVE_NOBURST)
     uint32_t resolve_nosplit;  // 1: no split walks of long files (SYNCR_CDC_FLAG_RESOLVE_NOSPLIT)
+    uint64_t split_patience;   // wall-clock ticks a split worker waits for file walkers (0: none,
+                               //   SYNCR_CDC_FLAG_SPLIT_NOWAIT)
 };
 
 // ---- split walks of long files (wave resolve) -------------
@@ -96,8 +98,10 @@ constexpr uint32_t SPLIT_END = 0xffffffffu;             // SplitSeg::link: walke
 constexpr uint32_t SPLIT_ABORT = 0xfffffffeu;           // (segment walk state: gave up)
 // split[] words: a 64-bit count (split files << 32 | eligible walkers
 // published), so one relaxed read gives both; segment records reserved;
-// queue head; split walkers done
-enum { SPL_PUB64 = 0, SPL_RESERVED = 2, SPL_HEAD = 3, SPL_DONE = 4, SPL_WORDS = 8 };
+// queue head; split walkers done; worker give-ups; segments walked by workers;
+// segments adopted by file walkers
+enum { SPL_PUB64 = 0, SPL_RESERVED = 2, SPL_HEAD = 3, SPL_DONE = 4, SPL_GIVEUP = 5, SPL_WALKED = 6,
+       SPL_ADOPTED = 7, SPL_WORDS = 8 };
 struct SplitSeg {            // 64 bytes
     uint64_t cidx;           // candidate index of the segment's first candidate
     uint64_t out_off;        // adopted: first cut slot within the file's output
@@ -161,6 +165,13 @@ struct Tables {
     DevCut *seg_cuts;              // [seg_cap * SPLIT_SCAP]
     uint32_t *split;               // [SPL_WORDS] counters                    (zeroed per launch)
     uint32_t epoch;                // this launch's id (!= 0, unique in the process): SplitSeg::ready
+    // The per-launch counters above (ctr, nonempty, super_cnt, split) live in one
+    // of two zeroed blocks, alternating by launch.  The resolve kernel zeroes the
+    // OTHER block for the next launch (and the hash counters of this launch),
+    // so a step needs no memset packet (cdc_api.cpp do_launch).
+    uint4 *znext;                  // [znext_vec] the next launch's block (nullptr: none)
+    uint32_t znext_vec;
+    uint64_t *hzero;               // [B3C_WORDS] hash counters of this launch (hashed launches), or nullptr
 };
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------
@@ -216,9 +227,10 @@ int scan_lds_bytes(ScanGeom g);
 int scan_blocks_per_cu(ScanGeom g);
 hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d_bytes, const KParams &p, const Tables &t,
                        hipStream_t s);
-hipError_t launch_post(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s,
-                       hipEvent_t after_dense);
+bool scan_dense_inline(ScanGeom g, const KParams &p);      // the scan passes dense tiles itself
+hipError_t launch_post(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s, bool dense_inline);
 hipError_t launch_resolve(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s);
+bool resolve_splits(const KParams &p, const Tables &t);   // launch_resolve starts split workers
 hipError_t launch_gen(uint8_t *d_base, const uint64_t *d_foff, const uint64_t *d_flen,
                       const uint64_t *d_findex, const uint64_t *d_seg_prefix, uint32_t nfiles,
                       uint64_t nseg, uint64_t first_index, const uint64_t *d_jump, hipStream_t s);

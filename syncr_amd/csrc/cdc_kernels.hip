@@ -185,6 +185,16 @@ __device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
         anyz = anyz || zg[g];
     }
     if (__builtin_expect(__ballot(anyz) != 0ull, 0)) {
+        // more dirty groups than side slots (low-entropy / periodic data): the
+        // tile goes to the exact dense pass anyway, so capture none of them
+        // (each capture is a closed-form window_state of 64 v_dot4)
+        uint32_t tot = 0;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) tot += (uint32_t)__builtin_popcountll(__ballot(zg[g]));
+        if (tot > (uint32_t)DIRTYCAP) {
+            if (lane == 0) *dcount = tot;
+            return;
+        }
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
             if (zg[g]) {
@@ -373,6 +383,11 @@ __device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, u
 // The product's scan: non-temporal tile loads (4) + dynamic tile groups (8) +
 // single-op dependency chains in the roll (16; same process, zipf10k: scan
 // 1.591 vs 1.640 ms, profiles/r02_ab_roll2.log).
+// Bit 7 (development A/B only, SYNCR_CDC_ABLATE=11): a tile with more dirty
+// groups than side slots is passed exactly by the scan wave itself
+// (scan_dense_tile), with no separate dense launch.  Inlined, the pass raises
+// the scan to 256 VGPRs (one wave per SIMD); out of line it needs 384 B of
+// scratch per lane and 254 VGPRs; the product keeps the separate launch.
 constexpr int SCAN_PRODUCT_MODE = 4 | 8 | 16;
 // Small batches use the static stride: a group of 8 tiles is ~46 us of one
 // wave's roll, and below ~80-100 tiles per wave the last groups' imbalance
@@ -473,8 +488,13 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         const uint32_t nd = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)dcount, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_WAVEFRONT));
-        if (nd) rewalk_dirty<RUN>(P, lane, nd < (uint32_t)DIRTYCAP ? nd : (uint32_t)DIRTYCAP, dslots,
-                                  lim_rel, wcount, wlist);
+        if constexpr ((MODE & 128) != 0) {                          // dense tile: exact pass right here
+            if (__builtin_expect(nd > (uint32_t)DIRTYCAP, 0)) {
+                scan_dense_tile<RUN>(data, P, T, tile, t0, lane);
+                continue;
+            }
+        }
+        if (nd && nd <= (uint32_t)DIRTYCAP) rewalk_dirty<RUN>(P, lane, nd, dslots, lim_rel, wcount, wlist);
         publish_tile(data, P, T, tile, t0, wlist, wcount, lane, nd > (uint32_t)DIRTYCAP);
     }
 }
@@ -971,6 +991,8 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
     }
 }
 
+#ifdef SYNCR_CDC_DEV
+// (development library: the dense pass of scan geometries other than the product's)
 // ---------------------------------------------------------------------------
 // Dense tiles (more than LISTCAP candidates: low-entropy / periodic /
 // adversarial data): recompute G for every position of the tile into a bitmap
@@ -1039,6 +1061,195 @@ __global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict
             out[wi] = bits;
             cnt += __builtin_popcount(bits);
         }
+        for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if (lane == 0) {
+            T.dense_cnt[idx] = cnt;
+            atomicAdd(&T.super_cnt[tile >> 6], cnt);
+        }
+    }
+}
+#endif  // SYNCR_CDC_DEV
+
+// Exact packed roll of one dense tile-lane (runs lane and lane+64 in the two
+// 16-bit halves, as roll_fast): every position's full digest test.  Per byte
+// pair:
+//   S += x - d; V = S - 64 d; T += k V           as in the scan (4 ops)
+//   Z = ((S + 1985) & m1) | T                    zero iff both halves of the
+//        digest test pass: (s1 & m1) == m1 <=> ((s1 + 1) & m1) == 0 for the
+//        low-bit mask m1 = mask >> 16, s1 = 1984 + S; T = ((s2+1) k) mod 2^16
+//   h = sat(1 - Z); acc = 2 acc + h              (v_pk_sub_u16 clamp, v_pk_mad_u16)
+// so each run's 16-position group ends as a 16-bit hit mask (first position
+// in bit 15; one v_bfrev per group puts both runs' masks in bitmap order).
+// ~9.4 VALU per byte pair against ~27 for the byte-at-a-time exact roll.
+// put(g, r): r = group g's masks, run A in the high half, run B in the low;
+// positions at or past `lim` (tile-relative) are masked off.  Returns the
+// lane's hit count.
+template <int RUN, class Put>
+__device__ __forceinline__ uint32_t dense_roll(const uint32_t (&A)[(HALO + RUN) / 4],
+                                               const uint32_t (&B)[(HALO + RUN) / 4], const KParams &P,
+                                               int lane, int64_t lim, Put put) {
+    constexpr int NG = RUN / 16;
+    const uint32_t m1x2 = P.m1 | (P.m1 << 16);
+    uint32_t S;
+    u16x2 Tv;
+    window_state<RUN>(A, B, P, 0, S, Tv);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const int i = g * 16 + jj;
+            const uint32_t x = pair_at<RUN>(A, B, HALO + i), d = pair_at<RUN>(A, B, i);
+            S = S + x - d;
+            const u16x2 V = pk_mad(d, 0xFFC0FFC0u, as_u16x2(S));      // S - 64 d
+            Tv = pk_mad(as_u32(V), P.kk, Tv);                         // T += k (S - 64 d)
+            const uint32_t U = as_u32(as_u16x2(S) + (u16x2){(unsigned short)1985, (unsigned short)1985});
+            const uint32_t Z = (U & m1x2) | as_u32(Tv);
+            uint32_t h;
+            asm volatile("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(h) : "s"(0x00010001u), "v"(Z));
+            acc = as_u32(pk_mad(acc, 0x00020002u, as_u16x2(h)));      // acc = 2 acc + h
+        }
+        uint32_t r = __builtin_bitreverse32(acc);    // lo half: run B's mask, hi half: run A's
+        if (lim < (int64_t)tile_bytes(RUN)) {
+            const int64_t pa = (int64_t)lane * RUN + 16 * g, pb = pa + 64 * RUN;
+            const int64_t na = lim - pa, nb = lim - pb;
+            const uint32_t ma = na >= 16 ? 0xffffu : (na <= 0 ? 0u : (1u << na) - 1u);
+            const uint32_t mb = nb >= 16 ? 0xffffu : (nb <= 0 ? 0u : (1u << nb) - 1u);
+            r &= (ma << 16) | mb;
+        }
+        cnt += (uint32_t)__builtin_popcount(r);
+        put(g, r);
+    }
+    return cnt;
+}
+
+// The scan wave's own exact pass over a tile with more dirty groups than side
+// slots (low-entropy / periodic data): no separate dense launch.  The runs are
+// re-read from memory (the landing buffer already holds the next tile, and
+// keeping the roll's registers alive for this rare path would cost the scan
+// its second wave per SIMD); bytes outside [0, span) read as zero.  The bitmap
+// words go straight to dense_bits (halfword stores); the tile joins the dense
+// list that cdc_gather_kernel expands.
+template <int RUN>
+__device__ __forceinline__ void load_runs(const uint8_t *__restrict__ data, int64_t span, int64_t t0, int lane,
+                                          uint32_t (&A)[(HALO + RUN) / 4], uint32_t (&B)[(HALO + RUN) / 4]) {
+    constexpr int NQ = (HALO + RUN) / 16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int64_t g0 = t0 + (int64_t)(lane + 64 * h) * RUN - HALO;
+        uint32_t *dst = h ? B : A;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int64_t g = g0 + 16 * q;
+            uint4 v;
+            if (g >= 0 && g + 16 <= span) {
+                v = *(const uint4 *)(data + g);
+            } else {
+                uint32_t w4[4] = {0u, 0u, 0u, 0u};
+                for (int b = 0; b < 16; ++b)
+                    if (g + b >= 0 && g + b < span) w4[b >> 2] |= (uint32_t)data[g + b] << (8 * (b & 3));
+                v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+            }
+            dst[4 * q] = v.x; dst[4 * q + 1] = v.y; dst[4 * q + 2] = v.z; dst[4 * q + 3] = v.w;
+        }
+    }
+}
+
+template <int RUN>
+__device__ __forceinline__ void scan_dense_tile(const uint8_t *__restrict__ data, const KParams &P,
+                                                const Tables &T, uint32_t tile, int64_t t0, int lane) {
+    constexpr int NG = RUN / 16;
+    uint32_t idx = 0;
+    if (lane == 0) {
+        atomicOr(&T.nonempty[tile >> 6], 1ull << (tile & 63));
+        idx = atomicAdd(&T.ctr[CTR_DENSE], 1u);
+    }
+    idx = (uint32_t)__builtin_amdgcn_readfirstlane(idx);
+    if (idx >= T.dense_cap) {                            // the host re-runs with a bigger list
+        if (lane == 0) {
+            T.tile_meta[tile] = DENSE_BIT | 0x7fffffffu;
+            atomicOr(&T.ctr[CTR_FLAGS], FLAG_DENSE_OVERFLOW);
+        }
+        return;
+    }
+    uint32_t A[(HALO + RUN) / 4], B[(HALO + RUN) / 4];
+    load_runs<RUN>(data, (int64_t)T.span, t0, lane, A, B);
+    uint16_t *bm = (uint16_t *)(T.dense_bits + (size_t)idx * (tile_bytes(RUN) / 32));
+    uint32_t cnt = dense_roll<RUN>(A, B, P, lane, (int64_t)T.span - t0, [&](int g, uint32_t r) {
+        bm[lane * NG + g] = (uint16_t)(r >> 16);
+        bm[(lane + 64) * NG + g] = (uint16_t)r;
+    });
+    for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if (lane == 0) {
+        T.dense_list[idx] = tile;
+        T.dense_cnt[idx] = cnt;
+        T.tile_meta[tile] = DENSE_BIT | idx;
+        atomicAdd(&T.super_cnt[tile >> 6], cnt);
+    }
+}
+
+// Dense tiles, packed (the product's dense pass for the scan's tile
+// geometry): the tile and its halo are staged in LDS exactly like the scan's
+// landing buffer, and lane l rolls runs l and l+64 as the two 16-bit halves of
+// packed registers, as the scan does (roll_fast), but tests every position
+// exactly instead of filtering 16-byte groups.  Per byte pair:
+//   S += x - d; V = S - 64 d; T += k V           as in the scan (4 ops)
+//   Z = ((S + 1985) & m1) | T                    zero iff both halves of the
+//        digest test pass: (s1 & m1) == m1 <=> ((s1 + 1) & m1) == 0 for the
+//        low-bit mask m1 = mask >> 16, s1 = 1984 + S; T = ((s2+1) k) mod 2^16
+//   h = sat(1 - Z); acc = 2 acc + h              (v_pk_sub_u16 clamp, v_pk_mad_u16)
+// so each run's 16-position group ends as a 16-bit hit mask (first position
+// in bit 15; one v_bfrev per group puts both runs' masks in bitmap order).
+// ~9.4 VALU per byte pair against ~27 for the byte-at-a-time exact roll.
+// The bitmap halfwords go through LDS (the staging buffer, once the runs are
+// in registers) and out as coalesced 16-byte stores.
+template <int RUN>
+__global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__restrict__ data, KParams P,
+                                                              Tables T) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dbuf[];   // [HALO + tile]
+    constexpr int TILE = tile_bytes(RUN), BUF = buf_bytes(RUN), NQ = (HALO + RUN) / 16, NG = RUN / 16;
+    const int lane = threadIdx.x;
+    const uint32_t nd = min(T.ctr[CTR_DENSE], T.dense_cap);
+    const int64_t span = (int64_t)T.span;
+    for (uint32_t idx = blockIdx.x; idx < nd; idx += gridDim.x) {
+        const uint32_t tile = T.dense_list[idx];
+        const int64_t t0 = (int64_t)tile * TILE, base = t0 - HALO;
+        __syncthreads();                                 // the previous tile's bitmap has left LDS
+        for (uint32_t o = (uint32_t)lane * 16u; o < (uint32_t)BUF; o += 1024u) {
+            const int64_t g = base + o;
+            uint4 v;
+            if (g >= 0 && g + 16 <= span) {
+                v = *(const uint4 *)(data + g);          // d_bytes and the tile size are 16-byte aligned
+            } else {                                     // batch edges: zeros outside [0, span)
+                uint32_t w4[4] = {0u, 0u, 0u, 0u};
+                for (int b = 0; b < 16; ++b)
+                    if (g + b >= 0 && g + b < span) w4[b >> 2] |= (uint32_t)data[g + b] << (8 * (b & 3));
+                v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+            }
+            *(uint4 *)(dbuf + o) = v;
+        }
+        __syncthreads();
+        uint32_t A[NQ * 4], B[NQ * 4];
+        {
+            const uint4 *la = (const uint4 *)(dbuf + lane * RUN);          // = run start - 64
+            const uint4 *lb = (const uint4 *)(dbuf + (lane + 64) * RUN);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const uint4 a = la[q], b = lb[q];
+                A[4 * q + 0] = a.x; A[4 * q + 1] = a.y; A[4 * q + 2] = a.z; A[4 * q + 3] = a.w;
+                B[4 * q + 0] = b.x; B[4 * q + 1] = b.y; B[4 * q + 2] = b.z; B[4 * q + 3] = b.w;
+            }
+        }
+        __syncthreads();                                 // every lane's runs are in registers: LDS is free
+        uint16_t *bm = (uint16_t *)dbuf;                 // halfword r * NG + g: run r, positions 16g..16g+15
+        uint32_t cnt = dense_roll<RUN>(A, B, P, lane, span - t0, [&](int g, uint32_t r) {
+            bm[lane * NG + g] = (uint16_t)(r >> 16);
+            bm[(lane + 64) * NG + g] = (uint16_t)r;
+        });
+        __syncthreads();
+        uint4 *out = (uint4 *)(T.dense_bits + (size_t)idx * (TILE / 32));
+        for (uint32_t o = (uint32_t)lane; o < (uint32_t)(TILE / 128); o += 64u) out[o] = ((const uint4 *)dbuf)[o];
         for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
         if (lane == 0) {
             T.dense_cnt[idx] = cnt;
@@ -1214,8 +1425,18 @@ __device__ uint64_t head_scan(const uint8_t *data, uint64_t a, uint64_t b, uint3
     return hit;
 }
 
+// The next launch's zeroed block (and this launch's hash counters), written by
+// the resolve kernel's threads instead of a memset packet before the next scan.
+__device__ __forceinline__ void zero_next(const Tables &T) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nthr = gridDim.x * blockDim.x;
+    if (T.znext)
+        for (uint32_t k = tid; k < T.znext_vec; k += nthr) T.znext[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (T.hzero && tid < (uint32_t)B3C_WORDS) T.hzero[tid] = 0ull;
+}
+
 __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restrict__ data, KParams P,
                                                          Tables T) {
+    zero_next(T);
     const uint32_t kf = blockIdx.x * 64 + threadIdx.x;
     if (kf >= T.nfiles) return;
     const uint32_t i = T.order[kf];
@@ -1605,7 +1826,8 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                                 T.segs[rq].verdict = 1u;
                             }
                             cnt += (Off)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                            bstart = (uint32_t)cnt & 63u;          // slots below: the copy phase's
+                            if (lane == 0) atomicAdd(&T.split[SPL_ADOPTED], (uint32_t)__builtin_popcountll(adopted));
+                            bstart = (uint32_t)cnt & 63u;          // slots below: the copy kernel's
                             if (last == SPLIT_END) {
                                 stop = true;
                                 break;
@@ -1888,7 +2110,10 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
         }
         const uint32_t st = (link == SPLIT_ABORT || (uint64_t)cnt > cap) ? 2u : 1u;
         __threadfence();
-        if (lane == 0) __hip_atomic_store(&g.status, st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) {
+            __hip_atomic_store(&g.status, st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (st == 1u) atomicAdd(&T.split[SPL_WALKED], 1u);
+        }
         return;
     }
     if (lane == 0) {
@@ -1902,11 +2127,16 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
 }
 
 // The extra resolve waves (split workers): walk segments as the file walkers
-// publish them, then copy every adopted segment's cuts into its file's
-// output.  They never hold up a file walker (which walks a segment itself when
-// that segment's walk is not done), and they only wait for file walkers,
-// which are dispatched first.  split_next: the next segment record to walk, or
-// SPLIT_END once every eligible walker has published and the queue is empty.
+// publish them.  They never hold up a file walker (which walks a segment itself
+// when that segment's walk is not done), and the only thing they wait for is a
+// file walker publishing its segments.  File-walker blocks have the lower
+// block indices and are dispatched first, but the programming model does not
+// promise it, so every wait is bounded: past KParams::split_patience of wall
+// clock (~100 ms; 0 with SYNCR_CDC_FLAG_SPLIT_NOWAIT) the worker gives up,
+// counts itself in SPL_GIVEUP and stops -- the segments it would have walked
+// stay pending and their file walkers walk them, so a give-up costs time,
+// never correctness.  Adopted segments' cuts are copied by a separate launch
+// (cdc_split_copy_kernel), so no wave ever waits for the walkers to finish.
 // Polls are relaxed: an agent-scope acquire invalidates the XCD's L2 on gfx950,
 // so it is taken once, only before reading what another wave published.
 __device__ __forceinline__ uint32_t ld_relaxed(const uint32_t *p) {
@@ -1917,7 +2147,24 @@ __device__ __forceinline__ uint64_t ld64_relaxed(const unsigned long long *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ uint32_t split_next(const Tables &T, int lane) {
+// Wall-clock budget of one worker's waits (s_memrealtime, constant rate).
+struct Patience {
+    uint64_t deadline;
+    __device__ __forceinline__ explicit Patience(uint64_t ticks)
+        : deadline(ticks ? wall_clock64() + ticks : 0ull) {}
+    __device__ __forceinline__ bool spent() const { return deadline == 0ull || wall_clock64() > deadline; }
+};
+
+__device__ __forceinline__ uint32_t give_up(const Tables &T, int lane) {
+    if (lane == 0) atomicAdd(&T.split[SPL_GIVEUP], 1u);
+    return SPLIT_END;
+}
+
+// The next segment record to walk, or SPLIT_END once every eligible walker has
+// published and the queue is empty (or the worker ran out of patience).
+__device__ __forceinline__ uint32_t split_next(const KParams &P, const Tables &T, int lane) {
+    const Patience pat(P.split_patience);
+    if (P.split_patience == 0ull) return give_up(T, lane);           // SYNCR_CDC_FLAG_SPLIT_NOWAIT
     uint32_t q = 0;
     if (lane == 0) q = atomicAdd(&T.split[SPL_HEAD], 1u);
     q = (uint32_t)__builtin_amdgcn_readfirstlane(q);
@@ -1929,43 +2176,44 @@ __device__ __forceinline__ uint32_t split_next(const Tables &T, int lane) {
             if (q < min(ld_relaxed(&T.split[SPL_RESERVED]), T.seg_cap)) break;
             return SPLIT_END;
         }
+        if (pat.spent()) return give_up(T, lane);
         __builtin_amdgcn_s_sleep(16);
     }
-    while (ld_relaxed(&T.segs[q].ready) != T.epoch) __builtin_amdgcn_s_sleep(4);   // not a stale record
+    while (ld_relaxed(&T.segs[q].ready) != T.epoch) {                 // not a stale record
+        if (pat.spent()) return give_up(T, lane);                     // record q stays pending
+        __builtin_amdgcn_s_sleep(4);
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");        // the record's fields
     return q;
 }
 
-// Once every split file's walker is done: copy the adopted segments' cuts.
-__device__ void split_copy(const Tables &T, int lane, uint32_t wid, uint32_t nw) {
-    uint64_t pub;
-    while ((uint32_t)(pub = ld64_relaxed(split_pub(T))) < T.n_elig) __builtin_amdgcn_s_sleep(16);
-    const uint32_t nsplit = (uint32_t)(pub >> 32);          // final with the last count
-    if (nsplit == 0u) return;                               // nothing split: nothing to copy
-    while (ld_relaxed(&T.split[SPL_DONE]) < nsplit) __builtin_amdgcn_s_sleep(16);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");        // verdicts, offsets and segment cuts
-    const uint32_t nrec = min(ld_relaxed(&T.split[SPL_RESERVED]), T.seg_cap);
-    for (uint32_t q = wid; q < nrec; q += nw) {
-        const SplitSeg &g = T.segs[q];
-        if (seg_ld(g.k) == 0u || seg_ld(g.verdict) != 1u) continue;
-        const uint32_t i = seg_ld(g.file);
-        const uint64_t cap = T.cut_cap[i], o = seg_ld(g.out_off), n = seg_ld(g.n);
-        const DevCut *src = T.seg_cuts + (uint64_t)q * SPLIT_SCAP;
-        DevCut *dst = T.cuts + T.cut_base[i];
-        for (uint64_t t = (uint64_t)lane; t < n && o + t < cap; t += 64) dst[o + t] = src[t];
-    }
-}
-
-__device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P, const Tables &T, int lane,
-                             uint32_t wid, uint32_t nw) {
+__device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P, const Tables &T, int lane) {
     for (;;) {
-        const uint32_t q = split_next(T, lane);
+        const uint32_t q = split_next(P, T, lane);
         if (q == SPLIT_END) break;
         if (seg_ld(T.segs[q].k) == 0u) continue;
         const uint32_t i = seg_ld(T.segs[q].file);
         resolve_walk<uint32_t>(data, P, T, i, T.flen[i], T.foff[i], lane, false, q);
     }
-    split_copy(T, lane, wid, nw);
+}
+
+// After the resolve launch (so after every walker): copy the cuts of every
+// segment walk a file walker adopted into that file's output.
+__global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
+    const uint32_t nsplit = (uint32_t)(*split_pub(T) >> 32);
+    if (nsplit == 0u) return;                                 // nothing split: nothing to copy
+    const uint32_t nrec = min(T.split[SPL_RESERVED], T.seg_cap);
+    for (uint32_t q = wid; q < nrec; q += nw) {
+        const SplitSeg &g = T.segs[q];
+        if (g.k == 0u || g.verdict != 1u || g.ready != T.epoch) continue;
+        const uint32_t i = g.file;
+        const uint64_t cap = T.cut_cap[i], o = g.out_off, n = g.n;
+        const DevCut *src = T.seg_cuts + (uint64_t)q * SPLIT_SCAP;
+        DevCut *dst = T.cuts + T.cut_base[i];
+        for (uint64_t t = (uint64_t)lane; t < n && o + t < cap; t += 64) dst[o + t] = src[t];
+    }
 }
 
 // One wave per file; files below 4 GiB walk in 32-bit offsets.  Blocks past
@@ -1975,9 +2223,10 @@ __device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P,
 __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__restrict__ data,
                                                                KParams P, Tables T) {
     const int lane = threadIdx.x & 63;
+    zero_next(T);
     const uint32_t nmain = (T.nfiles + 3u) / 4u;
     if (blockIdx.x >= nmain) {
-        split_worker(data, P, T, lane, (blockIdx.x - nmain) * 4u + (threadIdx.x >> 6), (gridDim.x - nmain) * 4u);
+        split_worker(data, P, T, lane);
         return;
     }
     const uint32_t kf = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -2165,6 +2414,8 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 5u)                                         // A/B: round-1 roll (two dependent mads, exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 11u)                                        // A/B: dense tiles passed by the scan wave
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 128>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 6u)                                         // timing only: roll, no DMA
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
@@ -2220,6 +2471,10 @@ static void launch_mfma_t(int var, uint32_t grid, const uint8_t *d, const KParam
     }
 }
 
+bool scan_dense_inline(ScanGeom g, const KParams &p) {
+    return g.kind == SCAN_VALU && g.param != W3_RUN && p.ablate == 11u;     // the mode-128 instance
+}
+
 hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
                        hipStream_t s) {
     if (!t.ntiles) return hipSuccess;
@@ -2251,6 +2506,7 @@ bool scan_supported(ScanGeom g) { return g.kind == SCAN_VALU && g.param == DEFAU
 int scan_tile_bytes(ScanGeom) { return tile_bytes(DEFAULT_RUN); }
 int scan_lds_bytes(ScanGeom) { return lds_wave_bytes(DEFAULT_RUN); }
 static const void *scan_kernel_ptr(ScanGeom) { return (const void *)&cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>; }
+bool scan_dense_inline(ScanGeom, const KParams &) { return false; }
 
 hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
                        hipStream_t s) {
@@ -2275,14 +2531,23 @@ int scan_blocks_per_cu(ScanGeom g) {
     return n > 0 ? n : 1;
 }
 
-hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s,
-                       hipEvent_t) {
+hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s, bool dense_inline) {
     if (!t.ntiles) return hipSuccess;
     const uint32_t dblocks = t.dense_cap < 2048u ? (t.dense_cap ? t.dense_cap : 1u) : 2048u;
-    hipLaunchKernelGGL(cdc_dense_kernel, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
+    if (dense_inline) {
+        // (development A/B) the scan passed its dense tiles itself
+    } else if (t.tile == (uint32_t)tile_bytes(DEFAULT_RUN)) {
+        hipLaunchKernelGGL(cdc_dense_packed_kernel<DEFAULT_RUN>, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
+    } else {                                          // other scan geometries (development library)
+#ifdef SYNCR_CDC_DEV
+        hipLaunchKernelGGL(cdc_dense_kernel, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
+#endif
+    }
     hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
-    // + up to 256 blocks that expand dense tiles (they exit at once when none are)
-    const uint32_t dgb = std::min<uint32_t>((t.dense_cap + 3) / 4, 256u);
+    // + up to 2048 blocks (one wave per dense tile) that expand dense tiles; they
+    // exit at once when there are none.  (256 blocks left ~33 serial tile
+    // expansions per wave on the dense workload: 0.2 ms.)
+    const uint32_t dgb = std::min<uint32_t>((t.dense_cap + 3) / 4, 2048u);
     hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4 + dgb), dim3(256), 0, s, t);
     const uint64_t want = (t.cand_cap + t.ngrid + 255) / 256;
     const uint32_t blocks = (uint32_t)(want < 2048 ? (want ? want : 1) : 2048);
@@ -2290,14 +2555,19 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
     return hipGetLastError();
 }
 
+bool resolve_splits(const KParams &p, const Tables &t) {
+    return t.nfiles && !p.resolve_lane && t.n_elig && t.seg_cap && !p.resolve_nosplit;
+}
+
 hipError_t launch_resolve(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    if (!t.nfiles) return hipSuccess;
+    if (!t.nfiles) return hipSuccess;           // (do_launch then memsets the next block itself)
     if (p.resolve_lane)
         hipLaunchKernelGGL(cdc_resolve_kernel, dim3((t.nfiles + 63) / 64), dim3(64), 0, s, d, p, t);
     else {
-        const bool split = t.n_elig && t.seg_cap && !p.resolve_nosplit;
+        const bool split = resolve_splits(p, t);
         hipLaunchKernelGGL(cdc_resolve_wave_kernel, dim3((t.nfiles + 3) / 4 + (split ? SPLIT_BLOCKS : 0u)),
                            dim3(256), 0, s, d, p, t);
+        if (split) hipLaunchKernelGGL(cdc_split_copy_kernel, dim3(SPLIT_BLOCKS), dim3(256), 0, s, t);
     }
     return hipGetLastError();
 }

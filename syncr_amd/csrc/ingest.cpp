@@ -180,17 +180,25 @@ void free_slot_buffers(Pipe *g, Slot &s) {
     s.cap = 0;
 }
 
+// Grow a slot's buffers to `bytes`.  The new buffers are allocated before the
+// old ones are freed (device memory first: a file too big for the GPU fails
+// there without touching host memory), so a failed allocation for one
+// oversized file leaves the slot as it was and only that file fails.
 int32_t ensure_slot(Pipe *g, Slot &s, uint64_t bytes) {
     if (bytes <= s.cap && s.host) return SYNCR_CDC_OK;
-    free_slot_buffers(g, s);
     const uint64_t want = std::max<uint64_t>(bytes, 64);
+    uint8_t *dev = nullptr, *host = nullptr;
     hipError_t e = hipSetDevice(g->device);
-    if (e == hipSuccess) e = hipHostMalloc((void **)&s.host, want, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipMalloc((void **)&s.dev, want);
+    if (e == hipSuccess) e = hipMalloc((void **)&dev, want);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&host, want, hipHostMallocDefault);
     if (e != hipSuccess) {
-        free_slot_buffers(g, s);
+        (void)hipGetLastError();                            // the failure is this call's, not sticky
+        if (dev) (void)hipFree(dev);
         return hip_rc(e);
     }
+    free_slot_buffers(g, s);
+    s.host = host;
+    s.dev = dev;
     s.cap = want;
     return SYNCR_CDC_OK;
 }
@@ -498,6 +506,7 @@ int32_t pipe_flush(Pipe *g) {
 
 struct Result {
     int32_t status = 0;
+    bool skip = false;                // a failed synchronous submit: no callback (as single-device)
     std::vector<syncr_chunk_info> chunks;
 };
 
@@ -565,6 +574,21 @@ void deliver_multi(void *owner, uint64_t seq, int32_t status, const syncr_chunk_
     g->reorder.put(seq, std::move(r));
 }
 
+// A job that failed for its own file only (the pipe has no sticky engine
+// error: e.g. ENOMEM for the pinned buffer of a file larger than a batch, which
+// the single-device pipeline also reports for that call alone) still takes its
+// place in the submission order, so later files keep being delivered: an
+// asynchronous job (submit_file, commit) is delivered with its error status and
+// no chunks; a synchronous submit, whose caller already got the error, is
+// dropped without a callback, exactly as single-device mode does.
+void fail_in_order(Pipe *p, const Job &j, int32_t rc) {
+    syncr_ingest *g = (syncr_ingest *)p->owner;
+    Result r;
+    r.status = rc;
+    r.skip = j.kind == J_COPY;
+    g->reorder.put(j.seq, std::move(r));
+}
+
 void worker_main(Worker *w) {
     (void)hipSetDevice(w->pipe->device);
     for (;;) {
@@ -586,9 +610,11 @@ void worker_main(Worker *w) {
             case J_COMMIT: rc = pipe_commit(p, j.seq); break;
             case J_FLUSH: rc = pipe_flush(p); break;
         }
+        const bool per_file = rc && !p->error && (j.kind == J_FILE || j.kind == J_COPY || j.kind == J_COMMIT);
+        if (per_file) fail_in_order(p, j, rc);
         {
             std::lock_guard<std::mutex> l(w->mu);
-            if (rc && !w->err) w->err = rc;
+            if (rc && p->error && !w->err) w->err = p->error;      // only engine errors are sticky
             if (j.sync) {
                 j.sync->rc = rc;
                 j.sync->dst = dst;
@@ -632,6 +658,7 @@ void drain(syncr_ingest *g) {
     while (g->reorder.take(r, seq)) {
         const uint64_t tag = g->tags.front();
         g->tags.pop_front();
+        if (r.skip) continue;
         if (g->cb) g->cb(g->ctx, tag, r.status, r.chunks.empty() ? nullptr : r.chunks.data(), r.chunks.size());
     }
 }

@@ -95,6 +95,23 @@ def test_empty_or_torn_header_file_is_a_new_cache(tmp_path):
             assert np.array_equal(c.get("f", 1, int(a["len"].sum())), a), name
 
 
+def test_old_format_log_is_a_stale_cache(tmp_path):
+    """a log written by the ABI-v2 library (magic SYNCRCC1, no
+    parameter header) opens as an empty cache, rewritten with the current
+    header, instead of failing with EIO; its entries are never served."""
+    import struct
+    p = tmp_path / "old.cache"
+    rec = struct.pack("<I", 1) + b"f" + struct.pack("<IQQ", 5, 100, 0)
+    p.write_bytes(b"SYNCRCC1" + rec + b"\0" * 8)
+    with syncr_amd.ChunkCache(str(p)) as c:
+        assert c.get("f", 5, 100) is None and c.stats()["entries"] == 0
+        a = chunks(2, 4)
+        c.put("g", 2, int(a["len"].sum()), a)
+    assert p.read_bytes()[:8] == b"SYNCRCC2"
+    with syncr_amd.ChunkCache(str(p)) as c:
+        assert np.array_equal(c.get("g", 2, int(a["len"].sum())), a)
+
+
 def test_header_is_durable_before_first_put(tmp_path):
     p = tmp_path / "c"
     c = syncr_amd.ChunkCache(str(p))

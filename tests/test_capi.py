@@ -82,10 +82,11 @@ def test_invalid_params_rejected(lib):
         p = syncr_amd.Params(bits, 0, mx, 0)
         assert lib.syncr_cdc_open(0, ctypes.byref(p), ctypes.byref(h)) in (-22, -19)
     assert lib.syncr_cdc_open(0, None, None) == -22
-    for flags in (8, 16, 1 << 31):                        # only SYNCR_CDC_FLAG_* bits
+    for flags in (16, 32, 1 << 31):                       # only SYNCR_CDC_FLAG_* bits
         p = syncr_amd.Params(20, flags, 16 << 20, 2 << 20)
         assert lib.syncr_cdc_open(0, ctypes.byref(p), ctypes.byref(h)) == -22
-    for flags in (0, syncr_amd.FLAG_RESOLVE_LANE, syncr_amd.FLAG_RESOLVE_NOBURST, syncr_amd.FLAG_RESOLVE_NOSPLIT):
+    for flags in (0, syncr_amd.FLAG_RESOLVE_LANE, syncr_amd.FLAG_RESOLVE_NOBURST, syncr_amd.FLAG_RESOLVE_NOSPLIT,
+                  syncr_amd.FLAG_SPLIT_NOWAIT):
         p = syncr_amd.Params(20, flags, 16 << 20, 2 << 20)
         assert lib.syncr_cdc_open(0, ctypes.byref(p), ctypes.byref(h)) in (0, -19)
         if h.value:

@@ -12,7 +12,7 @@ import bench
 
 
 def test_lpt_shard_partition_and_balance():
-    sizes, idx, _ = bench.workload("zipf10k", 8)
+    sizes, idx, _ = bench.workload("zipf10k", 8, "weak")
     assert sizes.size == 80000 and np.array_equal(idx, np.arange(80000))
     parts = bench.lpt_shard(sizes, 8)
     allf = np.sort(np.concatenate(parts))
@@ -39,7 +39,7 @@ def _worker(rank, world, port, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     d = bench.Dist()
-    sizes, _, _ = bench.workload("uniform1k", world)
+    sizes, _, _ = bench.workload("uniform1k", world, "weak")
     mine = bench.lpt_shard(sizes, world)[d.rank]
     span = float(sizes[mine].sum())
     d.barrier()
@@ -103,18 +103,35 @@ def _run_bench(args, env=None, timeout=240):
 def test_bench_gpus2_self_launches_two_ranks():
     """`bench.py --gpus N` (no launcher) must run N ranks itself.
     The dry run touches no device: it prints the LPT shard plan gathered from
-    both ranks over gloo."""
+    both ranks over gloo.  Weak scaling: one 10 000-file set per rank."""
     pytest.importorskip("torch")
-    r = _run_bench(["--gpus", "2", "--dry-run"])
+    r = _run_bench(["--gpus", "2", "--dry-run", "--scaling", "weak"])
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout                                   # rank 0 only
     out = lines[0]
-    assert out["n_gpus"] == 2 and out["launcher"] == "bench.py"
+    assert out["n_gpus"] == 2 and out["launcher"] == "bench.py" and out["scaling"] == "weak"
     assert [s["rank"] for s in out["shards"]] == [0, 1]
     assert out["disjoint"] and out["covers_all"]
     assert all(s["files"] == 10000 and s["bytes"] == 10447937536 for s in out["shards"])
     assert out["max_over_mean"] < 1.01
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_strong_scaling_shards_one_corpus(n):
+    """VERDICT r2 #2 / BASELINE config 4: `--scaling strong` (the default) shards
+    THE 10 000-file zipf10k corpus per file across N ranks: disjoint shards that
+    cover exactly those files, LPT-balanced to max/mean < 1.05."""
+    pytest.importorskip("torch")
+    r = _run_bench(["--gpus", str(n), "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert out["n_gpus"] == n and out["scaling"] == "strong"
+    assert out["total_files"] == 10000 and out["total_bytes"] == 10447937536
+    assert len(out["shards"]) == n and out["disjoint"] and out["covers_all"]
+    assert sum(s["files"] for s in out["shards"]) == 10000
+    assert sum(s["bytes"] for s in out["shards"]) == 10447937536
+    assert out["max_over_mean"] < 1.05
 
 
 def test_bench_world_size_must_match_gpus():

@@ -1,0 +1,75 @@
+"""Full-size parity of the HIP engine against the golden per-file digests of
+the CPU oracle (tests/golden/*_digests.npz, made by
+tests/golden/make_corpus_digests.py): every file of the zipf10k corpus (SURVEY
+§8d config 3) in both semantics and with chunk hashes, the device-built dedup
+corpus (config 5) and the adversarial dense workload -- the same checks
+bench.py's parity leg reports on the driver's box.  Bar: bit-exact."""
+import numpy as np
+import pytest
+
+import syncr_amd
+from benchlib import golden as G
+from benchlib import legs as L
+from benchlib import workloads as WL
+
+pytestmark = pytest.mark.gpu
+M = 1 << 20
+
+
+def test_zipf10k_every_file_vs_golden_digests():
+    lens = WL.zipf_sizes()
+    offs = WL.offsets_of(lens)
+    span = int(lens.sum())
+    idx = np.arange(lens.size)
+    with syncr_amd.Chunker() as ch:
+        buf = syncr_amd.DeviceBuffer(ch, span)
+        try:
+            buf.gen_corpus(offs, lens)
+            ch.plan(offs, lens, span)
+            ch.launch(buf.ptr, hashed=True)
+            p = G.check_files("zipf10k", ch.fetch(hashed=True), idx, hashed=True)
+            assert p["files"] == 10000 and p["mismatches"] == 0, p
+            ideal = L.ideal_leg(buf, offs, lens, idx, 0)
+            assert ideal["files"] == 10000 and ideal["mismatches"] == 0, ideal
+        finally:
+            buf.free()
+
+
+def test_dedup_built_on_device_vs_golden_digests():
+    """The dedup corpus assembled in HBM (gen_corpus + syncr_cdc_memcpy_d2d)
+    equals the host-built variants the golden digests were computed from."""
+    r = L.dedup_leg(0, steps=2, warmup=1)
+    assert r["parity"]["files"] == 1000 and r["parity"]["mismatches"] == 0, r["parity"]
+    assert r["parity_hashed"]["mismatches"] == 0, r["parity_hashed"]
+    assert r["stability"]["kept_median"] >= 0.9
+
+
+def test_dense_workload_vs_golden_digests():
+    r = L.dense_leg(0, steps=2, warmup=1)
+    assert r["parity"]["files"] == 10000 and r["parity"]["mismatches"] == 0, r["parity"]
+    assert r["parity_hashed"]["mismatches"] == 0, r["parity_hashed"]
+    assert r["dense_tiles"] > 0 and r["split"]["adopted"] > 0, r
+
+
+def test_parity_legs_of_smoke_and_bench():
+    for leg in (L.kat_leg, L.blake3_vectors_leg, L.dense_subset_leg):
+        r = leg(0)
+        assert r["mismatches"] == 0 and r.get("hash_mismatches", 0) == 0, (leg.__name__, r)
+    r = L.ingest_multi_leg(0)
+    assert r["parity"]["mismatches"] == 0 and r["parity"]["files"] > 500, r
+
+
+def test_memcpy_d2d():
+    with syncr_amd.Chunker() as ch:
+        a = syncr_amd.DeviceBuffer(ch, 1 << 20)
+        b = syncr_amd.DeviceBuffer(ch, 1 << 20)
+        try:
+            a.gen_corpus([0], [1 << 20])
+            b.upload(np.zeros(1 << 20, np.uint8))
+            b.copy_from(a.ptr + 5, 1000, offset=77)
+            ch.synchronize()
+            ha, hb = a.download(), b.download()
+            assert np.array_equal(hb[77:1077], ha[5:1005]) and not hb[:77].any() and not hb[1077:].any()
+        finally:
+            a.free()
+            b.free()

@@ -291,3 +291,45 @@ def test_periodic_files_split_walks():
         assert np.array_equal(got["len"].astype(np.uint64), ends - starts), tag
         hs = O.blake3_batch(data, starts, ends - starts, nthreads=8)
         assert np.array_equal(got["hash"], hs), tag
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_oversized_file_fails_alone(tmp_path, devices):
+    """a file whose batch cannot be allocated (here a
+    sparse 512 GiB file: more than the GPU's memory) fails by itself.
+    Single device: submit_file raises ENOMEM for that call.  Multi-device: the
+    call returned before the job ran, so the file is delivered in its place
+    with -ENOMEM and no chunks; either way every later file is still chunked
+    and delivered in order and flush succeeds (only engine errors are sticky)."""
+    files = corpus(8, 41, 2 * M)
+    paths = []
+    for i, f in enumerate(files):
+        p = tmp_path / f"f{i}.bin"
+        p.write_bytes(f.tobytes())
+        paths.append(str(p))
+    big = tmp_path / "sparse.bin"
+    try:
+        with open(big, "wb") as fh:
+            fh.truncate(512 << 30)
+    except OSError:
+        pytest.skip("no sparse files here")
+    paths.insert(3, str(big))
+    got = []
+    with syncr_amd.Ingest(batch_bytes=4 * M, depth=2, copy_threads=2, devices=devices,
+                          on_file=lambda t, s, a: got.append((t, s, a))) as g:
+        for i, p in enumerate(paths):
+            if devices is None and i == 3:
+                with pytest.raises(syncr_amd.SyncrCdcError) as ei:
+                    g.submit_file(p, i)
+                assert ei.value.code == -errno.ENOMEM
+                continue
+            g.submit_file(p, i)
+        g.flush()
+    if devices is None:
+        assert [t for t, _, _ in got] == [i for i in range(len(paths)) if i != 3]
+        rest = got
+    else:
+        assert [t for t, _, _ in got] == list(range(len(paths)))
+        assert got[3][1] == -errno.ENOMEM and got[3][2].size == 0
+        rest = got[:3] + got[4:]
+    check([(i, s, a) for i, (_, s, a) in enumerate(rest)], files)

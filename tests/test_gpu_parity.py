@@ -519,20 +519,12 @@ def test_long_resolve_chains(chunkers, bits, mx, cap):
     check_contiguous(cuts, data.size, mx)
 
 
-@pytest.mark.parametrize("bits,mx,cap", [(8, 4096, 3000), (8, 1 << 16, 0), (10, 1 << 14, 2 << 20),
-                                         (20, 16 << 20, 2 << 20), (20, 16 << 20, 0)])
-def test_split_walks(bits, mx, cap):
-    """Split walks of long files: files of >= 4 MiB holding
-    >= 2 x 16384 candidates are walked in segments by extra resolve waves and
-    stitched where a walk lands on a segment's start with its start state.
-    Mixed content makes segment starts that are not cuts, read-limit
-    mismatches and aborted segment walks; every file must equal the oracle
-    and the unsplit walk (SYNCR_CDC_FLAG_RESOLVE_NOSPLIT)."""
-    import bench
-    pat = bench.periodic_pattern() if bits == 20 else None
+def _split_corpus(bits, cap):
+    from benchlib.workloads import periodic_pattern
+    pat = periodic_pattern() if bits == 20 else None
     rng = np.random.default_rng(bits * 7919 + cap)
     files = []
-    lo, hi = (34 * M, 44 * M) if bits == 10 else (5 * M, 14 * M)     # >= 2 x 16384 candidates for most
+    lo, hi = (34 * M, 44 * M) if bits == 10 else (5 * M, 14 * M)
     for k in range(3 if bits == 10 else 4):
         n = int(rng.integers(lo, hi))
         if pat is not None:                         # periodic with random glitches every ~1-3 MiB
@@ -551,15 +543,56 @@ def test_split_walks(bits, mx, cap):
     data = np.zeros(span, np.uint8)
     for o, f in zip(offs.tolist(), files):
         data[o:o + f.size] = f
-    got = {}
+    return data, offs, lens
+
+
+def _split_oracle(data, offs, lens, bits, mx, cap):
+    return [(O.chunk_production_window(data[o:o + n], bits, mx, cap) if cap else
+             O.chunk_ideal(data[o:o + n], bits, mx)).tolist() for o, n in zip(offs.tolist(), lens.tolist())]
+
+
+@pytest.mark.parametrize("bits,mx,cap", [(8, 4096, 3000), (8, 1 << 16, 0), (10, 1 << 14, 2 << 20),
+                                         (20, 16 << 20, 2 << 20), (20, 16 << 20, 0)])
+def test_split_walks(bits, mx, cap):
+    """Split walks of long files: files of >= SPLIT_MIN_BYTES
+    (256 KiB) holding >= 2 x SPLIT_SEGC (4096) candidates are walked in
+    segments of 4096 candidates by extra resolve waves and stitched where a
+    walk lands on a segment's start with its start state; the handle launches
+    the extra waves once a fetch has seen >= 64 Ki candidates at >= 1 per
+    16 KiB.  Mixed content makes segment starts that are not cuts, read-limit
+    mismatches and aborted segment walks; every file must equal the oracle and
+    the unsplit walk (SYNCR_CDC_FLAG_RESOLVE_NOSPLIT), and the split run must
+    have split files and adopted segment walks (syncr_cdc_split_stats)."""
+    data, offs, lens = _split_corpus(bits, cap)
+    got, stats = {}, {}
     for flags in (0, syncr_amd.FLAG_RESOLVE_NOSPLIT):
         with syncr_amd.Chunker(bits, mx, cap, flags=flags) as ch:
-            # the handle splits once a fetch has seen >= 2 x 16384 candidates:
-            # the second call (and the re-runs of the first) walk split
+            # the first call's fetch turns the split hint on: the second call
+            # (and the re-runs of the first) walk split
             got[flags] = [ends_of(r) for r in ch.batch_arrays(data, offs, lens)]
             got[flags + 100] = [ends_of(r) for r in ch.batch_arrays(data, offs, lens)]
-    for i, (o, n) in enumerate(zip(offs.tolist(), lens.tolist())):
-        f = data[o:o + n]
-        want = (O.chunk_production_window(f, bits, mx, cap) if cap else O.chunk_ideal(f, bits, mx)).tolist()
+            stats[flags] = ch.split_stats()
+    want = _split_oracle(data, offs, lens, bits, mx, cap)
+    for i in range(lens.size):
         for k in got:
-            assert got[k][i] == want, (i, n, bits, mx, cap, k)
+            assert got[k][i] == want[i], (i, int(lens[i]), bits, mx, cap, k)
+    sp = stats[0]
+    assert sp["workers_launched"] == 1 and sp["files_split"] >= 1 and sp["segments"] >= 1, sp
+    assert sp["walked"] >= 1 and sp["adopted"] >= 1 and sp["giveups"] == 0, sp
+    assert stats[syncr_amd.FLAG_RESOLVE_NOSPLIT]["workers_launched"] == 0
+
+
+@pytest.mark.parametrize("bits,mx,cap", [(8, 4096, 3000), (20, 16 << 20, 2 << 20)])
+def test_split_workers_give_up(bits, mx, cap):
+    """a split worker's waits are bounded; one that gives up
+    leaves its segments to the file walkers, which never wait.  With
+    SYNCR_CDC_FLAG_SPLIT_NOWAIT every worker gives up at once: no segment walk
+    is done or adopted, and every file is still oracle-exact."""
+    data, offs, lens = _split_corpus(bits, cap)
+    with syncr_amd.Chunker(bits, mx, cap, flags=syncr_amd.FLAG_SPLIT_NOWAIT) as ch:
+        ch.batch_arrays(data, offs, lens)
+        got = [ends_of(r) for r in ch.batch_arrays(data, offs, lens)]
+        sp = ch.split_stats()
+    assert got == _split_oracle(data, offs, lens, bits, mx, cap)
+    assert sp["workers_launched"] == 1 and sp["files_split"] >= 1, sp
+    assert sp["giveups"] == 1024 and sp["walked"] == 0 and sp["adopted"] == 0, sp
