@@ -280,7 +280,7 @@ int32_t syncr_cdc_kernel_times_ex(syncr_cdc *h, double *ms, uint32_t n, uint64_t
 /* Diagnostics of the last fetched launch: [candidates, dense_tiles, tiles, overflow]. */
 int32_t syncr_cdc_last_stats(syncr_cdc *h, uint64_t *stats4);
 /* Split walks of long files (wave resolve) in the last fetched launch:
- * [workers_launched (0/1), files_split, segments, segments walked by the split
+ * [worker waves launched (0: none), files_split, segments, segments walked by the split
  * workers, segments adopted by their file's walker, worker give-ups].  A worker
  * waits only for file walkers to publish their segments; it gives up (and
  * leaves the rest to the file walkers, which never wait) after ~100 ms. */

@@ -347,7 +347,7 @@ class Chunker:
         """Split walks of long files in the last fetched launch (syncr_cdc_split_stats)."""
         st = (ctypes.c_uint64 * 6)()
         _check(library().syncr_cdc_split_stats(self._h, st), "syncr_cdc_split_stats")
-        return dict(zip(("workers_launched", "files_split", "segments", "walked", "adopted", "giveups"),
+        return dict(zip(("workers", "files_split", "segments", "walked", "adopted", "giveups"),
                         (int(x) for x in st)))
 
     def info(self) -> dict:

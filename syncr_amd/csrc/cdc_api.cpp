@@ -88,6 +88,7 @@ struct syncr_cdc {
     DevBuf gpos, gend, gfix, gbase;
     // split walks of long files (Tables::segs...): files order[0 .. n_elig) may split
     uint32_t n_elig = 0, seg_cap = 0;
+    uint32_t split_segc = SPLIT_SEGC, split_blocks = SPLIT_BLOCKS;   // (development library: SYNCR_CDC_SPLIT_*)
     DevBuf segs, seg_cuts;
     // split only when walks can be long: the last launch fetched held >= 64 Ki
     // candidates at >= 1 per 16 KiB (random data: ~1 per MiB, so never;
@@ -216,6 +217,9 @@ Tables make_tables(syncr_cdc *h) {
     t.seg_cap = h->seg_cap;
     t.segs = h->segs.as<SplitSeg>();
     t.seg_cuts = h->seg_cuts.as<DevCut>();
+    t.seg_segc = h->split_segc;
+    t.seg_scap = split_scap(h->split_segc);
+    t.split_blocks = h->split_blocks;
     t.split = reinterpret_cast<uint32_t *>(zb + split_ctr_offset(h));
     t.znext = reinterpret_cast<uint4 *>(zblock(h, h->zpar ^ 1u));
     t.znext_vec = (uint32_t)(zstride(h) / 16);
@@ -313,15 +317,15 @@ int32_t ensure_dense(syncr_cdc *h, uint32_t cap) {
 }
 
 // Split-walk records and scratch, only while the handle splits (split_hint):
-// a file splits into segments of SPLIT_SEGC of its candidates, so
-// cand_cap / SPLIT_SEGC records cover every split file.
+// a file splits into segments of split_segc of its candidates, so
+// cand_cap / split_segc records cover every split file.
 int32_t ensure_split(syncr_cdc *h) {
     h->seg_cap = 0;
     if (h->n_elig && h->split_hint) {
-        const uint64_t segs = std::min<uint64_t>(h->cand_cap / SPLIT_SEGC + 8, 0xffffffull);
+        const uint64_t segs = std::min<uint64_t>(h->cand_cap / h->split_segc + 8, 0xffffffull);
         CHECK_HIP(h->segs.ensure(segs * sizeof(SplitSeg)));
         CHECK_HIP(hipMemset(h->segs.p, 0, segs * sizeof(SplitSeg)));     // no ready word from other memory
-        CHECK_HIP(h->seg_cuts.ensure(segs * SPLIT_SCAP * sizeof(DevCut)));
+        CHECK_HIP(h->seg_cuts.ensure(segs * split_scap(h->split_segc) * sizeof(DevCut)));
         h->seg_cap = (uint32_t)segs;
     }
     return SYNCR_CDC_OK;
@@ -495,6 +499,8 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
         h->kp.resolve_nosplit = strcmp(rs, "nosplit") == 0;
     }
     if (const char *a = getenv("SYNCR_CDC_SERIAL")) h->serial_scans = atoi(a) != 0;
+    if (const char *a = getenv("SYNCR_CDC_SPLIT_SEGC")) h->split_segc = std::max(256, atoi(a));        // A/B only
+    if (const char *a = getenv("SYNCR_CDC_SPLIT_BLOCKS")) h->split_blocks = std::max(1, atoi(a));     // A/B only
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
     if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
     if (const char *sp = getenv("SYNCR_B3_SPLIT")) h->b3_nosplit = atoi(sp) == 0;          // A/B only
@@ -629,8 +635,9 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         h->zpar = h->zlast = 0;
         CHECK_HIP(h->super_off.ensure(((size_t)h->nwords + 1) * 8));
         // dense tiles are rare (adversarial data); grow on demand in fetch()
+        // (scan waves take dense-list slots 8 at a time, so a list may hold up to
+        // ntiles + 8 x scan_grid slots, unused ones included: no clamp to ntiles)
         uint32_t dcap = std::max<uint32_t>(64u, h->ntiles / 256u);
-        dcap = std::min<uint32_t>(dcap, std::max<uint32_t>(h->ntiles, 1u));
         int32_t rc = ensure_dense(h, dcap);
         if (rc) return rc;
         rc = ensure_cand(h, std::max<uint64_t>(4096, 2ull * h->ntiles));
@@ -741,8 +748,10 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
 #endif
             bool rerun = false;
             if (ctr[CTR_FLAGS] & FLAG_DENSE_OVERFLOW) {
-                uint32_t want = std::min<uint32_t>(std::max<uint32_t>(h->ntiles, 1u),
-                                                   std::max<uint32_t>(ctr[CTR_DENSE] + ctr[CTR_DENSE] / 4 + 16, 2 * h->dense_cap));
+                // the counter includes the slots of every wave's last chunk: enough
+                const uint64_t need = (uint64_t)ctr[CTR_DENSE] + ctr[CTR_DENSE] / 4 + 16;
+                const uint64_t lim = (uint64_t)h->ntiles + 8ull * h->scan_grid + 64;
+                const uint32_t want = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(need, 2ull * h->dense_cap), lim);
                 int32_t rc = ensure_dense(h, want);
                 if (rc) return rc;
                 rerun = true;
@@ -775,7 +784,7 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
                 uint32_t sp[SPL_WORDS];
                 CHECK_HIP(hipMemcpy(sp, zblock(h, h->zlast) + split_ctr_offset(h), sizeof sp,
                                     hipMemcpyDeviceToHost));
-                h->split_stats[0] = h->split_launched ? 1u : 0u;
+                h->split_stats[0] = h->split_launched ? 4ull * h->split_blocks : 0ull;   // worker waves
                 h->split_stats[1] = sp[SPL_PUB64 + 1];          // split files (high half of the 64-bit count)
                 h->split_stats[2] = std::min<uint32_t>(sp[SPL_RESERVED], h->seg_cap);
                 h->split_stats[3] = sp[SPL_WALKED];

@@ -90,10 +90,10 @@ struct KParams {
 // segment b's start with exactly that R continues identically to segment b's
 // walk (the walk's future is a function of (s, R) only), so the file's walker
 // adopts segment b's cuts and jumps to where that walk linked in turn.
-constexpr uint32_t SPLIT_SEGC = 4096;                   // candidates per segment
-constexpr uint32_t SPLIT_SCAP = 3 * SPLIT_SEGC + 64;    // scratch cuts per segment walk
+constexpr uint32_t SPLIT_SEGC = 4096;                   // candidates per segment (default; Tables::seg_segc)
+__host__ __device__ constexpr uint32_t split_scap(uint32_t segc) { return 3 * segc + 64; }   // scratch cuts per walk
 constexpr uint64_t SPLIT_MIN_BYTES = 256ull << 10;       // smaller files never split
-constexpr uint32_t SPLIT_BLOCKS = 256;                  // extra resolve blocks (4 waves each)
+constexpr uint32_t SPLIT_BLOCKS = 256;                  // extra resolve blocks (4 waves each; default)
 constexpr uint32_t SPLIT_END = 0xffffffffu;             // SplitSeg::link: walked to the file end
 constexpr uint32_t SPLIT_ABORT = 0xfffffffeu;           // (segment walk state: gave up)
 // split[] words: a 64-bit count (split files << 32 | eligible walkers
@@ -162,7 +162,9 @@ struct Tables {
     uint32_t n_elig;               // order[0 .. n_elig): files of >= SPLIT_MIN_BYTES (largest first)
     uint32_t seg_cap;              // SplitSeg records
     SplitSeg *segs;                // [seg_cap]
-    DevCut *seg_cuts;              // [seg_cap * SPLIT_SCAP]
+    DevCut *seg_cuts;              // [seg_cap * seg_scap]
+    uint32_t seg_segc, seg_scap;   // candidates per segment, scratch cuts per segment walk
+    uint32_t split_blocks;         // extra resolve blocks (split workers)
     uint32_t *split;               // [SPL_WORDS] counters                    (zeroed per launch)
     uint32_t epoch;                // this launch's id (!= 0, unique in the process): SplitSeg::ready
     // The per-launch counters above (ctr, nonempty, super_cnt, split) live in one

@@ -293,11 +293,23 @@ __device__ __forceinline__ void rewalk_dirty(const KParams &P, int lane, uint32_
     }
 }
 
+// Dense-list slots are handed to a wave DENSE_CHUNK at a time: one atomic on
+// the list counter per 8 dense tiles of a wave instead of per tile (periodic
+// data makes tens of thousands of dense tiles, and a single counter serialises
+// them: the scan of the dense workload ran 0.2 ms longer than random data's).
+// A chunk's unused slots stay DENSE_HOLE, which the dense pass and the gather
+// skip.
+constexpr uint32_t DENSE_CHUNK = 8;
+constexpr uint32_t DENSE_HOLE = 0xffffffffu;
+struct DenseSlots {
+    uint32_t lo = 0, hi = 0;       // the wave's unused slots [lo, hi) (wave-uniform)
+};
+
 // Publish this tile's candidates (sorted, with head fix-ups) or mark it dense.
 __device__ __forceinline__ void publish_tile(const uint8_t *__restrict__ data, const KParams &P,
                                              const Tables &T, uint32_t tile, int64_t t0,
                                              uint32_t *wlist, uint32_t *wcount, int lane,
-                                             bool force_dense) {
+                                             bool force_dense, DenseSlots &ds) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     // LDS-typed read: a generic (flat) read would wait vmcnt(0) on the tile DMA.
@@ -307,8 +319,17 @@ __device__ __forceinline__ void publish_tile(const uint8_t *__restrict__ data, c
     if (n == 0u && !force_dense) return;
     if (lane == 0) atomicOr(&T.nonempty[tile >> 6], 1ull << (tile & 63));
     if (n > (uint32_t)LISTCAP || force_dense) {
+        if (ds.lo == ds.hi) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&T.ctr[CTR_DENSE], DENSE_CHUNK);
+            base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
+            ds.lo = base;
+            ds.hi = base + DENSE_CHUNK;
+            if ((uint32_t)lane < DENSE_CHUNK && base + (uint32_t)lane < T.dense_cap)
+                T.dense_list[base + (uint32_t)lane] = DENSE_HOLE;
+        }
+        const uint32_t idx = ds.lo++;
         if (lane == 0) {
-            const uint32_t idx = atomicAdd(&T.ctr[CTR_DENSE], 1u);
             if (idx < T.dense_cap) {
                 T.dense_list[idx] = tile;
                 T.tile_meta[tile] = DENSE_BIT | idx;
@@ -433,6 +454,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     const int64_t span = (int64_t)T.span;
     issue_tile<RUN, (MODE & 4) != 0>(data, T.span, tile, lds0, lane);
     uint32_t gj = 0, pend = 0;
+    DenseSlots dslots_alloc;
     for (uint32_t next; tile < T.ntiles; tile = next) {
         bool grabbed = false;
         uint32_t gjn = 0;
@@ -495,7 +517,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             }
         }
         if (nd && nd <= (uint32_t)DIRTYCAP) rewalk_dirty<RUN>(P, lane, nd, dslots, lim_rel, wcount, wlist);
-        publish_tile(data, P, T, tile, t0, wlist, wcount, lane, nd > (uint32_t)DIRTYCAP);
+        publish_tile(data, P, T, tile, t0, wlist, wcount, lane, nd > (uint32_t)DIRTYCAP, dslots_alloc);
     }
 }
 
@@ -632,6 +654,7 @@ void cdc_scan3_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     issue_tile<RUN, NT>(data, T.span, tile, lds0, lane);
     if (lane == 0) { *wcount = 0u; *dcount = 0u; }
     uint32_t gj = 0, pend = 0;
+    DenseSlots dslots_alloc;
     // the previous tile's dirty groups: count, tile, this lane's slot and bytes
     uint32_t pnd = 0, ptile = 0, prel = 0;
     uint4 ra[5], rb[5];
@@ -659,7 +682,7 @@ void cdc_scan3_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         if (pnd) {
             const int64_t pt0 = (int64_t)ptile * TILE;
             if ((uint32_t)lane < pnd) rewalk_reread<RUN>(P, prel, ra, rb, span - pt0, wcount, wlist);
-            publish_tile(data, P, T, ptile, pt0, wlist, wcount, lane, false);
+            publish_tile(data, P, T, ptile, pt0, wlist, wcount, lane, false, dslots_alloc);
             if (lane == 0) *wcount = 0u;
         }
         uint32_t A[NQ * 4], B[NQ * 4];
@@ -702,7 +725,7 @@ void cdc_scan3_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             __builtin_amdgcn_wave_barrier();
             if (lane == 0) *dcount = 0u;
             if (nd > (uint32_t)DIRTYCAP3) {
-                publish_tile(data, P, T, tile, t0, wlist, wcount, lane, true);    // exact dense pass
+                publish_tile(data, P, T, tile, t0, wlist, wcount, lane, true, dslots_alloc);    // exact dense pass
             } else {
                 pnd = nd;
                 ptile = tile;
@@ -721,7 +744,7 @@ void cdc_scan3_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         wait_vmcnt<0>();
         const int64_t pt0 = (int64_t)ptile * TILE;
         if ((uint32_t)lane < pnd) rewalk_reread<RUN>(P, prel, ra, rb, span - pt0, wcount, wlist);
-        publish_tile(data, P, T, ptile, pt0, wlist, wcount, lane, false);
+        publish_tile(data, P, T, ptile, pt0, wlist, wcount, lane, false, dslots_alloc);
     }
 }
 
@@ -812,6 +835,7 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
     issue_buf<BUF, TILE, NT>(data, T.span, tile, lds0, lane);
     if (DB && tile + stride < T.ntiles && (MODE & 3) != 2)
         issue_buf<BUF, TILE, NT>(data, T.span, tile + stride, lds0 + BUF, lane);
+    DenseSlots dslots_alloc;
     uint32_t cur = 0;                                 // buffer of this tile
     for (; tile < T.ntiles; tile += stride, cur ^= (DB ? 1u : 0u)) {
         const uint32_t after = tile + (DB ? 2 : 1) * stride;   // lands in this tile's buffer
@@ -917,7 +941,7 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
                 }
             }
         }
-        publish_tile(data, P, T, tile, t0, wlist, wcount, lane, false);
+        publish_tile(data, P, T, tile, t0, wlist, wcount, lane, false, dslots_alloc);
     }
 }
 #endif  // SYNCR_CDC_DEV
@@ -930,16 +954,35 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
 // on byte loads: of every candidate e (first chunk-local hit in [e+1, e+63])
 // and of every read-boundary grid point (first chunk-local hit in
 // [p, min(p+63, file end)), stored as offset + 1).
-// First chunk-local hit in [e+1, e+63] (as k = hit - e; 0 = none) for a chunk
-// starting at e+1, from global memory.  The window's bytes are fetched in one
-// round: four unaligned 16-byte loads (gfx950 global loads are
-// unaligned-capable) when the 64 bytes after e lie inside the batch.  Bytes at
-// or past `lim` are outside the file: no hit there.
-__device__ __forceinline__ uint32_t head_fix_fast(const uint8_t *__restrict__ data, uint64_t span, uint64_t lim,
-                                                  uint64_t e, uint32_t mask) {
-    const uint64_t a = e + 1;
-    uint32_t w[16];
-    if (a + 64 <= span) {
+// Head fix-ups, two per thread as the 16-bit halves of packed registers (the
+// scan's trick): item k of the launch (a candidate, or past the candidates a
+// read-boundary grid point) rolls its 63 bytes from a zeroed window:
+//   S += x; T += k S                    (T = ((s2 + 1) k) mod 2^16, s2 = 124992 + W)
+//   Z = ((S + 1985) & m1) | T           zero iff the digest test passes
+//   acc = 2 acc + sat(1 - Z)            16-position hit masks, first position in bit 15
+// and the first hit is the leading one of the 63-bit mask (clz).  ~3.5 VALU per
+// item-byte against ~9.5 for one item per thread with an exit per byte; the
+// dense workload has a candidate every 64 bytes (7.5 M per launch).
+// (Fusing fix-ups into the dense and gather launches -- no separate launch --
+// measured 8 us SLOWER per step on zipf10k: the per-lane serial fix-ups
+// lengthen the gather's critical path; profiles/r02_ab_run_fusefix.log.)
+__device__ __forceinline__ void fix_item(const Tables &T, uint64_t n, uint64_t i, uint64_t &a, uint32_t &cnt) {
+    if (i < n) {                                          // a candidate e: chunk starts at e + 1
+        a = (T.cand[i] & CAND_POS_MASK) + 1;
+        cnt = (uint32_t)min<uint64_t>(63ull, T.span > a ? T.span - a : 0ull);
+    } else if (i < n + T.ngrid) {                         // a grid point p: chunk starts at p, ends by the file's end
+        a = T.gpos[i - n];
+        const uint64_t end = T.gend[i - n];
+        cnt = (uint32_t)min<uint64_t>(63ull, end > a ? end - a : 0ull);
+    } else {
+        a = 0;
+        cnt = 0;
+    }
+}
+
+__device__ __forceinline__ void fix_load(const uint8_t *__restrict__ data, uint64_t span, uint64_t a, uint32_t cnt,
+                                         uint32_t (&w)[16]) {
+    if (cnt && a + 64 <= span) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             uint4 v;
@@ -951,42 +994,66 @@ __device__ __forceinline__ uint32_t head_fix_fast(const uint8_t *__restrict__ da
         for (int i = 0; i < 16; ++i) {
             uint32_t x = 0;
             for (int b = 0; b < 4; ++b)
-                if (a + 4 * i + b < span) x |= (uint32_t)data[a + 4 * i + b] << (8 * b);
+                if ((uint32_t)(4 * i + b) < cnt) x |= (uint32_t)data[a + 4 * i + b] << (8 * b);
             w[i] = x;
         }
     }
-    const uint32_t n = lim > a ? (uint32_t)min<uint64_t>(63ull, lim - a) : 0u;
-    uint32_t S = 0, W = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 63; ++k) {
-        const uint32_t x = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        S += x;
-        W += S;
-        if (k < n && hit_exact(S, W, mask)) return k + 1;
-    }
-    return 0;
 }
 
-// One thread per candidate and per grid point.  (Fusing these into the dense
-// and gather launches -- no separate launch -- measured 8 us SLOWER per step on
-// zipf10k: the per-lane serial fix-ups lengthen the gather's critical path;
-// profiles/r02_ab_run_fusefix.log.)
+// first hit among the first cnt of 63 positions from the four 16-position masks of one half
+__device__ __forceinline__ uint32_t fix_first(uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3, uint32_t cnt) {
+    uint64_t m = ((uint64_t)m0 << 48) | ((uint64_t)m1 << 32) | ((uint64_t)m2 << 16) | (uint64_t)m3;
+    m &= cnt ? ~0ull << (64 - cnt) : 0ull;
+    return m ? (uint32_t)__builtin_clzll(m) + 1u : 0u;
+}
+
 __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict__ data, KParams P,
                                                       Tables T) {
     const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
     const uint64_t n = total < T.cand_cap ? total : T.cand_cap;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n + T.ngrid; i += (uint64_t)gridDim.x * 256) {
-        if (i < n) {
-            const uint64_t e = T.cand[i] & CAND_POS_MASK;
-            const uint32_t fix = head_fix_fast(data, T.span, T.span, e, P.mask);
-            T.cand[i] = e | ((uint64_t)fix << 48) | CAND_KNOWN;
-        } else {
-            const uint64_t g = i - n;
-            const uint64_t p = T.gpos[g];
-            // head_fix_fast(p - 1) scans [p, p+63) with the window reset at p
-            const uint64_t end = T.gend[g];
-            uint32_t f = head_fix_fast(data, T.span, end, p - 1, P.mask);
-            T.gfix[g] = (uint8_t)f;
+    const uint64_t items = n + T.ngrid;
+    const uint32_t m1x2 = P.m1 | (P.m1 << 16);
+    const uint32_t t0 = ((124993u * P.k) & 0xffffu) * 0x00010001u;   // T of an empty window, both halves
+    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; 2 * q < items; q += (uint64_t)gridDim.x * 256) {
+        uint64_t aA, aB;
+        uint32_t nA, nB;
+        fix_item(T, n, 2 * q, aA, nA);
+        fix_item(T, n, 2 * q + 1, aB, nB);
+        uint32_t A[16], B[16];
+        fix_load(data, T.span, aA, nA, A);
+        fix_load(data, T.span, aB, nB, B);
+        uint32_t S = 0, acc[4];
+        u16x2 Tv = as_u16x2(t0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                const int k = 16 * g + jj;
+                if (k < 63) {
+                    const uint32_t x = __builtin_amdgcn_perm(B[k >> 2], A[k >> 2],
+                                                             0x0C040C00u + (uint32_t)(k & 3) * 0x00010001u);
+                    S += x;                                               // halves < 2^15: no carry
+                    Tv = pk_mad(S, P.kk, Tv);                             // T += k S
+                    const uint32_t U = as_u32(as_u16x2(S) + (u16x2){(unsigned short)1985, (unsigned short)1985});
+                    const uint32_t Z = (U & m1x2) | as_u32(Tv);
+                    uint32_t h;
+                    asm volatile("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(h) : "s"(0x00010001u), "v"(Z));
+                    m = as_u32(pk_mad(m, 0x00020002u, as_u16x2(h)));     // m = 2 m + h
+                } else {
+                    m = as_u32(pk_mad(m, 0x00020002u, as_u16x2(0u)));    // position 63: none
+                }
+            }
+            acc[g] = m;
+        }
+        const uint32_t fA = fix_first(acc[0] & 0xffffu, acc[1] & 0xffffu, acc[2] & 0xffffu, acc[3] & 0xffffu, nA);
+        const uint32_t fB = fix_first(acc[0] >> 16, acc[1] >> 16, acc[2] >> 16, acc[3] >> 16, nB);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint64_t i = 2 * q + (uint64_t)h;
+            const uint32_t f = h ? fB : fA;
+            if (i < n) T.cand[i] = ((h ? aB : aA) - 1) | ((uint64_t)f << 48) | CAND_KNOWN;
+            else if (i < items) T.gfix[i - n] = (uint8_t)f;
         }
     }
 }
@@ -1014,6 +1081,7 @@ __global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict
     const int64_t span = (int64_t)T.span;
     for (uint32_t idx = blockIdx.x; idx < nd; idx += gridDim.x) {
         const uint32_t tile = T.dense_list[idx];
+        if (tile == DENSE_HOLE) continue;
         const int64_t base = (int64_t)tile * TB - HALO;
         __syncthreads();                                 // the previous tile's LDS reads are done
         for (uint32_t o = (uint32_t)lane * 16u; o < BUFB; o += 1024u) {
@@ -1189,47 +1257,48 @@ __device__ __forceinline__ void scan_dense_tile(const uint8_t *__restrict__ data
     }
 }
 
-// Dense tiles, packed (the product's dense pass for the scan's tile
-// geometry): the tile and its halo are staged in LDS exactly like the scan's
-// landing buffer, and lane l rolls runs l and l+64 as the two 16-bit halves of
-// packed registers, as the scan does (roll_fast), but tests every position
-// exactly instead of filtering 16-byte groups.  Per byte pair:
-//   S += x - d; V = S - 64 d; T += k V           as in the scan (4 ops)
-//   Z = ((S + 1985) & m1) | T                    zero iff both halves of the
-//        digest test pass: (s1 & m1) == m1 <=> ((s1 + 1) & m1) == 0 for the
-//        low-bit mask m1 = mask >> 16, s1 = 1984 + S; T = ((s2+1) k) mod 2^16
-//   h = sat(1 - Z); acc = 2 acc + h              (v_pk_sub_u16 clamp, v_pk_mad_u16)
-// so each run's 16-position group ends as a 16-bit hit mask (first position
-// in bit 15; one v_bfrev per group puts both runs' masks in bitmap order).
-// ~9.4 VALU per byte pair against ~27 for the byte-at-a-time exact roll.
-// The bitmap halfwords go through LDS (the staging buffer, once the runs are
-// in registers) and out as coalesced 16-byte stores.
+// Dense tiles, packed (the product's dense pass): the scan's own two-stage
+// pipeline -- a wave's tile lands in its LDS buffer by LDS-DMA, is copied to
+// registers (lane l: runs l and l+64 with their warm-up bytes), and the next
+// dense tile's DMA is issued at once, so it lands while this one is rolled by
+// dense_roll.  Edge tiles clamp out-of-range pieces like the scan (their bytes
+// only feed positions outside [0, span), which are masked, or before a file's
+// 63rd byte, which the resolve never reads).  The bitmap halfwords go straight
+// to dense_bits.
+__device__ __forceinline__ uint32_t sload_u32(const uint32_t *p) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const uint64_t u = ((uint64_t)hi << 32) | (uint64_t)lo;
+    uint32_t v;
+    asm volatile("s_nop 4\n\ts_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(u) : "memory");
+    return v;
+}
+
 template <int RUN>
 __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__restrict__ data, KParams P,
                                                               Tables T) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dbuf[];   // [HALO + tile]
-    constexpr int TILE = tile_bytes(RUN), BUF = buf_bytes(RUN), NQ = (HALO + RUN) / 16, NG = RUN / 16;
+    constexpr int TILE = tile_bytes(RUN), NQ = (HALO + RUN) / 16, NG = RUN / 16;
     const int lane = threadIdx.x;
-    const uint32_t nd = min(T.ctr[CTR_DENSE], T.dense_cap);
+    const uint32_t nd = min(sload_u32(&T.ctr[CTR_DENSE]), T.dense_cap);
+    uint32_t idx = blockIdx.x;
+    if (idx >= nd) return;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(dbuf));
     const int64_t span = (int64_t)T.span;
-    for (uint32_t idx = blockIdx.x; idx < nd; idx += gridDim.x) {
-        const uint32_t tile = T.dense_list[idx];
-        const int64_t t0 = (int64_t)tile * TILE, base = t0 - HALO;
-        __syncthreads();                                 // the previous tile's bitmap has left LDS
-        for (uint32_t o = (uint32_t)lane * 16u; o < (uint32_t)BUF; o += 1024u) {
-            const int64_t g = base + o;
-            uint4 v;
-            if (g >= 0 && g + 16 <= span) {
-                v = *(const uint4 *)(data + g);          // d_bytes and the tile size are 16-byte aligned
-            } else {                                     // batch edges: zeros outside [0, span)
-                uint32_t w4[4] = {0u, 0u, 0u, 0u};
-                for (int b = 0; b < 16; ++b)
-                    if (g + b >= 0 && g + b < span) w4[b >> 2] |= (uint32_t)data[g + b] << (8 * (b & 3));
-                v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-            }
-            *(uint4 *)(dbuf + o) = v;
-        }
-        __syncthreads();
+    // unused slots of the scan waves' chunks (DENSE_HOLE) are skipped
+    uint32_t tile = sload_u32(&T.dense_list[idx]);
+    while (tile == DENSE_HOLE) {
+        idx += gridDim.x;
+        if (idx >= nd) return;
+        tile = sload_u32(&T.dense_list[idx]);
+    }
+    issue_tile<RUN, true>(data, T.span, tile, lds0, lane);
+    for (uint32_t next; idx < nd; idx = next) {
+        next = idx + gridDim.x;
+        uint32_t ntile = DENSE_HOLE;
+        while (next < nd && (ntile = sload_u32(&T.dense_list[next])) == DENSE_HOLE) next += gridDim.x;
+        wait_vmcnt<0>();                                          // this tile has landed
         uint32_t A[NQ * 4], B[NQ * 4];
         {
             const uint4 *la = (const uint4 *)(dbuf + lane * RUN);          // = run start - 64
@@ -1241,20 +1310,20 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
                 B[4 * q + 0] = b.x; B[4 * q + 1] = b.y; B[4 * q + 2] = b.z; B[4 * q + 3] = b.w;
             }
         }
-        __syncthreads();                                 // every lane's runs are in registers: LDS is free
-        uint16_t *bm = (uint16_t *)dbuf;                 // halfword r * NG + g: run r, positions 16g..16g+15
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // runs are in registers
+        if (next < nd) issue_tile<RUN, true>(data, T.span, ntile, lds0, lane);
+        const int64_t t0 = (int64_t)tile * TILE;
+        uint16_t *bm = (uint16_t *)(T.dense_bits + (size_t)idx * (TILE / 32));
         uint32_t cnt = dense_roll<RUN>(A, B, P, lane, span - t0, [&](int g, uint32_t r) {
             bm[lane * NG + g] = (uint16_t)(r >> 16);
             bm[(lane + 64) * NG + g] = (uint16_t)r;
         });
-        __syncthreads();
-        uint4 *out = (uint4 *)(T.dense_bits + (size_t)idx * (TILE / 32));
-        for (uint32_t o = (uint32_t)lane; o < (uint32_t)(TILE / 128); o += 64u) out[o] = ((const uint4 *)dbuf)[o];
         for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
         if (lane == 0) {
             T.dense_cnt[idx] = cnt;
             atomicAdd(&T.super_cnt[tile >> 6], cnt);
         }
+        tile = ntile;
     }
 }
 
@@ -1332,6 +1401,7 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
     const uint32_t nw = T.tile / 32;
     for (uint32_t idx = wid; idx < nd; idx += nw_waves) {
         const uint32_t tile = T.dense_list[idx];
+        if (tile == DENSE_HOLE) continue;                        // an unused slot of a wave's chunk
         const uint32_t w = tile >> 6;
         // this tile's output offset: its word's prefix of per-tile counts
         const unsigned long long bits = T.nonempty[w];
@@ -1573,10 +1643,11 @@ __device__ __forceinline__ void split_setup(const KParams &P, const Tables &T, u
     if (!P.resolve_nosplit && F && F <= 0xFFFFFF00ull && T.seg_cap) {
         const uint32_t w0 = (uint32_t)((g0 / T.tile) >> 6), w1 = (uint32_t)(((g0 + F - 1) / T.tile) >> 6);
         const uint64_t a0 = T.super_off[w0], a1 = T.super_off[w0 + 1], b0 = T.super_off[w1], b1 = T.super_off[w1 + 1];
-        if (b1 - a0 >= 2ull * SPLIT_SEGC) {                       // upper bound on the file's candidates
+        const uint64_t SEGC = T.seg_segc;
+        if (b1 - a0 >= 2ull * SEGC) {                             // upper bound on the file's candidates
             const uint64_t j0 = wave_lower_bound(T.cand, min(a0, ncand), min(a1, ncand), g0, lane);
             const uint64_t j1 = wave_lower_bound(T.cand, min(b0, ncand), min(b1, ncand), g0 + F, lane);
-            const uint64_t ns = j1 > j0 ? (j1 - j0) / SPLIT_SEGC : 0;
+            const uint64_t ns = j1 > j0 ? (j1 - j0) / SEGC : 0;
             if (ns >= 2 && ns < 0x10000ull) {
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(&T.split[SPL_RESERVED], (uint32_t)ns - 1u);
@@ -1589,7 +1660,7 @@ __device__ __forceinline__ void split_setup(const KParams &P, const Tables &T, u
                     SplitSeg &g = T.segs[q];
                     g.k = 0;                                          // unusable unless it fits
                     if (fits) {
-                        const uint64_t cidx = j0 + (uint64_t)(r + 1) * SPLIT_SEGC;
+                        const uint64_t cidx = j0 + (uint64_t)(r + 1) * SEGC;
                         const uint64_t s0 = (T.cand[cidx] & CAND_POS_MASK) - g0 + 1;
                         g.cidx = cidx;
                         g.out_off = 0;
@@ -1641,8 +1712,8 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                                              bool elig, uint32_t spec) {
     constexpr Off OMAX = (Off)~(Off)0;
     const bool is_spec = spec != SPLIT_END;
-    DevCut *out = is_spec ? T.seg_cuts + (uint64_t)spec * SPLIT_SCAP : T.cuts + T.cut_base[i];
-    const uint64_t cap = is_spec ? (uint64_t)SPLIT_SCAP : (uint64_t)T.cut_cap[i];
+    DevCut *out = is_spec ? T.seg_cuts + (uint64_t)spec * T.seg_scap : T.cuts + T.cut_base[i];
+    const uint64_t cap = is_spec ? (uint64_t)T.seg_scap : (uint64_t)T.cut_cap[i];
     const Off Fo = (Off)F;
     const Off MAX = (Off)min<uint64_t>(P.max_chunk, (uint64_t)OMAX);
     const Off CAP = P.read_cap ? (Off)min<uint64_t>(P.read_cap, (uint64_t)OMAX) : OMAX;
@@ -2210,7 +2281,7 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
         if (g.k == 0u || g.verdict != 1u || g.ready != T.epoch) continue;
         const uint32_t i = g.file;
         const uint64_t cap = T.cut_cap[i], o = g.out_off, n = g.n;
-        const DevCut *src = T.seg_cuts + (uint64_t)q * SPLIT_SCAP;
+        const DevCut *src = T.seg_cuts + (uint64_t)q * T.seg_scap;
         DevCut *dst = T.cuts + T.cut_base[i];
         for (uint64_t t = (uint64_t)lane; t < n && o + t < cap; t += 64) dst[o + t] = src[t];
     }
@@ -2537,7 +2608,8 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
     if (dense_inline) {
         // (development A/B) the scan passed its dense tiles itself
     } else if (t.tile == (uint32_t)tile_bytes(DEFAULT_RUN)) {
-        hipLaunchKernelGGL(cdc_dense_packed_kernel<DEFAULT_RUN>, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
+        hipLaunchKernelGGL(cdc_dense_packed_kernel<DEFAULT_RUN>, dim3(dblocks), dim3(64), buf_bytes(DEFAULT_RUN), s,
+                           d, p, t);
     } else {                                          // other scan geometries (development library)
 #ifdef SYNCR_CDC_DEV
         hipLaunchKernelGGL(cdc_dense_kernel, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
@@ -2549,7 +2621,7 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
     // expansions per wave on the dense workload: 0.2 ms.)
     const uint32_t dgb = std::min<uint32_t>((t.dense_cap + 3) / 4, 2048u);
     hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4 + dgb), dim3(256), 0, s, t);
-    const uint64_t want = (t.cand_cap + t.ngrid + 255) / 256;
+    const uint64_t want = (t.cand_cap + t.ngrid + 511) / 512;       // two items per thread
     const uint32_t blocks = (uint32_t)(want < 2048 ? (want ? want : 1) : 2048);
     hipLaunchKernelGGL(cdc_fix_kernel, dim3(blocks), dim3(256), 0, s, d, p, t);
     return hipGetLastError();
@@ -2565,9 +2637,9 @@ hipError_t launch_resolve(const uint8_t *d, const KParams &p, const Tables &t, h
         hipLaunchKernelGGL(cdc_resolve_kernel, dim3((t.nfiles + 63) / 64), dim3(64), 0, s, d, p, t);
     else {
         const bool split = resolve_splits(p, t);
-        hipLaunchKernelGGL(cdc_resolve_wave_kernel, dim3((t.nfiles + 3) / 4 + (split ? SPLIT_BLOCKS : 0u)),
+        hipLaunchKernelGGL(cdc_resolve_wave_kernel, dim3((t.nfiles + 3) / 4 + (split ? t.split_blocks : 0u)),
                            dim3(256), 0, s, d, p, t);
-        if (split) hipLaunchKernelGGL(cdc_split_copy_kernel, dim3(SPLIT_BLOCKS), dim3(256), 0, s, t);
+        if (split) hipLaunchKernelGGL(cdc_split_copy_kernel, dim3(1024), dim3(256), 0, s, t);
     }
     return hipGetLastError();
 }

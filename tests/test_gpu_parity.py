@@ -577,9 +577,9 @@ def test_split_walks(bits, mx, cap):
         for k in got:
             assert got[k][i] == want[i], (i, int(lens[i]), bits, mx, cap, k)
     sp = stats[0]
-    assert sp["workers_launched"] == 1 and sp["files_split"] >= 1 and sp["segments"] >= 1, sp
+    assert sp["workers"] > 0 and sp["files_split"] >= 1 and sp["segments"] >= 1, sp
     assert sp["walked"] >= 1 and sp["adopted"] >= 1 and sp["giveups"] == 0, sp
-    assert stats[syncr_amd.FLAG_RESOLVE_NOSPLIT]["workers_launched"] == 0
+    assert stats[syncr_amd.FLAG_RESOLVE_NOSPLIT]["workers"] == 0
 
 
 @pytest.mark.parametrize("bits,mx,cap", [(8, 4096, 3000), (20, 16 << 20, 2 << 20)])
@@ -594,5 +594,5 @@ def test_split_workers_give_up(bits, mx, cap):
         got = [ends_of(r) for r in ch.batch_arrays(data, offs, lens)]
         sp = ch.split_stats()
     assert got == _split_oracle(data, offs, lens, bits, mx, cap)
-    assert sp["workers_launched"] == 1 and sp["files_split"] >= 1, sp
-    assert sp["giveups"] == 1024 and sp["walked"] == 0 and sp["adopted"] == 0, sp
+    assert sp["workers"] > 0 and sp["files_split"] >= 1, sp
+    assert sp["giveups"] == sp["workers"] and sp["walked"] == 0 and sp["adopted"] == 0, sp

@@ -43,6 +43,11 @@ def main():
     base = syncr_amd.Chunker()
     buf = syncr_amd.DeviceBuffer(base, span)
     buf.gen_corpus(offs, sizes, indices=idx)
+    if args.workload == "dense":
+        from benchlib import legs
+        legs.fill_dense(buf, offs, sizes, idx)
+    elif args.workload == "dense1":
+        buf.upload(np.resize(bench.periodic_pattern(), span))
     handles = []
     for v in args.variants:
         saved = dict(os.environ)
@@ -55,7 +60,7 @@ def main():
         c.plan(offs, sizes, span)
         c.launch(buf.ptr, hashed=args.hashed)
         ref = c.fetch(hashed=args.hashed)
-        if handles and args.hashed:      # every variant must give the first variant's records
+        if handles:                      # every variant must give the first variant's records
             same = all(np.array_equal(a, b) for a, b in zip(ref, handles[0][3]))
             print(f"{v}: records {'identical to' if same else 'DIFFER from'} {handles[0][0]}", flush=True)
         handles.append((v, c, sum(x.size for x in ref), ref))

@@ -9,5 +9,5 @@ shift
 cd /tmp && export TMPDIR=/tmp
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py --workload dense --steps 10 --warmup 3 --no-cpu-baseline --no-legs --sustained-steps 0 --no-hashed --pipeline-depth 1 --no-read-probe "$@" > $OUT/bench_trace.log 2>&1 || exit 11
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-legs --sustained-steps 0 --no-hashed --pipeline-depth 1 --no-read-probe --workload dense "$@" > $OUT/bench_trace.log 2>&1 || exit 11
 find $OUT -name "*kernel_stats.csv" | head -1 | xargs cat
