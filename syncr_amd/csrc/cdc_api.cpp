@@ -173,8 +173,13 @@ uint32_t default_cut_cap(uint64_t len, uint32_t bits) {
     return (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
 }
 
-// the per-launch zeroed block: ctr[4] | nonempty[nwords] (u64) | super_cnt[nwords] (u32) | split[SPL_WORDS]
-size_t split_ctr_offset(const syncr_cdc *h) { return (16 + (size_t)h->nwords * 12 + 15) & ~size_t(15); }
+// the per-launch zeroed block: ctr[4] | nonempty[nwords] (u64) | super_cnt[nwords] (u32) |
+// coarse[ncoarse * COARSE_STRIDE] (u32, 128-byte aligned) | split[SPL_WORDS]
+uint32_t ncoarse(const syncr_cdc *h) { return (h->nwords + 63) / 64; }
+size_t coarse_offset(const syncr_cdc *h) { return (16 + (size_t)h->nwords * 12 + 127) & ~size_t(127); }
+size_t split_ctr_offset(const syncr_cdc *h) {
+    return coarse_offset(h) + (size_t)ncoarse(h) * COARSE_STRIDE * 4;
+}
 size_t zeroed_bytes(const syncr_cdc *h) { return split_ctr_offset(h) + SPL_WORDS * 4; }
 size_t zstride(const syncr_cdc *h) { return (zeroed_bytes(h) + 255) & ~size_t(255); }
 uint8_t *zblock(const syncr_cdc *h, uint32_t par) { return h->zeroed.as<uint8_t>() + par * zstride(h); }
@@ -199,6 +204,8 @@ Tables make_tables(syncr_cdc *h) {
     t.ctr = reinterpret_cast<uint32_t *>(zb);
     t.nonempty = reinterpret_cast<unsigned long long *>(zb + 16);
     t.super_cnt = reinterpret_cast<uint32_t *>(zb + 16 + (size_t)h->nwords * 8);
+    t.coarse = reinterpret_cast<uint32_t *>(zb + coarse_offset(h));
+    t.ncoarse = ncoarse(h);
     t.super_off = h->super_off.as<uint64_t>();
     t.dense_list = h->dense_list.as<uint32_t>();
     t.dense_cnt = h->dense_cnt.as<uint32_t>();

@@ -15,6 +15,10 @@ constexpr int RUNS = 128;                // runs per wave tile
 constexpr int HALO = 64;                 // window warm-up bytes before the tile
 constexpr int LISTCAP = 64;              // candidate slots per tile
 constexpr uint32_t DENSE_BIT = 0x80000000u;
+// Tables::coarse keeps one counter per 128-byte line: the waves of a launch
+// work through a window of nearby tiles, so their atomics meet on a few
+// counters, and counters sharing a line serialise in one L2 channel.
+constexpr uint32_t COARSE_STRIDE = 32;
 constexpr uint64_t NONE = ~0ull;
 constexpr int DEFAULT_RUN = 144;
 
@@ -111,7 +115,7 @@ struct SplitSeg {            // 64 bytes
     uint32_t first, nseg;    // record of the file's boundary 1; the file's segment count
     uint32_t n;              // cuts the segment walk produced
     uint32_t link;           // record of the boundary the walk linked at, or SPLIT_END
-    uint32_t status;         // 0 pending, 1 done, 2 aborted (release)
+    uint32_t status;         // 0 pending, 3 being walked, 1 done, 2 aborted (release)
     uint32_t verdict;        // 1: adopted by the file's walker
     uint32_t ready;          // == Tables::epoch: initialised in this launch (release)
     uint32_t pad;
@@ -139,7 +143,10 @@ struct Tables {
     uint2 *slots;                  // [ntiles*LISTCAP] {tile-relative pos, head fix-up}
     unsigned long long *nonempty;  // [nwords] tile has >=1 candidate        (zeroed per launch)
     uint32_t *super_cnt;           // [nwords] candidates per 64-tile group   (zeroed per launch)
-    uint64_t *super_off;           // [nwords+1] exclusive prefix of super_cnt
+    uint32_t *coarse;              // [ncoarse * COARSE_STRIDE] candidates per 64 groups (4096 tiles),
+                                   // one counter per 128-byte line (zeroed per launch)
+    uint32_t ncoarse;
+    uint64_t *super_off;           // [nwords+1] exclusive prefix of super_cnt (written by the gather)
     uint32_t *ctr;                 // [4]                                      (zeroed per launch)
     uint32_t *dense_list;          // [dense_cap] tile ids
     uint32_t *dense_cnt;           // [dense_cap] candidates per dense tile

@@ -351,6 +351,7 @@ __device__ __forceinline__ void publish_tile(const uint8_t *__restrict__ data, c
     if (lane == 0) {
         T.tile_meta[tile] = n;
         atomicAdd(&T.super_cnt[tile >> 6], n);
+        atomicAdd(&T.coarse[(tile >> 12) * COARSE_STRIDE], n);
     }
 }
 
@@ -1133,6 +1134,7 @@ __global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict
         if (lane == 0) {
             T.dense_cnt[idx] = cnt;
             atomicAdd(&T.super_cnt[tile >> 6], cnt);
+            atomicAdd(&T.coarse[(tile >> 12) * COARSE_STRIDE], cnt);
         }
     }
 }
@@ -1254,6 +1256,7 @@ __device__ __forceinline__ void scan_dense_tile(const uint8_t *__restrict__ data
         T.dense_cnt[idx] = cnt;
         T.tile_meta[tile] = DENSE_BIT | idx;
         atomicAdd(&T.super_cnt[tile >> 6], cnt);
+        atomicAdd(&T.coarse[(tile >> 12) * COARSE_STRIDE], cnt);
     }
 }
 
@@ -1282,22 +1285,29 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
     constexpr int TILE = tile_bytes(RUN), NQ = (HALO + RUN) / 16, NG = RUN / 16;
     const int lane = threadIdx.x;
     const uint32_t nd = min(sload_u32(&T.ctr[CTR_DENSE]), T.dense_cap);
-    uint32_t idx = blockIdx.x;
-    if (idx >= nd) return;
+    // Block b takes the contiguous list range [b*per, (b+1)*per): the list is
+    // in scan order, so a grid stride over it put the whole grid's coarse
+    // atomics on the one or two counters of the scan's window (dense workload:
+    // 248 vs 152 us); contiguous ranges spread them over the batch, and a
+    // wave adds its consecutive tiles' counts to a coarse counter once.
+    const uint32_t per = (nd + gridDim.x - 1) / gridDim.x;
+    uint32_t idx = blockIdx.x * per;
+    const uint32_t iend = min(nd, idx + per);
+    if (idx >= iend) return;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(dbuf));
     const int64_t span = (int64_t)T.span;
     // unused slots of the scan waves' chunks (DENSE_HOLE) are skipped
     uint32_t tile = sload_u32(&T.dense_list[idx]);
     while (tile == DENSE_HOLE) {
-        idx += gridDim.x;
-        if (idx >= nd) return;
+        if (++idx >= iend) return;
         tile = sload_u32(&T.dense_list[idx]);
     }
+    uint32_t cur_c = tile >> 12, acc_c = 0;
     issue_tile<RUN, true>(data, T.span, tile, lds0, lane);
-    for (uint32_t next; idx < nd; idx = next) {
-        next = idx + gridDim.x;
+    for (uint32_t next; idx < iend; idx = next) {
+        next = idx + 1;
         uint32_t ntile = DENSE_HOLE;
-        while (next < nd && (ntile = sload_u32(&T.dense_list[next])) == DENSE_HOLE) next += gridDim.x;
+        while (next < iend && (ntile = sload_u32(&T.dense_list[next])) == DENSE_HOLE) ++next;
         wait_vmcnt<0>();                                          // this tile has landed
         uint32_t A[NQ * 4], B[NQ * 4];
         {
@@ -1311,7 +1321,7 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // runs are in registers
-        if (next < nd) issue_tile<RUN, true>(data, T.span, ntile, lds0, lane);
+        if (next < iend) issue_tile<RUN, true>(data, T.span, ntile, lds0, lane);
         const int64_t t0 = (int64_t)tile * TILE;
         uint16_t *bm = (uint16_t *)(T.dense_bits + (size_t)idx * (TILE / 32));
         uint32_t cnt = dense_roll<RUN>(A, B, P, lane, span - t0, [&](int g, uint32_t r) {
@@ -1319,73 +1329,19 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
             bm[(lane + 64) * NG + g] = (uint16_t)r;
         });
         for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if ((tile >> 12) != cur_c) {
+            if (lane == 0 && acc_c) atomicAdd(&T.coarse[cur_c * COARSE_STRIDE], acc_c);
+            cur_c = tile >> 12;
+            acc_c = 0;
+        }
+        acc_c += cnt;
         if (lane == 0) {
             T.dense_cnt[idx] = cnt;
             atomicAdd(&T.super_cnt[tile >> 6], cnt);
         }
         tile = ntile;
     }
-}
-
-// Exclusive prefix of the per-64-tile candidate counts (one block).  Each
-// pass covers 4096 words: thread t loads words 4t..4t+3 (one coalesced 16-byte
-// load), the 1024 partial sums are scanned by wave shuffles plus one LDS pass
-// over the 16 wave totals, and the running carry moves to the next pass.
-__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint64_t u = __shfl_up(v, off);
-        if (lane >= off) v += u;
-    }
-    return v;
-}
-
-__global__ __launch_bounds__(1024) void cdc_prefix_kernel(Tables T) {
-    __shared__ uint64_t wsum[16];
-    const uint32_t n = T.nwords, t = threadIdx.x;
-    const int lane = t & 63, wv = t >> 6;
-    uint64_t carry = 0;
-    auto load4 = [&](uint32_t i0, uint32_t (&c)[4]) {
-        if (i0 + 3 < n && (n & 3) == 0) {
-            const uint4 v = *(const uint4 *)(T.super_cnt + i0);
-            c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) c[k] = i0 + k < n ? T.super_cnt[i0 + k] : 0u;
-        }
-    };
-    uint32_t nxt[4];
-    load4(4 * t, nxt);                                    // pass 0; pass p+1 is loaded during pass p
-    for (uint32_t base = 0; base < n; base += 4096) {
-        const uint32_t i0 = base + 4 * t;
-        uint32_t c[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
-        if (base + 4096 < n) load4(i0 + 4096, nxt);
-        const uint64_t mine = (uint64_t)c[0] + c[1] + c[2] + c[3];
-        const uint64_t incl = wave_incl_scan64(mine, lane);
-        if (lane == 63) wsum[wv] = incl;
-        __syncthreads();
-        uint64_t before = carry, total = carry;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint64_t x = wsum[k];
-            before += k < wv ? x : 0ull;
-            total += x;
-        }
-        __syncthreads();                                  // wsum reused next pass
-        uint64_t run = before + incl - mine;              // exclusive
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (i0 + k < n) T.super_off[i0 + k] = run;
-            run += c[k];
-        }
-        carry = total;
-    }
-    if (t == 0) {
-        T.super_off[n] = carry;
-        T.ctr[CTR_CANDS_LO] = (uint32_t)carry;
-        T.ctr[CTR_CANDS_HI] = (uint32_t)(carry >> 32);
-        if (carry > T.cand_cap) T.ctr[CTR_FLAGS] |= FLAG_CAND_OVERFLOW;
-    }
+    if (lane == 0 && acc_c) atomicAdd(&T.coarse[cur_c * COARSE_STRIDE], acc_c);
 }
 
 // Compact every tile's candidates into T.cand in position order (one wave per
@@ -1393,6 +1349,28 @@ __global__ __launch_bounds__(1024) void cdc_prefix_kernel(Tables T) {
 // lane copies its slot list; the wave then walks the group's dense tiles
 // together: 64 bitmap words at a time, a wave prefix of their popcounts gives
 // each lane its output run.
+// The exclusive prefix of the candidate counts before 64-tile group w, from
+// the counts per 4096 tiles (coarse) and per 64 tiles (super_cnt): two wave
+// reductions instead of a separate one-block prefix launch.  Every wave of the
+// gather computes its own word's prefix; the resolve reads super_off.
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, off), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), off);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t word_prefix(const Tables &T, uint32_t w, int lane) {
+    const uint32_t c = w >> 6;
+    uint64_t a = 0;
+    for (uint32_t k = (uint32_t)lane; k < c; k += 64) a += T.coarse[k * COARSE_STRIDE];
+    const uint32_t f = 64 * c + (uint32_t)lane;
+    if (f < w) a += T.super_cnt[f];
+    return readlane64(wave_sum64(a), 0);
+}
+
 // Dense tiles are expanded by the blocks past the word blocks, one wave per
 // dense tile (grid-stride over the dense list): a word of 64 dense tiles on
 // one wave was 64 dependent bitmap passes (dense1: 330 us for 2.1 M candidates).
@@ -1418,7 +1396,7 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
         }
         const uint32_t incl = wave_incl_scan(c, lane);
         const uint32_t j = tile & 63u;
-        const uint64_t tb = T.super_off[w] + (uint32_t)__builtin_amdgcn_readlane((int)(incl - c), (int)j);
+        const uint64_t tb = word_prefix(T, w, lane) + (uint32_t)__builtin_amdgcn_readlane((int)(incl - c), (int)j);
         const uint32_t tc = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)j);
         if (!tc || tb + tc > T.cand_cap) continue;                // overflow: flagged by prefix, re-run
         const uint32_t *bm = T.dense_bits + (size_t)idx * nw;
@@ -1448,6 +1426,19 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
         return;
     }
     if (w >= T.nwords) return;
+    if (w == 0) {                                             // the total (fix-ups, resolve, fetch)
+        uint64_t a = 0;
+        for (uint32_t k = (uint32_t)lane; k < T.ncoarse; k += 64) a += T.coarse[k * COARSE_STRIDE];
+        const uint64_t total = readlane64(wave_sum64(a), 0);
+        if (lane == 0) {
+            T.super_off[T.nwords] = total;
+            T.ctr[CTR_CANDS_LO] = (uint32_t)total;
+            T.ctr[CTR_CANDS_HI] = (uint32_t)(total >> 32);
+            if (total > T.cand_cap) T.ctr[CTR_FLAGS] |= FLAG_CAND_OVERFLOW;
+        }
+    }
+    const uint64_t pre = word_prefix(T, w, lane);
+    if (lane == 0) T.super_off[w] = pre;
     const unsigned long long bits = T.nonempty[w];
     if (!bits) return;
     const uint32_t tile = w * 64 + lane;
@@ -1463,7 +1454,7 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
         }
     }
     const uint32_t incl = wave_incl_scan(c, lane);
-    const uint64_t base = T.super_off[w] + (incl - c);
+    const uint64_t base = pre + (incl - c);
     const bool dense = has && (meta & DENSE_BIT) && c;
     if (has && c && !dense && base + c <= T.cand_cap) {   // overflow is flagged by prefix; host re-runs
         const uint64_t t0 = (uint64_t)tile * T.tile;
@@ -1625,6 +1616,14 @@ __device__ __forceinline__ uint64_t seg_ld(const uint64_t &f) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
 }
+
+// Wall-clock budget of a wave's waits on other waves (s_memrealtime, constant rate).
+struct Patience {
+    uint64_t deadline;
+    __device__ __forceinline__ explicit Patience(uint64_t ticks)
+        : deadline(ticks ? wall_clock64() + ticks : 0ull) {}
+    __device__ __forceinline__ bool spent() const { return deadline == 0ull || wall_clock64() > deadline; }
+};
 
 __device__ __forceinline__ unsigned long long *split_pub(const Tables &T) {
     return reinterpret_cast<unsigned long long *>(&T.split[SPL_PUB64]);
@@ -1859,6 +1858,13 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                         link = brec;
                         stop = true;
                         break;
+                    }
+                    // A segment a worker is walking right now (status 3) ends soon:
+                    // wait for it rather than walk it again.  The worker is resident
+                    // and its walk has no waits, so this ends; it is bounded anyway.
+                    {
+                        const Patience pat(P.split_patience);
+                        while (seg_ld(T.segs[brec].status) == 3u && !pat.spent()) __builtin_amdgcn_s_sleep(2);
                     }
                     // Adopt a chain of done segment walks at once: lane k reads record
                     // brec + k, and the chain brec -> link -> link ... is followed on
@@ -2218,14 +2224,6 @@ __device__ __forceinline__ uint64_t ld64_relaxed(const unsigned long long *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wall-clock budget of one worker's waits (s_memrealtime, constant rate).
-struct Patience {
-    uint64_t deadline;
-    __device__ __forceinline__ explicit Patience(uint64_t ticks)
-        : deadline(ticks ? wall_clock64() + ticks : 0ull) {}
-    __device__ __forceinline__ bool spent() const { return deadline == 0ull || wall_clock64() > deadline; }
-};
-
 __device__ __forceinline__ uint32_t give_up(const Tables &T, int lane) {
     if (lane == 0) atomicAdd(&T.split[SPL_GIVEUP], 1u);
     return SPLIT_END;
@@ -2264,6 +2262,7 @@ __device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P,
         if (q == SPLIT_END) break;
         if (seg_ld(T.segs[q].k) == 0u) continue;
         const uint32_t i = seg_ld(T.segs[q].file);
+        if (lane == 0) __hip_atomic_store(&T.segs[q].status, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         resolve_walk<uint32_t>(data, P, T, i, T.flen[i], T.foff[i], lane, false, q);
     }
 }
@@ -2615,7 +2614,6 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
         hipLaunchKernelGGL(cdc_dense_kernel, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);
 #endif
     }
-    hipLaunchKernelGGL(cdc_prefix_kernel, dim3(1), dim3(1024), 0, s, t);
     // + up to 2048 blocks (one wave per dense tile) that expand dense tiles; they
     // exit at once when there are none.  (256 blocks left ~33 serial tile
     // expansions per wave on the dense workload: 0.2 ms.)

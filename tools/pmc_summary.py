@@ -126,8 +126,13 @@ def main(tag, src=None):
     sq_csv = os.path.join(src, "pmc_sq", "run_counter_collection.csv")
     if os.path.exists(sq_csv):
         per = defaultdict(dict)
+        allk = defaultdict(lambda: defaultdict(dict))      # kernel -> dispatch -> counters
         for r in csv.DictReader(open(sq_csv)):
-            if short(r["Kernel_Name"]) != k:
+            kn = short(r["Kernel_Name"])
+            a = allk[kn][int(r["Dispatch_Id"])]
+            a[r["Counter_Name"]] = a.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            a["dur_ms"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            if kn != k:
                 continue
             d = per[int(r["Dispatch_Id"])]
             d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -138,7 +143,18 @@ def main(tag, src=None):
             clk = d.get("GRBM_GUI_ACTIVE", 0) / 8 / (d["dur_ms"] / 1e3) / 1e9 if d.get("dur_ms") else None
             rows.append({"dispatch": disp, "ms": round(d["dur_ms"], 4), "clock_ghz": round(clk, 3) if clk else None,
                          **{c: d[c] for c in d if c.startswith("SQ_")}})
+        per_kernel = {}
+        for kn, disp in allk.items():
+            ds = list(disp.values())
+            m = {c: sum(d.get(c, 0.0) for d in ds) / len(ds) for c in ds[0] if c.startswith(("SQ_", "GRBM_"))}
+            ms = sum(d["dur_ms"] for d in ds) / len(ds)
+            act = m.get("SQ_ACTIVE_INST_VALU", 0.0)
+            wc = m.get("SQ_WAVE_CYCLES", 0.0)
+            per_kernel[kn] = {"dispatches": len(ds), "ms_mean": round(ms, 4), **{c: round(v, 1) for c, v in m.items()},
+                              "valu_active_over_wave_cycles": round(act / wc, 4) if wc else None,
+                              "wait_any_over_wave_cycles": round(m.get("SQ_WAIT_ANY", 0.0) / wc, 4) if wc else None}
         json.dump({"kernel": k, "source": f"tools/prof.sh {tag} pass 4", "per_dispatch": rows,
+                   "per_kernel_mean": per_kernel,
                    "units": "SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* in quad-cycles (MI355X_MICROARCH.md); "
                             "clock = GRBM_GUI_ACTIVE / 8 XCDs / duration"},
                   open(os.path.join(dst, f"{tag}_pmc_sq.json"), "w"), indent=1)
