@@ -207,6 +207,13 @@ int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4);
 /* per sub-pipeline k: stats[4k..4k+3] = [device, files, bytes, batches];
  * SYNCR_CDC_ERANGE if n < 4 * ndevices */
 int32_t syncr_ingest_device_stats(const syncr_ingest *g, uint64_t *stats, uint32_t n);
+/* Fault injection (tests of the read-error contract, file_operations.rs:
+ * 727-744, 776-782): every later submit_file reads only the bytes before file
+ * offset `offset`; the read that would cross it fails with errno `err`
+ * (err = 0: it returns EOF there, as if the file shrank to `offset`).
+ * offset = UINT64_MAX (the default) turns it off. Applies to every
+ * sub-pipeline; set it before submitting the files it is meant for. */
+int32_t syncr_ingest_set_read_fault(syncr_ingest *g, uint64_t offset, int32_t err);
 /* release everything; files not yet delivered (no flush since their submit)
  * get no callback */
 void syncr_ingest_close(syncr_ingest *g);

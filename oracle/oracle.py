@@ -58,6 +58,8 @@ def lib():
         L.orc_chunk_closed_form.restype = ctypes.c_uint64
         L.orc_chunk_no_head_fixup.argtypes = L.orc_chunk_production.argtypes
         L.orc_chunk_no_head_fixup.restype = ctypes.c_uint64
+        L.orc_chunk_production_read_error.argtypes = L.orc_chunk_production.argtypes
+        L.orc_chunk_production_read_error.restype = ctypes.c_uint64
         L.orc_chunk_ideal.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                       _u64p, ctypes.c_uint64]
         L.orc_chunk_ideal.restype = ctypes.c_uint64
@@ -114,6 +116,13 @@ def _run(fn, data, *args) -> np.ndarray:
 def chunk_production(data, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE, read_cap=TOKIO_READ_CAP):
     """Cut END offsets of compute_file_chunks (file_operations.rs:721-788)."""
     return _run(lib().orc_chunk_production, data, bits, max_chunk, read_cap)
+
+
+def chunk_production_read_error(data, P, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE, read_cap=TOKIO_READ_CAP):
+    """Cut ends compute_file_chunks keeps when every read at file offset >= P
+    fails (file_operations.rs:738-743 for P = 0, :776-782 otherwise); only
+    data[:P] is ever read (bup_oracle.c orc_chunk_production_read_error)."""
+    return _run(lib().orc_chunk_production_read_error, _as_u8(data)[:P], bits, max_chunk, read_cap)
 
 
 def chunk_production_window(data, bits=CHUNK_BITS, max_chunk=MAX_CHUNK_SIZE, read_cap=TOKIO_READ_CAP):

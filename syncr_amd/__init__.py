@@ -56,6 +56,7 @@ EXPORTED_SYMBOLS = (
     "syncr_cache_open", "syncr_cache_get", "syncr_cache_put", "syncr_cache_sync", "syncr_cache_stats",
     "syncr_cache_close", "syncr_ingest_set_cache", "syncr_ingest_cache_hits",
     "syncr_ingest_open_multi", "syncr_ingest_device_stats", "syncr_cache_get_params",
+    "syncr_ingest_set_read_fault",
 )
 
 ABI_VERSION = 3
@@ -169,6 +170,7 @@ def library():
             "syncr_ingest_open_multi": ([ctypes.POINTER(_i32), _u32, ctypes.POINTER(Params), _u64, _u32, _u32,
                                          _INGEST_CB, _vp, ctypes.POINTER(_vp)], _i32),
             "syncr_ingest_device_stats": ([_vp, _pu64, _u32], _i32),
+            "syncr_ingest_set_read_fault": ([_vp, _u64, _i32], _i32),
             "syncr_cache_get": ([_vp, ctypes.c_char_p, _u32, _u64, _vp, _u64, _pu64], _i32),
             "syncr_cache_put": ([_vp, ctypes.c_char_p, _u32, _u64, _vp, _u64], _i32),
             "syncr_cache_sync": ([_vp], _i32),
@@ -567,6 +569,14 @@ class Ingest:
         hits = ctypes.c_uint64(0)
         _check(library().syncr_ingest_cache_hits(self._h, ctypes.byref(hits)), "syncr_ingest_cache_hits")
         return {"files": st[0], "bytes": st[1], "batches": st[2], "chunks": st[3], "cache_hits": hits.value}
+
+    def set_read_fault(self, offset: int | None, err: int = 0) -> None:
+        """Fault injection for tests of the read-error contract: later
+        submit_file calls read only the bytes before `offset`; the read that
+        would cross it fails with errno `err` (0: EOF there, a file that
+        shrank). offset None turns it off."""
+        off = 2**64 - 1 if offset is None else offset
+        _check(library().syncr_ingest_set_read_fault(self._h, off, err), "syncr_ingest_set_read_fault")
 
     def device_stats(self) -> list[dict]:
         """Per sub-pipeline: device, files, bytes, batches."""

@@ -164,6 +164,10 @@ struct Pipe {
     int32_t error = 0;                  // sticky engine error
     syncr_cache *cache = nullptr;       // optional (syncr_ingest_set_cache)
     std::atomic<uint64_t> cache_hits{0};
+    // syncr_ingest_set_read_fault: submit_file's reads stop at this file
+    // offset with fault_err (0 = EOF there, as if the file shrank)
+    std::atomic<uint64_t> fault_off{UINT64_MAX};
+    std::atomic<int32_t> fault_err{0};
 };
 
 int32_t hip_rc(hipError_t e) {
@@ -452,9 +456,24 @@ int32_t pipe_submit_file(Pipe *g, const char *path, uint64_t tag) {
     const unsigned pieces = len ? (unsigned)((len + PIECE - 1) / PIECE) : 0u;
     std::vector<uint64_t> got(pieces, 0);
     std::vector<int> perr(pieces, 0);
+    const uint64_t fault_off = g->fault_off.load();
+    const int fault_err = g->fault_err.load();
     auto read_piece = [&](unsigned i) {
         const uint64_t a = (uint64_t)i * PIECE, b = std::min<uint64_t>(len, a + PIECE);
+        const uint64_t e = std::min(b, std::max(a, fault_off));    // injected fault (test hook)
         uint64_t pos = a;
+        if (e < b) {
+            // bytes at and after the fault offset are never read
+            while (pos < e) {
+                const ssize_t r = pread(fd, dst + pos, (size_t)(e - pos), (off_t)pos);
+                if (r < 0 && errno == EINTR) continue;
+                if (r <= 0) break;
+                pos += (uint64_t)r;
+            }
+            if (pos == e) perr[i] = fault_err;
+            got[i] = pos - a;
+            return;
+        }
         while (pos < b) {
             const ssize_t r = pread(fd, dst + pos, (size_t)(b - pos), (off_t)pos);
             if (r < 0 && errno == EINTR) continue;
@@ -866,6 +885,15 @@ int32_t syncr_ingest_device_stats(const syncr_ingest *g, uint64_t *stats, uint32
         stats[4 * k + 1] = p->stats[0].load();           // files handled by this device
         stats[4 * k + 2] = p->stats[1].load();           // bytes
         stats[4 * k + 3] = p->stats[2].load();           // batches
+    }
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_ingest_set_read_fault(syncr_ingest *g, uint64_t offset, int32_t err) {
+    if (!g || err < 0) return SYNCR_CDC_EINVAL;
+    for (Pipe *p : g->pipes) {
+        p->fault_err.store(err);
+        p->fault_off.store(offset);
     }
     return SYNCR_CDC_OK;
 }

@@ -333,3 +333,51 @@ def test_oversized_file_fails_alone(tmp_path, devices):
         assert got[3][1] == -errno.ENOMEM and got[3][2].size == 0
         rest = got[:3] + got[4:]
     check([(i, s, a) for i, (_, s, a) in enumerate(rest)], files)
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_read_fault_keeps_reference_prefix(tmp_path, devices):
+    """the read-error contract end to end, through an injected read
+    fault (syncr_ingest_set_read_fault).  A read that fails at file offset P > 0
+    keeps the chunks compute_file_chunks cut before its loop breaks
+    (file_operations.rs:776-782; oracle orc_chunk_production_read_error) and
+    reports -errno; P = 0 is the failed first read (:738-743): -errno, no
+    chunks; a fault with errno 0 is EOF at P (a file that shrank): status 0 and
+    the chunks of the P bytes read.  Faults mid-piece, on a 2 MiB read-piece
+    boundary, near a cut and past the end; boundaries and BLAKE3 bit-exact."""
+    import bench
+    data = O.xorshift_bytes(4242, 13 * M + 777)
+    periodic = np.resize(bench.periodic_pattern(), M + 3)   # small: the literal oracle memmoves per cut
+    p_rand, p_per = tmp_path / "rand.bin", tmp_path / "per.bin"
+    p_rand.write_bytes(data.tobytes())
+    p_per.write_bytes(periodic.tobytes())
+    ends = O.chunk_production(data)
+    cases = [(p_rand, data, 5 * M + 123, errno.EIO), (p_rand, data, 6 * M, errno.EIO),
+             (p_rand, data, int(ends[2]) + 1, errno.EIO), (p_rand, data, 0, errno.EIO),
+             (p_rand, data, 7 * M + 5, 0), (p_rand, data, 20 * M, errno.EIO),
+             (p_per, periodic, 700 * 1024 + 17, errno.EIO), (p_per, periodic, 512 * 1024 + 64, 0)]
+    got = []
+    with syncr_amd.Ingest(batch_bytes=16 * M, depth=2, copy_threads=4, devices=devices,
+                          on_file=lambda t, s, a: got.append((t, s, a))) as g:
+        for i, (path, _, P, err) in enumerate(cases):
+            g.set_read_fault(P, err)
+            g.submit_file(str(path), i)
+            g.flush()
+        g.set_read_fault(None)
+        g.submit_file(str(p_rand), len(cases))
+        g.flush()
+    assert [t for t, _, _ in got] == list(range(len(cases) + 1))
+    for (tag, status, arr), (_, d, P, err) in zip(got, cases + [(p_rand, data, data.size, 0)]):
+        if P >= d.size:                                    # the fault lies past the end: a complete read
+            want_status, e = 0, O.chunk_production_window(d)
+        elif err:
+            want_status, e = -err, O.chunk_production_read_error(d, P)
+        else:
+            want_status, e = 0, O.chunk_production_window(d[:P])
+        assert status == want_status, (tag, status, want_status)
+        e = e.astype(np.uint64)
+        starts = np.concatenate([[0], e[:-1]]).astype(np.uint64)[:e.size]
+        assert np.array_equal(arr["offset"], starts), tag
+        assert np.array_equal(arr["len"].astype(np.uint64), e - starts), tag
+        hs = O.blake3_batch(d, starts, e - starts, nthreads=8) if e.size else np.zeros((0, 32), np.uint8)
+        assert np.array_equal(arr["hash"], hs), tag
