@@ -90,6 +90,7 @@ struct syncr_cdc {
     uint32_t n_elig = 0, seg_cap = 0;
     uint32_t split_segc = SPLIT_SEGC, split_blocks = SPLIT_BLOCKS;   // (development library: SYNCR_CDC_SPLIT_*)
     DevBuf segs, seg_cuts;
+    DevBuf dbg;                         // development library: resolve timeline (SYNCR_CDC_TRACE=1)
     // split only when walks can be long: the last launch fetched held >= 64 Ki
     // candidates at >= 1 per 16 KiB (random data: ~1 per MiB, so never;
     // periodic or low-entropy data: thousands per MiB).  Off until a fetch has
@@ -231,6 +232,7 @@ Tables make_tables(syncr_cdc *h) {
     t.znext = reinterpret_cast<uint4 *>(zblock(h, h->zpar ^ 1u));
     t.znext_vec = (uint32_t)(zstride(h) / 16);
     t.hzero = nullptr;
+    t.dbg = h->dbg.p ? h->dbg.as<uint64_t>() : nullptr;
     // SplitSeg records outlive a launch: a record is ready for this launch only
     // when its ready word holds this launch's id (records are zeroed when allocated)
     static std::atomic<uint32_t> epochs{0};
@@ -402,6 +404,9 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
         std::lock_guard<std::mutex> g(so.mu);        // held: the owner cannot close its event meanwhile
         if (so.owner && so.owner != h) CHECK_HIP(hipStreamWaitEvent(s, so.ev, 0));
     }
+#ifdef SYNCR_CDC_DEV
+    if (t.dbg) CHECK_HIP(hipMemsetAsync(t.dbg, 0, DBG_WORDS * sizeof(uint64_t), s));
+#endif
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[0], s));
     CHECK_HIP(launch_scan(h->geom, h->scan_grid, d_bytes, kp, t, s));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[1], s));
@@ -506,6 +511,9 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
         h->kp.resolve_nosplit = strcmp(rs, "nosplit") == 0;
     }
     if (const char *a = getenv("SYNCR_CDC_SERIAL")) h->serial_scans = atoi(a) != 0;
+    if (const char *a = getenv("SYNCR_CDC_RESOLVE_PF")) h->kp.resolve_pf = (uint32_t)atoi(a);      // A/B only
+    if (const char *a = getenv("SYNCR_CDC_TRACE"))                                              // timeline
+        if (atoi(a)) CHECK_HIP(h->dbg.ensure(DBG_WORDS * sizeof(uint64_t)));
     if (const char *a = getenv("SYNCR_CDC_SPLIT_SEGC")) h->split_segc = std::max(256, atoi(a));        // A/B only
     if (const char *a = getenv("SYNCR_CDC_SPLIT_BLOCKS")) h->split_blocks = std::max(1, atoi(a));     // A/B only
     if (const char *a = getenv("SYNCR_B3_ABLATE")) h->b3_ablate = (uint32_t)atoi(a) % 3;   // timing-only
@@ -1195,3 +1203,14 @@ extern "C" int32_t syncr_cdc_format_chunks(const syncr_chunk_info *c, uint64_t n
     if (len_out) *len_out = s.n;
     return s.n > s.cap ? SYNCR_CDC_ERANGE : SYNCR_CDC_OK;
 }
+
+#ifdef SYNCR_CDC_DEV
+// Development library only: the last launch's resolve timeline (SYNCR_CDC_TRACE=1).
+extern "C" int32_t syncr_cdc_dev_trace(syncr_cdc *h, uint64_t *out, uint32_t n) {
+    if (!h || !out || !h->dbg.p) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
+    CHECK_HIP(hipStreamSynchronize(h->last_stream ? h->last_stream : h->stream));
+    CHECK_HIP(hipMemcpy(out, h->dbg.p, std::min<uint32_t>(n, DBG_WORDS) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return SYNCR_CDC_OK;
+}
+#endif

@@ -84,7 +84,10 @@ struct KParams {
     uint32_t resolve_nosplit;  // 1: no split walks of long files (SYNCR_CDC_FLAG_RESOLVE_NOSPLIT)
     uint64_t split_patience;   // wall-clock ticks a split worker waits for file walkers (0: none,
                                //   SYNCR_CDC_FLAG_SPLIT_NOWAIT)
+    uint32_t resolve_pf;       // development library only (SYNCR_CDC_RESOLVE_PF): candidate windows
+                               //   the resolve walk loads ahead (0: RESOLVE_PF)
 };
+constexpr int RESOLVE_PF = 2;  // product: candidate windows the resolve walk loads ahead
 
 // ---- split walks of long files (wave resolve) -------------
 // A file whose walk would be long (>= 2 SPLIT_SEGC candidates) is cut into
@@ -113,13 +116,24 @@ struct SplitSeg {            // 64 bytes
     uint32_t k;              // boundary number within the file (>= 1); 0: unusable record
     uint32_t s0, R0;         // walk state at the segment start
     uint32_t first, nseg;    // record of the file's boundary 1; the file's segment count
-    uint32_t n;              // cuts the segment walk produced
-    uint32_t link;           // record of the boundary the walk linked at, or SPLIT_END
-    uint32_t status;         // 0 pending, 3 being walked, 1 done, 2 aborted (release)
+    uint64_t res;            // the walk's result in one word (seg_res): cuts n, link, status --
+                             //   one atomic load gives a file walker all it needs of a record
     uint32_t verdict;        // 1: adopted by the file's walker
     uint32_t ready;          // == Tables::epoch: initialised in this launch (release)
-    uint32_t pad;
+    uint32_t pad[2];
 };
+enum { SEG_PENDING = 0, SEG_DONE = 1, SEG_ABORTED = 2, SEG_WALKING = 3 };
+// res = n << 32 | link (30 bits; SPLIT_END / SPLIT_ABORT keep their low 30) << 2 | status
+__host__ __device__ constexpr uint64_t seg_res(uint32_t status, uint32_t link, uint32_t n) {
+    return ((uint64_t)n << 32) | ((uint64_t)(link & 0x3fffffffu) << 2) | (uint64_t)status;
+}
+__host__ __device__ constexpr uint32_t seg_res_status(uint64_t r) { return (uint32_t)r & 3u; }
+__host__ __device__ constexpr uint32_t seg_res_n(uint64_t r) { return (uint32_t)(r >> 32); }
+__host__ __device__ constexpr uint32_t seg_res_link(uint64_t r) {
+    return ((uint32_t)(r >> 2) & 0x3fffffffu) >= 0x3ffffffeu ? ((uint32_t)(r >> 2) | 0xc0000000u)
+                                                             : ((uint32_t)(r >> 2) & 0x3fffffffu);
+}
+static_assert(sizeof(SplitSeg) == 64, "SplitSeg is one 64-byte record");
 
 struct DevCut {        // == syncr_cut
     uint64_t offset;
@@ -181,7 +195,15 @@ struct Tables {
     uint4 *znext;                  // [znext_vec] the next launch's block (nullptr: none)
     uint32_t znext_vec;
     uint64_t *hzero;               // [B3C_WORDS] hash counters of this launch (hashed launches), or nullptr
+    uint64_t *dbg;                 // development library only (SYNCR_CDC_TRACE=1): [DBG_WORDS] resolve
+                                   //   timeline (wall_clock64 stamps, DBG_*), else nullptr
 };
+// dev timeline slots: resolve entry (min over waves), end (max); the largest
+// split file's walker: entry, after split setup, adoption blocks (start, end),
+// walk end; split workers: record q < DBG_NREC walk start / end; copy kernel
+enum { DBG_RES_START = 0, DBG_RES_END = 1, DBG_W_ENTRY = 2, DBG_W_SETUP = 3, DBG_W_END = 4, DBG_W_NBLK = 5,
+       DBG_W_BLK = 8, DBG_MAXBLK = 120, DBG_COPY_START = 248, DBG_COPY_END = 249, DBG_REC = 256,
+       DBG_NREC = 1024, DBG_WORDS = DBG_REC + 2 * DBG_NREC };
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------
 // A lane TASK is B3_LANE_LEAVES consecutive 1 KiB leaves of one chunk.  A chunk

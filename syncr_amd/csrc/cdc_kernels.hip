@@ -1625,6 +1625,19 @@ struct Patience {
     __device__ __forceinline__ bool spent() const { return deadline == 0ull || wall_clock64() > deadline; }
 };
 
+// development timeline (Tables::dbg, SYNCR_CDC_TRACE=1): lane 0 stamps wall_clock64
+#ifdef SYNCR_CDC_DEV
+#define DBG_STAMP(T, slot) do { if ((T).dbg && lane == 0) (T).dbg[(slot)] = wall_clock64(); } while (0)
+#define DBG_MIN(T, slot) do { if ((T).dbg && lane == 0) atomicMax((unsigned long long *)&(T).dbg[(slot)], \
+                                  ~(unsigned long long)wall_clock64()); } while (0)     /* stored inverted */
+#define DBG_MAX(T, slot) do { if ((T).dbg && lane == 0) atomicMax((unsigned long long *)&(T).dbg[(slot)], \
+                                  (unsigned long long)wall_clock64()); } while (0)
+#else
+#define DBG_STAMP(T, slot) do { } while (0)
+#define DBG_MIN(T, slot) do { } while (0)
+#define DBG_MAX(T, slot) do { } while (0)
+#endif
+
 __device__ __forceinline__ unsigned long long *split_pub(const Tables &T) {
     return reinterpret_cast<unsigned long long *>(&T.split[SPL_PUB64]);
 }
@@ -1669,9 +1682,7 @@ __device__ __forceinline__ void split_setup(const KParams &P, const Tables &T, u
                         g.R0 = (uint32_t)min(F, s0 + MAX);
                         g.first = base;
                         g.nseg = (uint32_t)ns;
-                        g.n = 0;
-                        g.link = 0;
-                        g.status = 0;
+                        g.res = seg_res(SEG_PENDING, 0u, 0u);
                         g.verdict = 0;
                     }
                 }
@@ -1705,7 +1716,7 @@ __device__ __forceinline__ void split_setup(const KParams &P, const Tables &T, u
 // walk of segment record `spec`, from that segment's start state into scratch,
 // until it lands on a later boundary with that boundary's start state (link),
 // reaches the file end, or passes two boundaries without landing (abort).
-template <typename Off>
+template <typename Off, int PF>
 __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, const KParams &P,
                                              const Tables &T, uint32_t i, uint64_t F, uint64_t g0, int lane,
                                              bool elig, uint32_t spec) {
@@ -1721,9 +1732,13 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
     // split state: the file's remaining boundaries are records [brec, bend);
     // sb = the next one's start (OMAX: none)
     uint32_t brec = 0, bend = 0;
+    const bool dbgw = elig && T.order[0] == i;              // (development timeline: the largest file)
+    (void)dbgw;
+    if (dbgw) DBG_STAMP(T, DBG_W_ENTRY);
     if (elig) {
         uint32_t first, nseg;
         split_setup(P, T, i, F, g0, ncand, lane, first, nseg);
+        if (dbgw) DBG_STAMP(T, DBG_W_SETUP);
         if (nseg) {
             brec = first;
             bend = first + nseg - 1;
@@ -1751,10 +1766,8 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
         const uint64_t k = b + (uint64_t)lane;
         return T.cand[k < ncand ? k : 0];
     };
-    // PF windows ahead: a slide then waits only for a load issued PF-1 windows
-    // earlier (a chained walk cuts a 64-candidate window in ~1 us, an HBM
-    // round trip is ~2 us)
-    constexpr int PF = 2;         // 4 measured no faster on dense1 (the slide is not load-bound)
+    // PF windows ahead (template parameter, RESOLVE_PF in the product): a slide
+    // then waits only for a load issued PF-1 windows earlier
     uint64_t pf[PF];
 #pragma unroll
     for (int k = 0; k < PF; ++k) pf[k] = fetch(wb + 64ull * k);
@@ -1859,65 +1872,94 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                         stop = true;
                         break;
                     }
-                    // A segment a worker is walking right now (status 3) ends soon:
-                    // wait for it rather than walk it again.  The worker is resident
-                    // and its walk has no waits, so this ends; it is bounded anyway.
-                    {
-                        const Patience pat(P.split_patience);
-                        while (seg_ld(T.segs[brec].status) == 3u && !pat.spent()) __builtin_amdgcn_s_sleep(2);
-                    }
-                    // Adopt a chain of done segment walks at once: lane k reads record
-                    // brec + k, and the chain brec -> link -> link ... is followed on
-                    // lane indices (one memory round trip per 64 records, not per hop).
-                    const uint32_t rq = brec + (uint32_t)lane;
-                    const bool in = rq < bend;
-                    const uint32_t st = in ? __hip_atomic_load(&T.segs[rq].status, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT) : 0u;
-                    // (atomic results are divergent to the compiler: readlane keeps the
-                    // walk state in scalar registers)
-                    if ((uint32_t)__builtin_amdgcn_readlane((int)st, 0) == 1u) {
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // the walks' results
-                        const bool done = st == 1u;
-                        const uint32_t nn = done ? __hip_atomic_load(&T.segs[rq].n, __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_AGENT) : 0u;
-                        const uint32_t lkv = done ? __hip_atomic_load(&T.segs[rq].link, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                    // Adopt the chain of done segment walks that starts here, 64
+                    // records per memory round trip: lane k reads record brec + k's
+                    // result word (cuts, link, status in one atomic load, so no
+                    // acquire is needed: the cuts themselves are read only by the
+                    // copy launch), and the chain brec -> link -> ... is followed on
+                    // lane indices; a chain that leaves the block continues with the
+                    // next block at once, without walking.  A segment a worker is
+                    // walking right now ends soon: wait for it (bounded) rather than
+                    // walk it again.
+                    bool moved = false;
+#ifdef SYNCR_CDC_DEV
+                    uint32_t nblk = 0;
+                    if (dbgw && T.dbg) nblk = (uint32_t)T.dbg[DBG_W_NBLK];
+#endif
+                    for (;;) {
+#ifdef SYNCR_CDC_DEV
+                        if (dbgw && nblk < DBG_MAXBLK / 2) DBG_STAMP(T, DBG_W_BLK + 2 * nblk);
+#endif
+                        const uint32_t rq = brec + (uint32_t)lane;
+                        uint64_t rs = rq < bend ? __hip_atomic_load(&T.segs[rq].res, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                        uint32_t st0 = (uint32_t)__builtin_amdgcn_readlane((int)seg_res_status(rs), 0);
+                        if (st0 == SEG_WALKING) {
+                            const Patience pat(P.split_patience);
+                            while (st0 == SEG_WALKING && !pat.spent()) {
+                                __builtin_amdgcn_s_sleep(2);
+                                rs = rq < bend ? __hip_atomic_load(&T.segs[rq].res, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                                st0 = (uint32_t)__builtin_amdgcn_readlane((int)seg_res_status(rs), 0);
+                            }
+                        }
+                        if (st0 != SEG_DONE) break;
+                        // (atomic results are divergent to the compiler: readlane keeps the
+                        // walk state in scalar registers)
+                        const uint32_t stv = seg_res_status(rs), nn = seg_res_n(rs), lkv = seg_res_link(rs);
                         unsigned long long adopted = 0;
                         uint32_t cur = 0, last = 0;
                         for (;;) {                                 // chain order = increasing lanes
-                            if ((uint32_t)__builtin_amdgcn_readlane((int)st, (int)cur) != 1u) break;
+                            if ((uint32_t)__builtin_amdgcn_readlane((int)stv, (int)cur) != SEG_DONE) {
+                                last = brec + cur;                 // not done: the walk goes on here
+                                break;
+                            }
                             const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)lkv, (int)cur);
-                            if (lk != SPLIT_END && (lk <= brec + cur || lk >= bend)) break;   // (never)
+                            if (lk != SPLIT_END && (lk <= brec + cur || lk >= bend)) {   // (never)
+                                last = brec + cur;
+                                break;
+                            }
                             adopted |= 1ull << cur;
                             last = lk;
                             if (lk == SPLIT_END || lk - brec >= 64u) break;
                             cur = lk - brec;
                         }
-                        if (adopted) {
-                            const uint32_t pend = (uint32_t)cnt & 63u;   // gathered cuts before the adopted ones
-                            if (pend > bstart) flush(pend);
-                            const bool mine = (adopted >> lane) & 1ull;
-                            const uint32_t incl = wave_incl_scan(mine ? nn : 0u, lane);
-                            if (mine) {
-                                T.segs[rq].out_off = (uint64_t)cnt + (incl - nn);
-                                T.segs[rq].verdict = 1u;
-                            }
-                            cnt += (Off)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                            if (lane == 0) atomicAdd(&T.split[SPL_ADOPTED], (uint32_t)__builtin_popcountll(adopted));
-                            bstart = (uint32_t)cnt & 63u;          // slots below: the copy kernel's
-                            if (last == SPLIT_END) {
-                                stop = true;
-                                break;
-                            }
-                            brec = last;                           // continue where the chain linked
-                            load_bnd();
-                            wb = seg_ld(T.segs[brec].cidx);
-#pragma unroll
-                            for (int k = 0; k < PF; ++k) pf[k] = fetch(wb + 64ull * k);
-                            load_window();
-                            start_at_lane0(sb, (Off)seg_ld(T.segs[brec].R0));
-                            continue;
+                        if (!adopted) break;
+                        const uint32_t pend = (uint32_t)cnt & 63u;   // gathered cuts before the adopted ones
+                        if (pend > bstart) flush(pend);
+                        const bool mine = (adopted >> lane) & 1ull;
+                        const uint32_t incl = wave_incl_scan(mine ? nn : 0u, lane);
+                        if (mine) {
+                            T.segs[rq].out_off = (uint64_t)cnt + (incl - nn);
+                            T.segs[rq].verdict = 1u;
                         }
+                        cnt += (Off)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                        if (lane == 0) atomicAdd(&T.split[SPL_ADOPTED], (uint32_t)__builtin_popcountll(adopted));
+                        bstart = (uint32_t)cnt & 63u;              // slots below: the copy kernel's
+                        moved = true;
+                        brec = last;
+#ifdef SYNCR_CDC_DEV
+                        if (dbgw && nblk < DBG_MAXBLK / 2) {
+                            DBG_STAMP(T, DBG_W_BLK + 2 * nblk + 1);
+                            ++nblk;
+                            if (lane == 0) T.dbg[DBG_W_NBLK] = nblk;
+                        }
+#endif
+                        if (last == SPLIT_END) break;
+                    }
+                    if (moved) {
+                        if (brec == SPLIT_END) {
+                            stop = true;
+                            break;
+                        }
+                        // at boundary brec with its start state: walk on from there
+                        load_bnd();
+                        wb = seg_ld(T.segs[brec].cidx);
+#pragma unroll
+                        for (int k = 0; k < PF; ++k) pf[k] = fetch(wb + 64ull * k);
+                        load_window();
+                        start_at_lane0(sb, (Off)seg_ld(T.segs[brec].R0));
+                        continue;
                     }
                 }
                 ++brec;                                            // passed without adopting
@@ -1929,6 +1971,75 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                 load_bnd();
             }
             if (stop) break;
+        }
+        if constexpr (sizeof(Off) == 4) {
+            // Chained windows (periodic / low-entropy data), whole windows at a
+            // time.  With the reference's buffer full (R = min(F, s + MAX)) and
+            // the last cut made at a candidate whose head fix-up is known to be
+            // empty (head 1, fix 0), the next cut is the next candidate c if
+            // c >= s + 63 (file_operations.rs:754-755 with the fix-up), and
+            // then c < R holds whenever c - (s - 1) <= MAX; if that gap is also
+            // <= CAP the buffer is full again after the cut (:776:
+            // R' = min(F, R + min(MAX - (R - s'), CAP)) = min(F, s' + MAX)).  So
+            // lane l of the window continues the chain iff its predecessor
+            // (lane l-1, or the last cut for the first lane) has a known empty
+            // fix-up and l's candidate lies 64 .. min(MAX, CAP) bytes past it:
+            // one ballot finds the run, its cuts are stored one per lane, and a
+            // used-up window slides to the next (loaded PF windows ahead).  Cuts
+            // stop at the first landing at or past the next split boundary.
+            if (head == 1 && fix == 0 && jlast >= 0 && !P.resolve_noburst &&
+                (uint64_t)R == min<uint64_t>((uint64_t)Fo, (uint64_t)s + (uint64_t)MAX)) {
+                const Off gapmax = CAP < MAX ? CAP : MAX;
+                for (;;) {
+                    if (jlast == 63) {                               // window used up: slide
+                        if (wb + 64 >= ncand) break;
+                        wb += 64;
+#pragma unroll
+                        for (int k = 0; k + 1 < PF; ++k) pf[k] = pf[k + 1];
+                        pf[PF - 1] = fetch(wb + 64ull * (PF - 1));
+                        load_window();
+                        jlast = -1;
+                    }
+                    const Off up = (Off)__shfl_up((int)wr, 1);
+                    const uint32_t kup = (uint32_t)__shfl_up((int)wk, 1);
+                    const bool first = lane == jlast + 1;
+                    const Off pw = first ? (Off)(s - 1) : up;      // the cut before this lane's
+                    const bool plink = first || (kup & 0x1ffu) == 0x100u;
+                    const bool ok = lane > jlast && plink && wr != OMAX && wr >= (Off)(pw + 64) &&
+                                    (Off)(wr - pw) <= gapmax;
+                    const unsigned long long run = __ballot(ok) >> (jlast + 1);   // jlast + 1 <= 63
+                    const uint32_t n0 = ~run ? (uint32_t)__builtin_ctzll(~run) : (uint32_t)(63 - jlast);
+                    if (!n0) break;
+                    uint32_t lastl = (uint32_t)jlast + n0;
+                    const unsigned long long past =
+                        __ballot(lane > jlast && (uint32_t)lane <= lastl && (Off)(wr + 1) >= sb);
+                    if (past) lastl = (uint32_t)__builtin_ctzll(past);
+                    const uint32_t n = lastl - (uint32_t)jlast;
+                    const uint32_t pend = (uint32_t)cnt & 63u;      // gathered cuts before these
+                    if (pend > bstart) flush(pend);
+                    if (lane > jlast && (uint32_t)lane <= lastl) {
+                        const uint64_t idx = (uint64_t)cnt + (uint64_t)(lane - jlast - 1);
+                        if (idx < cap) {
+                            DevCut d;
+                            d.offset = (uint64_t)pw + 1;
+                            d.len = (uint32_t)(wr - pw);
+                            d.file = i;
+                            out[idx] = d;
+                        }
+                    }
+                    cnt += (Off)n;
+                    bstart = (uint32_t)cnt & 63u;
+                    s = rl(wr, lastl) + 1;
+                    R = (Off)min<uint64_t>((uint64_t)Fo, (uint64_t)s + (uint64_t)MAX);
+                    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)wk, (int)lastl);
+                    head = (k & 0x100u) ? 1 : 2;
+                    fix = k & 0xffu;
+                    jlast = (int)lastl;
+                    if (lastl < 63u || s >= R || s >= sb || head != 1 || fix != 0) break;
+                }
+                if (s >= R) break;
+                if (s >= sb) continue;                              // the boundary first
+            }
         }
         if constexpr (sizeof(Off) == 4) {
             // Burst of chained hops: while every cut lands on a window candidate
@@ -2179,20 +2290,19 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
         R += rd;
     }
     if (cnt & 63u) flush((uint32_t)(cnt & 63u));
-    if (is_spec) {                                           // results, then the status (release)
-        SplitSeg &g = T.segs[spec];
+    if (is_spec) {
+        // the result in one word: a file walker needs nothing else of the record
+        // (the scratch cuts are read only by the copy launch), so no release fence
+        const uint32_t st = (link == SPLIT_ABORT || (uint64_t)cnt > cap) ? SEG_ABORTED : SEG_DONE;
         if (lane == 0) {
-            g.n = (uint32_t)min<uint64_t>((uint64_t)cnt, 0xffffffffull);
-            g.link = link;
-        }
-        const uint32_t st = (link == SPLIT_ABORT || (uint64_t)cnt > cap) ? 2u : 1u;
-        __threadfence();
-        if (lane == 0) {
-            __hip_atomic_store(&g.status, st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            if (st == 1u) atomicAdd(&T.split[SPL_WALKED], 1u);
+            __hip_atomic_store(&T.segs[spec].res,
+                               seg_res(st, link, (uint32_t)min<uint64_t>((uint64_t)cnt, 0xffffffffull)),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (st == SEG_DONE) atomicAdd(&T.split[SPL_WALKED], 1u);
         }
         return;
     }
+    if (dbgw) DBG_STAMP(T, DBG_W_END);
     if (lane == 0) {
         T.counts[i] = (uint64_t)cnt;
         if ((uint64_t)cnt > cap) atomicOr(&T.ctr[CTR_FLAGS], FLAG_CUT_OVERFLOW);
@@ -2256,14 +2366,19 @@ __device__ __forceinline__ uint32_t split_next(const KParams &P, const Tables &T
     return q;
 }
 
+template <int PF>
 __device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P, const Tables &T, int lane) {
     for (;;) {
         const uint32_t q = split_next(P, T, lane);
         if (q == SPLIT_END) break;
         if (seg_ld(T.segs[q].k) == 0u) continue;
         const uint32_t i = seg_ld(T.segs[q].file);
-        if (lane == 0) __hip_atomic_store(&T.segs[q].status, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        resolve_walk<uint32_t>(data, P, T, i, T.flen[i], T.foff[i], lane, false, q);
+        if (lane == 0)
+            __hip_atomic_store(&T.segs[q].res, seg_res(SEG_WALKING, 0u, 0u), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (q < DBG_NREC) DBG_STAMP(T, DBG_REC + 2 * q);
+        resolve_walk<uint32_t, PF>(data, P, T, i, T.flen[i], T.foff[i], lane, false, q);
+        if (q < DBG_NREC) DBG_STAMP(T, DBG_REC + 2 * q + 1);
     }
 }
 
@@ -2274,29 +2389,34 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
     const uint32_t wid = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
     const uint32_t nsplit = (uint32_t)(*split_pub(T) >> 32);
     if (nsplit == 0u) return;                                 // nothing split: nothing to copy
+    DBG_MIN(T, DBG_COPY_START);
     const uint32_t nrec = min(T.split[SPL_RESERVED], T.seg_cap);
     for (uint32_t q = wid; q < nrec; q += nw) {
         const SplitSeg &g = T.segs[q];
         if (g.k == 0u || g.verdict != 1u || g.ready != T.epoch) continue;
         const uint32_t i = g.file;
-        const uint64_t cap = T.cut_cap[i], o = g.out_off, n = g.n;
+        const uint64_t cap = T.cut_cap[i], o = g.out_off, n = seg_res_n(g.res);
         const DevCut *src = T.seg_cuts + (uint64_t)q * T.seg_scap;
         DevCut *dst = T.cuts + T.cut_base[i];
         for (uint64_t t = (uint64_t)lane; t < n && o + t < cap; t += 64) dst[o + t] = src[t];
     }
+    DBG_MAX(T, DBG_COPY_END);
 }
 
 // One wave per file; files below 4 GiB walk in 32-bit offsets.  Blocks past
 // the file walkers' (launched only when a file is eligible) are split workers.
 // (Their walk is a separate inlined copy: sharing one with the file walkers
 // made the file walk spill scalar registers.)
+template <int PF>
 __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__restrict__ data,
                                                                KParams P, Tables T) {
     const int lane = threadIdx.x & 63;
+    DBG_MIN(T, DBG_RES_START);
     zero_next(T);
     const uint32_t nmain = (T.nfiles + 3u) / 4u;
     if (blockIdx.x >= nmain) {
-        split_worker(data, P, T, lane);
+        split_worker<PF>(data, P, T, lane);
+        DBG_MAX(T, DBG_RES_END);
         return;
     }
     const uint32_t kf = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -2305,11 +2425,12 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
     const uint64_t F = T.flen[i], g0 = T.foff[i];
     const bool elig = kf < T.n_elig;
     if (F <= 0xFFFFFF00ull) {
-        resolve_walk<uint32_t>(data, P, T, i, F, g0, lane, elig, SPLIT_END);
+        resolve_walk<uint32_t, PF>(data, P, T, i, F, g0, lane, elig, SPLIT_END);
     } else {
         if (elig && lane == 0) atomicAdd(split_pub(T), 1ull);            // counted, never split
-        resolve_walk<uint64_t>(data, P, T, i, F, g0, lane, false, SPLIT_END);
+        resolve_walk<uint64_t, PF>(data, P, T, i, F, g0, lane, false, SPLIT_END);
     }
+    DBG_MAX(T, DBG_RES_END);
 }
 
 // ---------------------------------------------------------------------------
@@ -2635,8 +2756,18 @@ hipError_t launch_resolve(const uint8_t *d, const KParams &p, const Tables &t, h
         hipLaunchKernelGGL(cdc_resolve_kernel, dim3((t.nfiles + 63) / 64), dim3(64), 0, s, d, p, t);
     else {
         const bool split = resolve_splits(p, t);
-        hipLaunchKernelGGL(cdc_resolve_wave_kernel, dim3((t.nfiles + 3) / 4 + (split ? t.split_blocks : 0u)),
-                           dim3(256), 0, s, d, p, t);
+        const dim3 grid((t.nfiles + 3) / 4 + (split ? t.split_blocks : 0u));
+#ifdef SYNCR_CDC_DEV
+        if (p.resolve_pf && p.resolve_pf != RESOLVE_PF) {           // (development A/B: SYNCR_CDC_RESOLVE_PF)
+            switch (p.resolve_pf) {
+                case 2: hipLaunchKernelGGL(cdc_resolve_wave_kernel<2>, grid, dim3(256), 0, s, d, p, t); break;
+                case 4: hipLaunchKernelGGL(cdc_resolve_wave_kernel<4>, grid, dim3(256), 0, s, d, p, t); break;
+                case 8: hipLaunchKernelGGL(cdc_resolve_wave_kernel<8>, grid, dim3(256), 0, s, d, p, t); break;
+                default: return hipErrorInvalidValue;
+            }
+        } else
+#endif
+        hipLaunchKernelGGL(cdc_resolve_wave_kernel<RESOLVE_PF>, grid, dim3(256), 0, s, d, p, t);
         if (split) hipLaunchKernelGGL(cdc_split_copy_kernel, dim3(1024), dim3(256), 0, s, t);
     }
     return hipGetLastError();

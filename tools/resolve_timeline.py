@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Timeline of one resolve launch (development library, SYNCR_CDC_TRACE=1).
+
+The resolve kernel stamps wall_clock64 (Tables::dbg, cdc_internal.h DBG_*):
+kernel start/end, the largest split file's walker (entry, after its split
+setup, each block of 64 adopted records, walk end), every split worker's walk
+(start, end) of records < DBG_NREC, and the copy launch.  Printed in us from
+the resolve kernel's first wave.
+
+    python tools/resolve_timeline.py --workload dense1 [VAR=VAL ...]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+import syncr_amd  # noqa: E402
+
+syncr_amd.use_dev_library()
+
+DBG_RES_START, DBG_RES_END, DBG_W_ENTRY, DBG_W_SETUP, DBG_W_END, DBG_W_NBLK = 0, 1, 2, 3, 4, 5
+DBG_W_BLK, DBG_COPY_START, DBG_COPY_END, DBG_REC, DBG_NREC = 8, 248, 249, 256, 1024
+WORDS = DBG_REC + 2 * DBG_NREC
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("env", nargs="*")
+    ap.add_argument("--workload", default="dense1")
+    ap.add_argument("--launches", type=int, default=4)
+    args = ap.parse_args()
+    for kv in args.env:
+        k, v = kv.split("=", 1)
+        os.environ[k] = v
+    os.environ["SYNCR_CDC_TRACE"] = "1"
+    sizes, idx, _ = bench.workload(args.workload, 1)
+    offs = np.zeros_like(sizes)
+    offs[1:] = np.cumsum(sizes)[:-1]
+    span = int(sizes.sum())
+    c = syncr_amd.Chunker()
+    buf = syncr_amd.DeviceBuffer(c, span)
+    buf.gen_corpus(offs, sizes, indices=idx)
+    if args.workload == "dense":
+        from benchlib import legs
+        legs.fill_dense(buf, offs, sizes, idx)
+    elif args.workload == "dense1":
+        buf.upload(np.resize(bench.periodic_pattern(), span))
+    c.plan(offs, sizes, span)
+    L = syncr_amd.library()
+    L.syncr_cdc_dev_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+    L.syncr_cdc_dev_trace.restype = ctypes.c_int32
+    c.launch(buf.ptr)
+    c.fetch()                               # the fetch turns the split hint on
+    for n in range(args.launches):
+        c.launch(buf.ptr)
+        d = np.zeros(WORDS, np.uint64)
+        assert L.syncr_cdc_dev_trace(c.handle, d.ctypes.data, WORDS) == 0
+        t0 = int(~d[DBG_RES_START] & np.uint64(2**64 - 1)) if d[DBG_RES_START] else 0
+        us = lambda v: (int(v) - t0) / 100.0 if v else None          # 100 MHz wall clock
+        print(f"launch {n}: split {c.split_stats()}")
+        print(f"  resolve end {us(d[DBG_RES_END])} us; walker entry {us(d[DBG_W_ENTRY])} setup {us(d[DBG_W_SETUP])} "
+              f"end {us(d[DBG_W_END])}")
+        nb = int(d[DBG_W_NBLK])
+        blk = [(us(d[DBG_W_BLK + 2 * b]), us(d[DBG_W_BLK + 2 * b + 1])) for b in range(min(nb, 60))]
+        print(f"  walker adoption blocks ({nb}): " + ", ".join(f"{a:.1f}-{b:.1f}" for a, b in blk[:24]))
+        rec = d[DBG_REC:].reshape(-1, 2)
+        have = rec[:, 0] > 0
+        if have.any():
+            st = np.array([us(v) for v in rec[have, 0]])
+            en = np.array([us(v) for v in rec[have, 1] if v] or [0.0])
+            dur = en[:st.size] - st[:en.size]
+            print(f"  worker walks ({have.sum()}): start min {st.min():.1f} med {np.median(st):.1f} "
+                  f"max {st.max():.1f}; end max {en.max():.1f}; duration med {np.median(dur):.1f} max {dur.max():.1f}")
+        cs = d[DBG_COPY_START]
+        print(f"  copy start {us(~cs & np.uint64(2**64 - 1)) if cs else None} end {us(d[DBG_COPY_END])}")
+    buf.free()
+
+
+if __name__ == "__main__":
+    main()
