@@ -125,6 +125,9 @@ namespace {
 
 int32_t hip_err(hipError_t e) {
     if (e == hipSuccess) return SYNCR_CDC_OK;
+#ifdef SYNCR_CDC_DEV
+    fprintf(stderr, "syncr_cdc (dev): HIP error %d: %s\n", (int)e, hipGetErrorString(e));
+#endif
     if (e == hipErrorOutOfMemory) return SYNCR_CDC_ENOMEM;
     if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return SYNCR_CDC_ENODEV;
     return SYNCR_CDC_EIO;

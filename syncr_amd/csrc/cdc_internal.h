@@ -87,7 +87,7 @@ struct KParams {
     uint32_t resolve_pf;       // development library only (SYNCR_CDC_RESOLVE_PF): candidate windows
                                //   the resolve walk loads ahead (0: RESOLVE_PF)
 };
-constexpr int RESOLVE_PF = 2;  // product: candidate windows the resolve walk loads ahead
+constexpr int RESOLVE_PF = 8;  // product: candidate windows in the resolve walk's LDS ring (PF-1 ahead)
 
 // ---- split walks of long files (wave resolve) -------------
 // A file whose walk would be long (>= 2 SPLIT_SEGC candidates) is cut into

@@ -1719,7 +1719,7 @@ __device__ __forceinline__ void split_setup(const KParams &P, const Tables &T, u
 template <typename Off, int PF>
 __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, const KParams &P,
                                              const Tables &T, uint32_t i, uint64_t F, uint64_t g0, int lane,
-                                             bool elig, uint32_t spec) {
+                                             bool elig, uint32_t spec, const uint64_t *ring) {
     constexpr Off OMAX = (Off)~(Off)0;
     const bool is_spec = spec != SPLIT_END;
     DevCut *out = is_spec ? T.seg_cuts + (uint64_t)spec * T.seg_scap : T.cuts + T.cut_base[i];
@@ -1756,24 +1756,44 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                           : (F ? T.super_off[(uint32_t)((g0 / T.tile) >> 6)] : 0);   // the file's 64-tile group
     Off wr = OMAX;
     uint32_t wk = 0, nx = 64;
-    // the window after the current one is loaded ahead (a slide then costs no
-    // dependent HBM round trip on this serial walk)
-    // unconditional load of the raw word (clamped index; entries past ncand are
-    // masked when the window is consumed): an exec-predicated load, or using
-    // the value at issue, makes the waitcnt pass drain vmcnt(0) right there,
-    // which defeats the prefetch
-    auto fetch = [&](uint64_t b) -> uint64_t {
-        const uint64_t k = b + (uint64_t)lane;
-        return T.cand[k < ncand ? k : 0];
-    };
-    // PF windows ahead (template parameter, RESOLVE_PF in the product): a slide
-    // then waits only for a load issued PF-1 windows earlier
-    uint64_t pf[PF];
+    // Candidate windows stream through the wave's LDS ring of PF slots (ring:
+    // PF x 64 words) by LDS-DMA, two dword DMAs per 64-candidate window, PF-1
+    // windows ahead of the one in use.  Completion is tracked by hand: a window
+    // has 2 (PF-1) DMAs issued after it, so s_waitcnt vmcnt(2 (PF-1)) retires it
+    // (vector-memory operations retire in issue order; other loads and stores in
+    // between only make that wait stricter).  No register ever holds an
+    // in-flight window: a register ring rotated at each slide made hipcc wait
+    // vmcnt(0) at the rotation, one HBM round trip per 64 candidates.  Indices
+    // are clamped (entries past ncand are masked when the window is consumed).
+    const uint32_t ring0 = (uint32_t)__builtin_amdgcn_readfirstlane(lds_addr(ring));
+    uint32_t rh = 0;                                  // slot of the current window
+    auto issue = [&](uint64_t b, uint32_t slot) {
 #pragma unroll
-    for (int k = 0; k < PF; ++k) pf[k] = fetch(wb + 64ull * k);
-    uint64_t &pf_cur = pf[0];
+        for (int h = 0; h < 2; ++h) {
+            const uint64_t k = b + (uint64_t)((64 * h + lane) >> 1);   // dword 64h + lane of the window
+            const uint8_t *src = (const uint8_t *)(T.cand + (k < ncand ? k : 0)) + ((lane & 1) << 2);
+            dma4(src, (uint32_t)__builtin_amdgcn_readfirstlane(ring0 + slot * 512u + (uint32_t)h * 256u));
+        }
+    };
+    auto prime = [&]() {                              // the windows from wb on, slots 0 .. PF-1
+        wait_vmcnt<0>();                              // (no older DMA may still land in a slot)
+#pragma unroll
+        for (int k = 0; k < PF; ++k) issue(wb + 64ull * k, (uint32_t)k);
+        rh = 0;
+    };
+    auto cur = [&]() -> uint64_t {                    // this lane's word of the current window
+        wait_vmcnt<2 * (PF - 1)>();
+        return ring[rh * 64u + (uint32_t)lane];
+    };
+    auto slide = [&]() {                              // the current window has been consumed
+        issue(wb + 64ull * PF, rh);
+        wb += 64;
+        rh = (rh + 1u) & (uint32_t)(PF - 1);
+    };
+    prime();
     auto load_window = [&]() {
-        const uint64_t c = wb + (uint64_t)lane < ncand ? pf_cur : NONE;
+        const uint64_t raw = cur();
+        const uint64_t c = wb + (uint64_t)lane < ncand ? raw : NONE;
         wr = OMAX;
         wk = 0;
         if (c != NONE) {
@@ -1907,9 +1927,15 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                         // (atomic results are divergent to the compiler: readlane keeps the
                         // walk state in scalar registers)
                         const uint32_t stv = seg_res_status(rs), nn = seg_res_n(rs), lkv = seg_res_link(rs);
-                        unsigned long long adopted = 0;
-                        uint32_t cur = 0, last = 0;
-                        for (;;) {                                 // chain order = increasing lanes
+                        // the usual chain links each record to the next one (periodic
+                        // data): that prefix is one ballot; the rest (a jump, the chain's
+                        // end) is followed lane by lane
+                        const unsigned long long nextm =
+                            __ballot(stv == SEG_DONE && lkv == rq + 1u && rq + 1u < bend);
+                        const uint32_t run = ~nextm ? (uint32_t)__builtin_ctzll(~nextm) : 64u;
+                        unsigned long long adopted = run >= 64u ? ~0ull : ((1ull << run) - 1ull);
+                        uint32_t cur = run, last = brec + run;
+                        for (; cur < 64u;) {                       // chain order = increasing lanes
                             if ((uint32_t)__builtin_amdgcn_readlane((int)stv, (int)cur) != SEG_DONE) {
                                 last = brec + cur;                 // not done: the walk goes on here
                                 break;
@@ -1942,7 +1968,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                         if (dbgw && nblk < DBG_MAXBLK / 2) {
                             DBG_STAMP(T, DBG_W_BLK + 2 * nblk + 1);
                             ++nblk;
-                            if (lane == 0) T.dbg[DBG_W_NBLK] = nblk;
+                            if (lane == 0 && T.dbg) T.dbg[DBG_W_NBLK] = nblk;
                         }
 #endif
                         if (last == SPLIT_END) break;
@@ -1955,8 +1981,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                         // at boundary brec with its start state: walk on from there
                         load_bnd();
                         wb = seg_ld(T.segs[brec].cidx);
-#pragma unroll
-                        for (int k = 0; k < PF; ++k) pf[k] = fetch(wb + 64ull * k);
+                        prime();
                         load_window();
                         start_at_lane0(sb, (Off)seg_ld(T.segs[brec].R0));
                         continue;
@@ -1993,10 +2018,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                 for (;;) {
                     if (jlast == 63) {                               // window used up: slide
                         if (wb + 64 >= ncand) break;
-                        wb += 64;
-#pragma unroll
-                        for (int k = 0; k + 1 < PF; ++k) pf[k] = pf[k + 1];
-                        pf[PF - 1] = fetch(wb + 64ull * (PF - 1));
+                        slide();
                         load_window();
                         jlast = -1;
                     }
@@ -2262,10 +2284,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                         break;
                     }
                     if (wb + 64 >= ncand) break;             // whole window below `from`: slide
-                    wb += 64;
-#pragma unroll
-                    for (int k = 0; k + 1 < PF; ++k) pf[k] = pf[k + 1];
-                    pf[PF - 1] = fetch(wb + 64ull * (PF - 1));
+                    slide();
                     load_window();
                 }
             }
@@ -2290,6 +2309,10 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
         R += rd;
     }
     if (cnt & 63u) flush((uint32_t)(cnt & 63u));
+    // Retire the ring's outstanding LDS-DMAs before the walk ends: a wave must
+    // not end (and its workgroup's LDS be handed to another) with DMA writes
+    // into it still in flight.
+    wait_vmcnt<0>();
     if (is_spec) {
         // the result in one word: a file walker needs nothing else of the record
         // (the scratch cuts are read only by the copy launch), so no release fence
@@ -2367,7 +2390,8 @@ __device__ __forceinline__ uint32_t split_next(const KParams &P, const Tables &T
 }
 
 template <int PF>
-__device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P, const Tables &T, int lane) {
+__device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P, const Tables &T, int lane,
+                             const uint64_t *ring) {
     for (;;) {
         const uint32_t q = split_next(P, T, lane);
         if (q == SPLIT_END) break;
@@ -2377,7 +2401,7 @@ __device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P,
             __hip_atomic_store(&T.segs[q].res, seg_res(SEG_WALKING, 0u, 0u), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         if (q < DBG_NREC) DBG_STAMP(T, DBG_REC + 2 * q);
-        resolve_walk<uint32_t, PF>(data, P, T, i, T.flen[i], T.foff[i], lane, false, q);
+        resolve_walk<uint32_t, PF>(data, P, T, i, T.flen[i], T.foff[i], lane, false, q, ring);
         if (q < DBG_NREC) DBG_STAMP(T, DBG_REC + 2 * q + 1);
     }
 }
@@ -2389,18 +2413,32 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
     const uint32_t wid = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
     const uint32_t nsplit = (uint32_t)(*split_pub(T) >> 32);
     if (nsplit == 0u) return;                                 // nothing split: nothing to copy
-    DBG_MIN(T, DBG_COPY_START);
+    if (blockIdx.x == 0 && threadIdx.x < 64) DBG_STAMP(T, DBG_COPY_START);
     const uint32_t nrec = min(T.split[SPL_RESERVED], T.seg_cap);
-    for (uint32_t q = wid; q < nrec; q += nw) {
+    // COPY_PARTS waves per record (a record holds up to 3 x 4096 cuts: one wave
+    // per record left most of the grid idle and each wave latency-bound), four
+    // 16-byte loads in flight per lane
+    constexpr uint32_t COPY_PARTS = 8;
+    for (uint32_t w = wid; w < nrec * COPY_PARTS; w += nw) {
+        const uint32_t q = w / COPY_PARTS, part = w % COPY_PARTS;
         const SplitSeg &g = T.segs[q];
         if (g.k == 0u || g.verdict != 1u || g.ready != T.epoch) continue;
         const uint32_t i = g.file;
         const uint64_t cap = T.cut_cap[i], o = g.out_off, n = seg_res_n(g.res);
+        const uint64_t per = ((n + COPY_PARTS - 1) / COPY_PARTS + 255) & ~255ull;
+        const uint64_t a = (uint64_t)part * per, e = min(min(n, a + per), cap > o ? cap - o : 0ull);
         const DevCut *src = T.seg_cuts + (uint64_t)q * T.seg_scap;
-        DevCut *dst = T.cuts + T.cut_base[i];
-        for (uint64_t t = (uint64_t)lane; t < n && o + t < cap; t += 64) dst[o + t] = src[t];
+        DevCut *dst = T.cuts + T.cut_base[i] + o;
+        for (uint64_t t = a + (uint64_t)lane; t < e; t += 256) {
+            DevCut v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (t + 64u * u < e) v[u] = src[t + 64u * u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (t + 64u * u < e) dst[t + 64u * u] = v[u];
+        }
     }
-    DBG_MAX(T, DBG_COPY_END);
 }
 
 // One wave per file; files below 4 GiB walk in 32-bit offsets.  Blocks past
@@ -2411,12 +2449,13 @@ template <int PF>
 __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__restrict__ data,
                                                                KParams P, Tables T) {
     const int lane = threadIdx.x & 63;
-    DBG_MIN(T, DBG_RES_START);
+    __shared__ uint64_t rings[4 * PF * 64];                     // each wave's candidate-window ring
+    const uint64_t *ring = rings + (threadIdx.x >> 6) * (PF * 64);
+    if (blockIdx.x == 0 && threadIdx.x < 64) DBG_STAMP(T, DBG_RES_START);   // (one wave: no contention)
     zero_next(T);
     const uint32_t nmain = (T.nfiles + 3u) / 4u;
     if (blockIdx.x >= nmain) {
-        split_worker<PF>(data, P, T, lane);
-        DBG_MAX(T, DBG_RES_END);
+        split_worker<PF>(data, P, T, lane, ring);
         return;
     }
     const uint32_t kf = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -2425,12 +2464,11 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
     const uint64_t F = T.flen[i], g0 = T.foff[i];
     const bool elig = kf < T.n_elig;
     if (F <= 0xFFFFFF00ull) {
-        resolve_walk<uint32_t, PF>(data, P, T, i, F, g0, lane, elig, SPLIT_END);
+        resolve_walk<uint32_t, PF>(data, P, T, i, F, g0, lane, elig, SPLIT_END, ring);
     } else {
         if (elig && lane == 0) atomicAdd(split_pub(T), 1ull);            // counted, never split
-        resolve_walk<uint64_t, PF>(data, P, T, i, F, g0, lane, false, SPLIT_END);
+        resolve_walk<uint64_t, PF>(data, P, T, i, F, g0, lane, false, SPLIT_END, ring);
     }
-    DBG_MAX(T, DBG_RES_END);
 }
 
 // ---------------------------------------------------------------------------

@@ -43,6 +43,21 @@ __device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds) {
             : "memory");
 }
 
+// 4 B per lane from a per-lane address into LDS (M0 = wave-uniform LDS base;
+// lane l lands at +4*l).  Completion is tracked by hand (wait_vmcnt).
+__device__ __forceinline__ void dma4(const void *gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds)
+        : "memory");
+}
+
 // 16 B per lane from a wave-uniform SGPR base + per-lane VGPR offset into LDS.
 // NT: non-temporal policy (the bytes are read exactly once).
 template <bool NT>

@@ -2,9 +2,9 @@
 """Timeline of one resolve launch (development library, SYNCR_CDC_TRACE=1).
 
 The resolve kernel stamps wall_clock64 (Tables::dbg, cdc_internal.h DBG_*):
-kernel start/end, the largest split file's walker (entry, after its split
+the resolve kernel's block 0 start, the largest split file's walker (entry, after its split
 setup, each block of 64 adopted records, walk end), every split worker's walk
-(start, end) of records < DBG_NREC, and the copy launch.  Printed in us from
+(start, end) of records < DBG_NREC, and the copy launch's start.  Printed in us from
 the resolve kernel's first wave.
 
     python tools/resolve_timeline.py --workload dense1 [VAR=VAL ...]
@@ -61,10 +61,10 @@ def main():
         c.launch(buf.ptr)
         d = np.zeros(WORDS, np.uint64)
         assert L.syncr_cdc_dev_trace(c.handle, d.ctypes.data, WORDS) == 0
-        t0 = int(~d[DBG_RES_START] & np.uint64(2**64 - 1)) if d[DBG_RES_START] else 0
+        t0 = int(d[DBG_RES_START])
         us = lambda v: (int(v) - t0) / 100.0 if v else None          # 100 MHz wall clock
         print(f"launch {n}: split {c.split_stats()}")
-        print(f"  resolve end {us(d[DBG_RES_END])} us; walker entry {us(d[DBG_W_ENTRY])} setup {us(d[DBG_W_SETUP])} "
+        print(f"  walker entry {us(d[DBG_W_ENTRY])} setup {us(d[DBG_W_SETUP])} "
               f"end {us(d[DBG_W_END])}")
         nb = int(d[DBG_W_NBLK])
         blk = [(us(d[DBG_W_BLK + 2 * b]), us(d[DBG_W_BLK + 2 * b + 1])) for b in range(min(nb, 60))]
@@ -77,8 +77,7 @@ def main():
             dur = en[:st.size] - st[:en.size]
             print(f"  worker walks ({have.sum()}): start min {st.min():.1f} med {np.median(st):.1f} "
                   f"max {st.max():.1f}; end max {en.max():.1f}; duration med {np.median(dur):.1f} max {dur.max():.1f}")
-        cs = d[DBG_COPY_START]
-        print(f"  copy start {us(~cs & np.uint64(2**64 - 1)) if cs else None} end {us(d[DBG_COPY_END])}")
+        print(f"  copy start {us(d[DBG_COPY_START])}")
     buf.free()
 
 
