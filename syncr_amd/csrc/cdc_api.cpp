@@ -515,6 +515,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     }
     if (const char *a = getenv("SYNCR_CDC_SERIAL")) h->serial_scans = atoi(a) != 0;
     if (const char *a = getenv("SYNCR_CDC_RESOLVE_PF")) h->kp.resolve_pf = (uint32_t)atoi(a);      // A/B only
+    if (const char *a = getenv("SYNCR_CDC_SPLIT_FIRST")) h->kp.split_first = (uint32_t)atoi(a) != 0; // A/B only
     if (const char *a = getenv("SYNCR_CDC_TRACE"))                                              // timeline
         if (atoi(a)) CHECK_HIP(h->dbg.ensure(DBG_WORDS * sizeof(uint64_t)));
     if (const char *a = getenv("SYNCR_CDC_SPLIT_SEGC")) h->split_segc = std::max(256, atoi(a));        // A/B only

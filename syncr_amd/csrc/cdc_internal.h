@@ -84,6 +84,7 @@ struct KParams {
     uint32_t resolve_nosplit;  // 1: no split walks of long files (SYNCR_CDC_FLAG_RESOLVE_NOSPLIT)
     uint64_t split_patience;   // wall-clock ticks a split worker waits for file walkers (0: none,
                                //   SYNCR_CDC_FLAG_SPLIT_NOWAIT)
+    uint32_t split_first;      // 1: split workers take the resolve grid's first blocks (dev A/B: SYNCR_CDC_SPLIT_FIRST)
     uint32_t resolve_pf;       // development library only (SYNCR_CDC_RESOLVE_PF): candidate windows
                                //   the resolve walk loads ahead (0: RESOLVE_PF)
 };

@@ -39,6 +39,16 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
+// Whole-wave shifts by one lane as DPP moves (wave_shr:1 / wave_shl:1), not
+// ds_bpermute round trips through the LDS unit: lane l gets lane l-1's value
+// (up1; lane 0 gets 0) or lane l+1's (down1; lane 63 gets 0).  All lanes active.
+__device__ __forceinline__ uint32_t up1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t down1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
+
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
     return ((uint64_t)hi << 32) | lo;
@@ -1808,7 +1818,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
             // dense windows (periodic data: a candidate every 64 bytes): every
             // lane's answer is the next lane, found with one shuffle instead of
             // six dependent ones.  (nx of a lane past the file is never read.)
-            const Off up = (Off)__shfl_down((int)wr, 1);
+            const Off up = (Off)down1((uint32_t)wr);
             if (__ballot(lane == 63 || up >= key) == ~0ull) {
                 nx = (uint32_t)lane + 1u;
                 return;
@@ -2022,8 +2032,8 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                         load_window();
                         jlast = -1;
                     }
-                    const Off up = (Off)__shfl_up((int)wr, 1);
-                    const uint32_t kup = (uint32_t)__shfl_up((int)wk, 1);
+                    const Off up = (Off)up1((uint32_t)wr);
+                    const uint32_t kup = up1(wk);
                     const bool first = lane == jlast + 1;
                     const Off pw = first ? (Off)(s - 1) : up;      // the cut before this lane's
                     const bool plink = first || (kup & 0x1ffu) == 0x100u;
@@ -2132,7 +2142,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     // (periodic data): a_m falls with m, so the prefix minimum is a_m
                     // itself and R_{m-1} follows from the previous lane's candidate --
                     // one shuffle instead of the 6-step scan and two more shuffles
-                    wup = (Off)__shfl_up((int)wr, 1);
+                    wup = (Off)up1((uint32_t)wr);
                     const bool mono = chain_contig &&
                                       __ballot(on && below && (int64_t)wr - (int64_t)wup >= capv) == 0ull;
                     if (mono) {
@@ -2370,6 +2380,9 @@ __device__ __forceinline__ uint32_t split_next(const KParams &P, const Tables &T
     uint32_t q = 0;
     if (lane == 0) q = atomicAdd(&T.split[SPL_HEAD], 1u);
     q = (uint32_t)__builtin_amdgcn_readfirstlane(q);
+    // exponential backoff between polls: a thousand waves polling one word at
+    // full rate queue up in front of the file walkers' own loads
+    uint32_t nap = 1;
     for (;;) {
         if (q < min(ld_relaxed(&T.split[SPL_RESERVED]), T.seg_cap)) break;
         if ((uint32_t)ld64_relaxed(split_pub(T)) >= T.n_elig) {
@@ -2379,7 +2392,8 @@ __device__ __forceinline__ uint32_t split_next(const KParams &P, const Tables &T
             return SPLIT_END;
         }
         if (pat.spent()) return give_up(T, lane);
-        __builtin_amdgcn_s_sleep(16);
+        for (uint32_t k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(8);
+        nap = nap < 16u ? 2u * nap : 16u;
     }
     while (ld_relaxed(&T.segs[q].ready) != T.epoch) {                 // not a stale record
         if (pat.spent()) return give_up(T, lane);                     // record q stays pending
@@ -2453,16 +2467,23 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
     const uint64_t *ring = rings + (threadIdx.x >> 6) * (PF * 64);
     if (blockIdx.x == 0 && threadIdx.x < 64) DBG_STAMP(T, DBG_RES_START);   // (one wave: no contention)
     zero_next(T);
-    const uint32_t nmain = (T.nfiles + 3u) / 4u;
-    if (blockIdx.x >= nmain) {
+    if (blockIdx.x == 0 && threadIdx.x < 64) DBG_STAMP(T, 6);
+    const uint32_t nmain = (T.nfiles + 3u) / 4u, nwork = gridDim.x - nmain;
+    // split workers take the FIRST blocks when P.split_first: a grid larger than
+    // the resident set dispatched them last, after the file walkers of the big
+    // files had published their segments and waited (their waits are bounded,
+    // and the file walkers never wait on a worker that has not started)
+    const uint32_t b = P.split_first ? (blockIdx.x >= nwork ? blockIdx.x - nwork : nmain + blockIdx.x) : blockIdx.x;
+    if (b >= nmain) {
         split_worker<PF>(data, P, T, lane, ring);
         return;
     }
-    const uint32_t kf = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const uint32_t kf = __builtin_amdgcn_readfirstlane(b * 4 + (threadIdx.x >> 6));
     if (kf >= T.nfiles) return;
     const uint32_t i = T.order[kf];
     const uint64_t F = T.flen[i], g0 = T.foff[i];
     const bool elig = kf < T.n_elig;
+    if (kf == 0) DBG_STAMP(T, 7);
     if (F <= 0xFFFFFF00ull) {
         resolve_walk<uint32_t, PF>(data, P, T, i, F, g0, lane, elig, SPLIT_END, ring);
     } else {
@@ -2801,6 +2822,8 @@ hipError_t launch_resolve(const uint8_t *d, const KParams &p, const Tables &t, h
                 case 2: hipLaunchKernelGGL(cdc_resolve_wave_kernel<2>, grid, dim3(256), 0, s, d, p, t); break;
                 case 4: hipLaunchKernelGGL(cdc_resolve_wave_kernel<4>, grid, dim3(256), 0, s, d, p, t); break;
                 case 8: hipLaunchKernelGGL(cdc_resolve_wave_kernel<8>, grid, dim3(256), 0, s, d, p, t); break;
+                case 16: hipLaunchKernelGGL(cdc_resolve_wave_kernel<16>, grid, dim3(256), 0, s, d, p, t); break;
+                case 32: hipLaunchKernelGGL(cdc_resolve_wave_kernel<32>, grid, dim3(256), 0, s, d, p, t); break;
                 default: return hipErrorInvalidValue;
             }
         } else

@@ -64,6 +64,7 @@ def main():
         t0 = int(d[DBG_RES_START])
         us = lambda v: (int(v) - t0) / 100.0 if v else None          # 100 MHz wall clock
         print(f"launch {n}: split {c.split_stats()}")
+        print(f"  block 0: after zero_next {us(d[6])}, file loads {us(d[7])}")
         print(f"  walker entry {us(d[DBG_W_ENTRY])} setup {us(d[DBG_W_SETUP])} "
               f"end {us(d[DBG_W_END])}")
         nb = int(d[DBG_W_NBLK])
