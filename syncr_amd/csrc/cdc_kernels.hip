@@ -2374,12 +2374,20 @@ __device__ __forceinline__ uint32_t give_up(const Tables &T, int lane) {
 
 // The next segment record to walk, or SPLIT_END once every eligible walker has
 // published and the queue is empty (or the worker ran out of patience).
-__device__ __forceinline__ uint32_t split_next(const KParams &P, const Tables &T, int lane) {
+// A worker's first record is its own index (no atomic: a thousand workers
+// incrementing one counter at once held up every file walker's first loads by
+// ~10-20 us); later ones come from the queue counter, past the first nwork.
+__device__ __forceinline__ uint32_t split_next(const KParams &P, const Tables &T, int lane, uint32_t first,
+                                               uint32_t nwork) {
     const Patience pat(P.split_patience);
     if (P.split_patience == 0ull) return give_up(T, lane);           // SYNCR_CDC_FLAG_SPLIT_NOWAIT
-    uint32_t q = 0;
-    if (lane == 0) q = atomicAdd(&T.split[SPL_HEAD], 1u);
-    q = (uint32_t)__builtin_amdgcn_readfirstlane(q);
+    uint32_t q = first;
+    if (q == SPLIT_END) {
+        if (lane == 0) q = nwork + atomicAdd(&T.split[SPL_HEAD], 1u);
+        q = (uint32_t)__builtin_amdgcn_readfirstlane(q);
+    } else {
+        __builtin_amdgcn_s_sleep(32);                                // the walkers publish after ~5-10 us
+    }
     // exponential backoff between polls: a thousand waves polling one word at
     // full rate queue up in front of the file walkers' own loads
     uint32_t nap = 1;
@@ -2405,9 +2413,9 @@ __device__ __forceinline__ uint32_t split_next(const KParams &P, const Tables &T
 
 template <int PF>
 __device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P, const Tables &T, int lane,
-                             const uint64_t *ring) {
-    for (;;) {
-        const uint32_t q = split_next(P, T, lane);
+                             const uint64_t *ring, uint32_t widx, uint32_t nwork) {
+    for (uint32_t first = widx;; first = SPLIT_END) {
+        const uint32_t q = split_next(P, T, lane, first, nwork);
         if (q == SPLIT_END) break;
         if (seg_ld(T.segs[q].k) == 0u) continue;
         const uint32_t i = seg_ld(T.segs[q].file);
@@ -2475,7 +2483,8 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
     // and the file walkers never wait on a worker that has not started)
     const uint32_t b = P.split_first ? (blockIdx.x >= nwork ? blockIdx.x - nwork : nmain + blockIdx.x) : blockIdx.x;
     if (b >= nmain) {
-        split_worker<PF>(data, P, T, lane, ring);
+        const uint32_t widx = __builtin_amdgcn_readfirstlane((b - nmain) * 4u + (threadIdx.x >> 6));
+        split_worker<PF>(data, P, T, lane, ring, widx, 4u * nwork);
         return;
     }
     const uint32_t kf = __builtin_amdgcn_readfirstlane(b * 4 + (threadIdx.x >> 6));

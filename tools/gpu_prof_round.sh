@@ -8,6 +8,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 TAG=${1:-r03}
 bash tools/prof.sh ${TAG} || exit 21
-bash tools/prof.sh ${TAG}dense --workload dense --no-legs || exit 22
+bash tools/prof.sh ${TAG}dense --workload dense || exit 22
 bash tools/gpu_rehearsal.sh ${TAG}_rehearsal || exit 23
 echo all-done
