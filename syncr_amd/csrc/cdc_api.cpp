@@ -75,7 +75,7 @@ struct syncr_cdc {
     std::vector<uint64_t> h_foff, h_flen, h_cut_base;
     std::vector<uint32_t> h_cut_cap;
     DevBuf fstart, foff, flen, order, cut_base, cut_cap, tile_meta, slots, zeroed,
-        dense_list, dense_cnt, dense_bits, super_off, cand, cuts, counts;
+        dense_list, dense_cnt, dense_bits, super_off, cand, linkw, cuts, counts;
     // BLAKE3 of every chunk (launch_hashed)
     bool hash_on = false;
     uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 3, b3_nosplit = 0, b3_nouni = 0;     // dev A/B knobs; coop 3 = the product (LD_PAIR + quad merges)
@@ -216,6 +216,7 @@ Tables make_tables(syncr_cdc *h) {
     t.dense_cap = h->dense_cap;
     t.dense_bits = h->dense_bits.as<uint32_t>();
     t.cand = h->cand.as<uint64_t>();
+    t.linkw = h->linkw.as<uint64_t>();
     t.cand_cap = h->cand_cap;
     t.cuts = h->cuts.as<DevCut>();
     t.counts = h->counts.as<uint64_t>();
@@ -346,6 +347,7 @@ int32_t ensure_split(syncr_cdc *h) {
 int32_t ensure_cand(syncr_cdc *h, uint64_t cap) {
     h->cand_cap = cap;
     CHECK_HIP(h->cand.ensure(std::max<uint64_t>(cap, 1) * 8));
+    CHECK_HIP(h->linkw.ensure((cap / 64 + 4) * 8));
     return ensure_split(h);
 }
 
@@ -516,6 +518,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_CDC_SERIAL")) h->serial_scans = atoi(a) != 0;
     if (const char *a = getenv("SYNCR_CDC_RESOLVE_PF")) h->kp.resolve_pf = (uint32_t)atoi(a);      // A/B only
     if (const char *a = getenv("SYNCR_CDC_SPLIT_FIRST")) h->kp.split_first = (uint32_t)atoi(a) != 0; // A/B only
+    if (const char *a = getenv("SYNCR_CDC_NOSKIP")) h->kp.no_skip = atoi(a) != 0;                    // A/B only
     if (const char *a = getenv("SYNCR_CDC_TRACE"))                                              // timeline
         if (atoi(a)) CHECK_HIP(h->dbg.ensure(DBG_WORDS * sizeof(uint64_t)));
     if (const char *a = getenv("SYNCR_CDC_SPLIT_SEGC")) h->split_segc = std::max(256, atoi(a));        // A/B only

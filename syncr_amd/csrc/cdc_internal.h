@@ -67,6 +67,12 @@ enum { FLAG_DENSE_OVERFLOW = 1u, FLAG_CUT_OVERFLOW = 2u, FLAG_CAND_OVERFLOW = 4u
 // bit 63 = fix-up known
 constexpr uint64_t CAND_POS_MASK = (1ull << 48) - 1;
 constexpr uint64_t CAND_KNOWN = 1ull << 63;
+// chain link (cdc_fix_kernel): a cut at this candidate, with the reference's
+// buffer full, implies a cut at the next candidate -- its head fix-up is empty
+// and the next candidate lies 64 .. min(MAX, read_cap) bytes past it (one file
+// or not: the resolve bounds runs by its file).  Tables::linkw holds the same
+// bits 64 candidates per word.
+constexpr uint64_t CAND_LINK = 1ull << 62;
 
 struct KParams {
     uint32_t bits;     // chunk_bits
@@ -85,6 +91,7 @@ struct KParams {
     uint64_t split_patience;   // wall-clock ticks a split worker waits for file walkers (0: none,
                                //   SYNCR_CDC_FLAG_SPLIT_NOWAIT)
     uint32_t split_first;      // 1: split workers take the resolve grid's first blocks (dev A/B: SYNCR_CDC_SPLIT_FIRST)
+    uint32_t no_skip;          // 1: no run skips in the resolve walk (dev A/B: SYNCR_CDC_NOSKIP)
     uint32_t resolve_pf;       // development library only (SYNCR_CDC_RESOLVE_PF): candidate windows
                                //   the resolve walk loads ahead (0: RESOLVE_PF)
 };
@@ -168,6 +175,7 @@ struct Tables {
     uint32_t dense_cap;
     uint32_t *dense_bits;          // [dense_cap * tile/32] candidate bitmaps
     uint64_t *cand;                // [cand_cap] compacted sorted candidates
+    uint64_t *linkw;               // [cand_cap / 64 + 4] CAND_LINK bits, 64 candidates per word (cdc_fix_kernel)
     uint64_t cand_cap;
     DevCut *cuts;                  // [sum cut_cap]
     uint64_t *counts;              // [nfiles]

@@ -1018,6 +1018,17 @@ __device__ __forceinline__ uint32_t fix_first(uint32_t m0, uint32_t m1, uint32_t
     return m ? (uint32_t)__builtin_clzll(m) + 1u : 0u;
 }
 
+// bits x0..x31 to the even bit positions of a 64-bit word
+__device__ __forceinline__ uint64_t spread32(uint32_t x) {
+    uint64_t v = x;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    v = (v | (v << 1)) & 0x5555555555555555ull;
+    return v;
+}
+
 __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict__ data, KParams P,
                                                       Tables T) {
     const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
@@ -1059,12 +1070,30 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
         }
         const uint32_t fA = fix_first(acc[0] & 0xffffu, acc[1] & 0xffffu, acc[2] & 0xffffu, acc[3] & 0xffffu, nA);
         const uint32_t fB = fix_first(acc[0] >> 16, acc[1] >> 16, acc[2] >> 16, acc[3] >> 16, nB);
+        // chain links (CAND_LINK): empty fix-up, next candidate 64 .. gapmax past
+        const uint64_t gapmax = P.read_cap && P.read_cap < P.max_chunk ? P.read_cap : P.max_chunk;
+        bool lA = false, lB = false;
+        if (2 * q + 1 < n) {
+            const uint64_t d = aB - aA;                       // positions 2q+1 and 2q
+            lA = fA == 0u && d >= 64u && d <= gapmax;
+        }
+        if (2 * q + 2 < n) {
+            const uint64_t d = (T.cand[2 * q + 2] & CAND_POS_MASK) - (aB - 1);
+            lB = fB == 0u && d >= 64u && d <= gapmax;
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint64_t i = 2 * q + (uint64_t)h;
             const uint32_t f = h ? fB : fA;
-            if (i < n) T.cand[i] = ((h ? aB : aA) - 1) | ((uint64_t)f << 48) | CAND_KNOWN;
+            if (i < n) T.cand[i] = ((h ? aB : aA) - 1) | ((uint64_t)f << 48) | CAND_KNOWN | ((h ? lB : lA) ? CAND_LINK : 0ull);
             else if (i < items) T.gfix[i - n] = (uint8_t)f;
+        }
+        // the wave's 128 consecutive candidates (lane l: 2l, 2l+1) as two link words
+        const unsigned long long E = __ballot(lA), O = __ballot(lB);
+        const uint64_t q0 = q - (threadIdx.x & 63u);
+        if ((threadIdx.x & 63u) == 0u && 2 * q0 < n && T.linkw) {
+            T.linkw[q0 / 32] = spread32((uint32_t)E) | (spread32((uint32_t)O) << 1);
+            T.linkw[q0 / 32 + 1] = spread32((uint32_t)(E >> 32)) | (spread32((uint32_t)(O >> 32)) << 1);
         }
     }
 }
@@ -1760,7 +1789,11 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
     }
     if constexpr (sizeof(Off) != 4) bend = 0;
     Off sb = OMAX;
-    auto load_bnd = [&]() { sb = brec < bend ? (Off)seg_ld(T.segs[brec].s0) : OMAX; };
+    uint64_t sbi = NONE;                     // the next boundary's candidate index (run skips stop there)
+    auto load_bnd = [&]() {
+        sb = brec < bend ? (Off)seg_ld(T.segs[brec].s0) : OMAX;
+        sbi = brec < bend ? seg_ld(T.segs[brec].cidx) : NONE;
+    };
     load_bnd();
     uint64_t wb = is_spec ? seg_ld(T.segs[spec].cidx)
                           : (F ? T.super_off[(uint32_t)((g0 / T.tile) >> 6)] : 0);   // the file's 64-tile group
@@ -1809,7 +1842,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
         if (c != NONE) {
             const uint64_t p = c & CAND_POS_MASK;
             wr = p < g0 ? (Off)0 : (p - g0 >= F ? OMAX : (Off)(p - g0));
-            wk = (uint32_t)((c >> 48) & 0xffu) | ((c & CAND_KNOWN) ? 0x100u : 0u);
+            wk = (uint32_t)((c >> 48) & 0xffu) | ((c & CAND_KNOWN) ? 0x100u : 0u) | ((c & CAND_LINK) ? 0x200u : 0u);
         }
         // nx: window index of the first candidate >= this lane's + 64, where the
         // search resumes after a cut at it with no head hit (64 = past the window)
@@ -2026,6 +2059,70 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                 (uint64_t)R == min<uint64_t>((uint64_t)Fo, (uint64_t)s + (uint64_t)MAX)) {
                 const Off gapmax = CAP < MAX ? CAP : MAX;
                 for (;;) {
+                    // Run skip: when the chain continues through the rest of this
+                    // window, find where it ends from the link words (4096
+                    // candidates per load) instead of window by window, write the
+                    // run's cuts with independent loads/stores, and re-seat the
+                    // window ring at the run's last cut.  The run stops at the next
+                    // split boundary's candidate (a landing there is decided above)
+                    // and at the file's last candidate.
+                    if (T.linkw && !P.no_skip && ncand && __ballot((uint32_t)lane >= (uint32_t)jlast && !(wk & 0x200u)) == 0ull) {
+                        const uint64_t ci = wb + (uint64_t)jlast;               // the last cut's candidate
+                        uint64_t lim = ncand - 1;
+                        if (sbi < lim) lim = sbi;
+                        const uint64_t w0 = ci >> 6, wi = w0 + (uint64_t)lane;
+                        uint64_t word = wi <= (lim >> 6) ? T.linkw[wi] : 0ull;
+                        if (lane == 0) word |= (1ull << (ci & 63u)) - 1ull;     // below ci: not looked at
+                        const unsigned long long hz = __ballot(~word != 0ull);
+                        uint64_t z = (w0 + 64u) * 64u - 1u;                    // 4096 links, all set
+                        if (hz) {
+                            const uint32_t fl = (uint32_t)__builtin_ctzll(hz);
+                            z = (w0 + fl) * 64u + (uint64_t)__builtin_ctzll(~readlane64(word, fl));
+                        }
+                        if (z > lim) z = lim;
+                        uint64_t cz = z > ci ? T.cand[z] : 0ull;
+                        if (z > ci && (cz & CAND_POS_MASK) >= g0 + F) {         // past the file: its last candidate
+                            z = wave_lower_bound(T.cand, ci + 1, z + 1, g0 + F, lane) - 1;
+                            cz = T.cand[z];
+                        }
+                        if (z > ci) {
+                            const uint32_t pend = (uint32_t)cnt & 63u;      // gathered cuts before the run
+                            if (pend > bstart) flush(pend);
+                            for (uint64_t k0 = ci + 1; k0 <= z; k0 += 256u) {
+                                uint64_t pk[4], pp[4];
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    const uint64_t k = k0 + 64u * u + (uint64_t)lane;
+                                    const uint64_t kk = k <= z ? k : z;
+                                    pk[u] = T.cand[kk] & CAND_POS_MASK;
+                                    pp[u] = T.cand[kk - 1] & CAND_POS_MASK;
+                                }
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    const uint64_t k = k0 + 64u * u + (uint64_t)lane;
+                                    const uint64_t idx = (uint64_t)cnt + (k - ci - 1);
+                                    if (k <= z && idx < cap) {
+                                        DevCut d;
+                                        d.offset = pp[u] + 1 - g0;
+                                        d.len = (uint32_t)(pk[u] - pp[u]);
+                                        d.file = i;
+                                        out[idx] = d;
+                                    }
+                                }
+                            }
+                            cnt += (Off)(z - ci);
+                            bstart = (uint32_t)cnt & 63u;
+                            s = (Off)((cz & CAND_POS_MASK) - g0 + 1);
+                            R = (Off)min<uint64_t>((uint64_t)Fo, (uint64_t)s + (uint64_t)MAX);
+                            head = (cz & CAND_KNOWN) ? 1 : 2;
+                            fix = (uint32_t)(cz >> 48) & 0xffu;
+                            wb = z;                                          // window ring at the last cut
+                            prime();
+                            load_window();
+                            jlast = 0;
+                            if (s >= R || s >= sb || head != 1 || fix != 0) break;
+                        }
+                    }
                     if (jlast == 63) {                               // window used up: slide
                         if (wb + 64 >= ncand) break;
                         slide();
