@@ -89,7 +89,8 @@ struct syncr_cdc {
     // split walks of long files (Tables::segs...): files order[0 .. n_elig) may split
     uint32_t n_elig = 0, seg_cap = 0;
     uint32_t split_segc = SPLIT_SEGC, split_blocks = SPLIT_BLOCKS;   // (development library: SYNCR_CDC_SPLIT_*)
-    DevBuf segs, seg_cuts;
+    DevBuf segs, seg_cuts, runs;
+    uint32_t runs_cap = 0;
     DevBuf dbg;                         // development library: resolve timeline (SYNCR_CDC_TRACE=1)
     // split only when walks can be long: the last launch fetched held >= 64 Ki
     // candidates at >= 1 per 16 KiB (random data: ~1 per MiB, so never;
@@ -232,6 +233,8 @@ Tables make_tables(syncr_cdc *h) {
     t.seg_segc = h->split_segc;
     t.seg_scap = split_scap(h->split_segc);
     t.split_blocks = h->split_blocks;
+    t.runs = h->runs.as<RunJob>();
+    t.runs_cap = (h->n_elig && h->seg_cap) ? h->runs_cap : 0u;     // deferral only when the copy launch runs
     t.split = reinterpret_cast<uint32_t *>(zb + split_ctr_offset(h));
     t.znext = reinterpret_cast<uint4 *>(zblock(h, h->zpar ^ 1u));
     t.znext_vec = (uint32_t)(zstride(h) / 16);
@@ -339,6 +342,9 @@ int32_t ensure_split(syncr_cdc *h) {
         CHECK_HIP(h->segs.ensure(segs * sizeof(SplitSeg)));
         CHECK_HIP(hipMemset(h->segs.p, 0, segs * sizeof(SplitSeg)));     // no ready word from other memory
         CHECK_HIP(h->seg_cuts.ensure(segs * split_scap(h->split_segc) * sizeof(DevCut)));
+        const uint64_t runs = std::min<uint64_t>(h->cand_cap / 64 + 1024, 0xffffffull);
+        CHECK_HIP(h->runs.ensure(runs * sizeof(RunJob)));
+        h->runs_cap = (uint32_t)runs;
         h->seg_cap = (uint32_t)segs;
     }
     return SYNCR_CDC_OK;

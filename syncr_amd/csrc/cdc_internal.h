@@ -116,7 +116,7 @@ constexpr uint32_t SPLIT_ABORT = 0xfffffffeu;           // (segment walk state: 
 // queue head; split walkers done; worker give-ups; segments walked by workers;
 // segments adopted by file walkers
 enum { SPL_PUB64 = 0, SPL_RESERVED = 2, SPL_HEAD = 3, SPL_DONE = 4, SPL_GIVEUP = 5, SPL_WALKED = 6,
-       SPL_ADOPTED = 7, SPL_WORDS = 8 };
+       SPL_ADOPTED = 7, SPL_RUNS = 8, SPL_WORDS = 9 };
 struct SplitSeg {            // 64 bytes
     uint64_t cidx;           // candidate index of the segment's first candidate
     uint64_t out_off;        // adopted: first cut slot within the file's output
@@ -128,7 +128,18 @@ struct SplitSeg {            // 64 bytes
                              //   one atomic load gives a file walker all it needs of a record
     uint32_t verdict;        // 1: adopted by the file's walker
     uint32_t ready;          // == Tables::epoch: initialised in this launch (release)
-    uint32_t pad[2];
+    uint32_t run_pre, run_len;   // the walk's deferred run (RunJob): its cuts sit after run_pre
+                                 //   scratch cuts; run_len 0 = none
+};
+// A run of chained cuts the resolve walk deferred to the copy launch (cuts at
+// candidates a .. a+n-1, each starting after the previous candidate): the walk
+// only counts them.  rec == SPLIT_END: `out` is the absolute output slot of the
+// first; else `out` is the slot within segment walk `rec`'s cuts, placed when a
+// file walker adopts that walk.
+struct RunJob {
+    uint64_t out;
+    uint64_t a;
+    uint32_t n, file, rec, pad;
 };
 enum { SEG_PENDING = 0, SEG_DONE = 1, SEG_ABORTED = 2, SEG_WALKING = 3 };
 // res = n << 32 | link (30 bits; SPLIT_END / SPLIT_ABORT keep their low 30) << 2 | status
@@ -196,6 +207,8 @@ struct Tables {
     uint32_t seg_segc, seg_scap;   // candidates per segment, scratch cuts per segment walk
     uint32_t split_blocks;         // extra resolve blocks (split workers)
     uint32_t *split;               // [SPL_WORDS] counters                    (zeroed per launch)
+    RunJob *runs;                  // [runs_cap] deferred runs (only while split workers run)
+    uint32_t runs_cap;
     uint32_t epoch;                // this launch's id (!= 0, unique in the process): SplitSeg::ready
     // The per-launch counters above (ctr, nonempty, super_cnt, split) live in one
     // of two zeroed blocks, alternating by launch.  The resolve kernel zeroes the
@@ -212,7 +225,7 @@ struct Tables {
 // walk end; split workers: record q < DBG_NREC walk start / end; copy kernel
 enum { DBG_RES_START = 0, DBG_RES_END = 1, DBG_W_ENTRY = 2, DBG_W_SETUP = 3, DBG_W_END = 4, DBG_W_NBLK = 5,
        DBG_W_BLK = 8, DBG_MAXBLK = 120, DBG_COPY_START = 248, DBG_COPY_END = 249, DBG_REC = 256,
-       DBG_NREC = 1024, DBG_WORDS = DBG_REC + 2 * DBG_NREC };
+       DBG_NREC = 1024, DBG_FW = DBG_REC + 2 * DBG_NREC, DBG_NFW = 1024, DBG_WORDS = DBG_FW + DBG_NFW };
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------
 // A lane TASK is B3_LANE_LEAVES consecutive 1 KiB leaves of one chunk.  A chunk

@@ -1723,6 +1723,8 @@ __device__ __forceinline__ void split_setup(const KParams &P, const Tables &T, u
                         g.nseg = (uint32_t)ns;
                         g.res = seg_res(SEG_PENDING, 0u, 0u);
                         g.verdict = 0;
+                        g.run_pre = 0;
+                        g.run_len = 0;
                     }
                 }
                 __threadfence();
@@ -1762,7 +1764,11 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
     constexpr Off OMAX = (Off)~(Off)0;
     const bool is_spec = spec != SPLIT_END;
     DevCut *out = is_spec ? T.seg_cuts + (uint64_t)spec * T.seg_scap : T.cuts + T.cut_base[i];
-    const uint64_t cap = is_spec ? (uint64_t)T.seg_scap : (uint64_t)T.cut_cap[i];
+    uint64_t cap = is_spec ? (uint64_t)T.seg_scap : (uint64_t)T.cut_cap[i];
+    // runs deferred to the copy launch (only while it runs: split workers
+    // launched); a segment walk defers at most one, its scratch skipping it
+    const bool defer = T.runs_cap && !P.resolve_nosplit;
+    uint32_t run_pre = 0, run_len = 0;
     const Off Fo = (Off)F;
     const Off MAX = (Off)min<uint64_t>(P.max_chunk, (uint64_t)OMAX);
     const Off CAP = P.read_cap ? (Off)min<uint64_t>(P.read_cap, (uint64_t)OMAX) : OMAX;
@@ -2088,7 +2094,34 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                         if (z > ci) {
                             const uint32_t pend = (uint32_t)cnt & 63u;      // gathered cuts before the run
                             if (pend > bstart) flush(pend);
-                            for (uint64_t k0 = ci + 1; k0 <= z; k0 += 256u) {
+                            const uint64_t L = z - ci;
+                            bool deferred = false;
+                            if (defer && (is_spec ? run_len == 0u && L < 0xffffffffull
+                                                  : (uint64_t)cnt + L <= cap)) {
+                                uint32_t q = 0;
+                                if (lane == 0) q = atomicAdd(&T.split[SPL_RUNS], 1u);
+                                q = (uint32_t)__builtin_amdgcn_readfirstlane(q);
+                                if (q < T.runs_cap) {
+                                    if (lane == 0) {
+                                        RunJob j;
+                                        j.out = is_spec ? (uint64_t)cnt : T.cut_base[i] + (uint64_t)cnt;
+                                        j.a = ci + 1;
+                                        j.n = (uint32_t)L;
+                                        j.file = i;
+                                        j.rec = is_spec ? spec : SPLIT_END;
+                                        j.pad = 0;
+                                        T.runs[q] = j;
+                                    }
+                                    deferred = true;
+                                    if (is_spec) {                           // scratch skips the run
+                                        run_pre = (uint32_t)cnt;
+                                        run_len = (uint32_t)L;
+                                        out -= L;
+                                        cap += L;
+                                    }
+                                }
+                            }
+                            for (uint64_t k0 = ci + 1; !deferred && k0 <= z; k0 += 256u) {
                                 uint64_t pk[4], pp[4];
 #pragma unroll
                                 for (int u = 0; u < 4; ++u) {
@@ -2425,6 +2458,8 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
         // (the scratch cuts are read only by the copy launch), so no release fence
         const uint32_t st = (link == SPLIT_ABORT || (uint64_t)cnt > cap) ? SEG_ABORTED : SEG_DONE;
         if (lane == 0) {
+            T.segs[spec].run_pre = run_pre;                 // read by the copy launch only
+            T.segs[spec].run_len = run_len;
             __hip_atomic_store(&T.segs[spec].res,
                                seg_res(st, link, (uint32_t)min<uint64_t>((uint64_t)cnt, 0xffffffffull)),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2531,31 +2566,73 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
     const int lane = threadIdx.x & 63;
     const uint32_t wid = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
     const uint32_t nsplit = (uint32_t)(*split_pub(T) >> 32);
-    if (nsplit == 0u) return;                                 // nothing split: nothing to copy
+    const uint32_t nruns = T.runs_cap ? min(T.split[SPL_RUNS], T.runs_cap) : 0u;
+    if (nsplit == 0u && nruns == 0u) return;                  // nothing split or deferred
     if (blockIdx.x == 0 && threadIdx.x < 64) DBG_STAMP(T, DBG_COPY_START);
-    const uint32_t nrec = min(T.split[SPL_RESERVED], T.seg_cap);
-    // COPY_PARTS waves per record (a record holds up to 3 x 4096 cuts: one wave
-    // per record left most of the grid idle and each wave latency-bound), four
-    // 16-byte loads in flight per lane
+    const uint32_t nrec = nsplit ? min(T.split[SPL_RESERVED], T.seg_cap) : 0u;
+    // COPY_PARTS waves per record / run (up to 3 x 4096 cuts: one wave each left
+    // most of the grid idle and each wave latency-bound), four 16-byte loads in
+    // flight per lane
     constexpr uint32_t COPY_PARTS = 8;
+    // 1. scratch cuts of every adopted segment walk (its deferred run, if any,
+    //    leaves a gap of run_len slots after its first run_pre cuts)
     for (uint32_t w = wid; w < nrec * COPY_PARTS; w += nw) {
         const uint32_t q = w / COPY_PARTS, part = w % COPY_PARTS;
         const SplitSeg &g = T.segs[q];
         if (g.k == 0u || g.verdict != 1u || g.ready != T.epoch) continue;
         const uint32_t i = g.file;
-        const uint64_t cap = T.cut_cap[i], o = g.out_off, n = seg_res_n(g.res);
+        const uint64_t cap = T.cut_cap[i], o = g.out_off, rl = g.run_len, rp = g.run_pre;
+        const uint64_t n = seg_res_n(g.res) - rl;                    // scratch cuts
         const uint64_t per = ((n + COPY_PARTS - 1) / COPY_PARTS + 255) & ~255ull;
-        const uint64_t a = (uint64_t)part * per, e = min(min(n, a + per), cap > o ? cap - o : 0ull);
+        const uint64_t a = (uint64_t)part * per, e = min(n, a + per);
         const DevCut *src = T.seg_cuts + (uint64_t)q * T.seg_scap;
-        DevCut *dst = T.cuts + T.cut_base[i] + o;
+        DevCut *dst = T.cuts + T.cut_base[i];
         for (uint64_t t = a + (uint64_t)lane; t < e; t += 256) {
             DevCut v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (t + 64u * u < e) v[u] = src[t + 64u * u];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (t + 64u * u < e) dst[t + 64u * u] = v[u];
+            for (int u = 0; u < 4; ++u) {
+                const uint64_t tt = t + 64u * u, d = o + tt + (tt < rp ? 0u : rl);
+                if (tt < e && d < cap) dst[d] = v[u];
+            }
+        }
+    }
+    // 2. deferred runs: cut k starts right after candidate k-1 (file-relative)
+    for (uint32_t w = wid; w < nruns * COPY_PARTS; w += nw) {
+        const RunJob j = T.runs[w / COPY_PARTS];
+        const uint32_t part = w % COPY_PARTS, i = j.file;
+        uint64_t rel = j.out - T.cut_base[i];                        // slot within the file's output
+        if (j.rec != SPLIT_END) {
+            const SplitSeg &g = T.segs[j.rec];
+            if (g.k == 0u || g.verdict != 1u || g.ready != T.epoch) continue;
+            rel = g.out_off + j.out;
+        }
+        const uint64_t cap = T.cut_cap[i], g0 = T.foff[i];
+        const uint64_t per = (((uint64_t)j.n + COPY_PARTS - 1) / COPY_PARTS + 255) & ~255ull;
+        const uint64_t a = (uint64_t)part * per, e = min((uint64_t)j.n, a + per);
+        DevCut *dst = T.cuts + T.cut_base[i] + rel;
+        const uint64_t lim = cap > rel ? cap - rel : 0ull;
+        for (uint64_t t = a + (uint64_t)lane; t < e; t += 256) {
+            uint64_t pk[4], pp[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint64_t k = j.a + min(t + 64u * u, (uint64_t)j.n - 1);
+                pk[u] = T.cand[k] & CAND_POS_MASK;
+                pp[u] = T.cand[k - 1] & CAND_POS_MASK;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint64_t tt = t + 64u * u;
+                if (tt < e && tt < lim) {
+                    DevCut d;
+                    d.offset = pp[u] + 1 - g0;
+                    d.len = (uint32_t)(pk[u] - pp[u]);
+                    d.file = i;
+                    dst[tt] = d;
+                }
+            }
         }
     }
 }
@@ -2592,6 +2669,7 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
     if (kf == 0) DBG_STAMP(T, 7);
     if (F <= 0xFFFFFF00ull) {
         resolve_walk<uint32_t, PF>(data, P, T, i, F, g0, lane, elig, SPLIT_END, ring);
+        if (kf < DBG_NFW) DBG_STAMP(T, DBG_FW + kf);
     } else {
         if (elig && lane == 0) atomicAdd(split_pub(T), 1ull);            // counted, never split
         resolve_walk<uint64_t, PF>(data, P, T, i, F, g0, lane, false, SPLIT_END, ring);

@@ -26,7 +26,8 @@ syncr_amd.use_dev_library()
 
 DBG_RES_START, DBG_RES_END, DBG_W_ENTRY, DBG_W_SETUP, DBG_W_END, DBG_W_NBLK = 0, 1, 2, 3, 4, 5
 DBG_W_BLK, DBG_COPY_START, DBG_COPY_END, DBG_REC, DBG_NREC = 8, 248, 249, 256, 1024
-WORDS = DBG_REC + 2 * DBG_NREC
+DBG_FW, DBG_NFW = DBG_REC + 2 * DBG_NREC, 1024
+WORDS = DBG_FW + DBG_NFW
 
 
 def main():
@@ -79,6 +80,11 @@ def main():
             print(f"  worker walks ({have.sum()}): start min {st.min():.1f} med {np.median(st):.1f} "
                   f"max {st.max():.1f}; end max {en.max():.1f}; duration med {np.median(dur):.1f} max {dur.max():.1f}")
         print(f"  copy start {us(d[DBG_COPY_START])}")
+        fw = d[DBG_FW:DBG_FW + DBG_NFW]
+        ends = sorted(((us(v), k) for k, v in enumerate(fw) if v), reverse=True)[:6]
+        order = np.argsort(-sizes.astype(np.int64), kind="stable")
+        print("  latest file walkers (end us, order index, size KiB, corpus index): " +
+              ", ".join(f"{e:.1f}/{k}/{int(sizes[order[k]]) >> 10}/{int(idx[order[k]])}" for e, k in ends))
     buf.free()
 
 
