@@ -71,7 +71,7 @@ def main():
         nb = int(d[DBG_W_NBLK])
         blk = [(us(d[DBG_W_BLK + 2 * b]), us(d[DBG_W_BLK + 2 * b + 1])) for b in range(min(nb, 60))]
         print(f"  walker adoption blocks ({nb}): " + ", ".join(f"{a:.1f}-{b:.1f}" for a, b in blk[:24]))
-        rec = d[DBG_REC:].reshape(-1, 2)
+        rec = d[DBG_REC:DBG_FW].reshape(-1, 2)
         have = rec[:, 0] > 0
         if have.any():
             st = np.array([us(v) for v in rec[have, 0]])
