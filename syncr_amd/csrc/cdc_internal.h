@@ -105,7 +105,7 @@ constexpr int RESOLVE_PF = 8;  // product: candidate windows in the resolve walk
 // segment b's start with exactly that R continues identically to segment b's
 // walk (the walk's future is a function of (s, R) only), so the file's walker
 // adopts segment b's cuts and jumps to where that walk linked in turn.
-constexpr uint32_t SPLIT_SEGC = 4096;                   // candidates per segment (default; Tables::seg_segc)
+constexpr uint32_t SPLIT_SEGC = 8192;                   // candidates per segment (default; Tables::seg_segc; 4096 before run skips)
 __host__ __device__ constexpr uint32_t split_scap(uint32_t segc) { return 3 * segc + 64; }   // scratch cuts per walk
 constexpr uint64_t SPLIT_MIN_BYTES = 256ull << 10;       // smaller files never split
 constexpr uint32_t SPLIT_BLOCKS = 256;                  // extra resolve blocks (4 waves each; default)

@@ -555,8 +555,8 @@ def _split_oracle(data, offs, lens, bits, mx, cap):
                                          (20, 16 << 20, 2 << 20), (20, 16 << 20, 0)])
 def test_split_walks(bits, mx, cap):
     """Split walks of long files: files of >= SPLIT_MIN_BYTES
-    (256 KiB) holding >= 2 x SPLIT_SEGC (4096) candidates are walked in
-    segments of 4096 candidates by extra resolve waves and stitched where a
+    (256 KiB) holding >= 2 x SPLIT_SEGC (8192) candidates are walked in
+    segments of 8192 candidates by extra resolve waves and stitched where a
     walk lands on a segment's start with its start state; the handle launches
     the extra waves once a fetch has seen >= 64 Ki candidates at >= 1 per
     16 KiB.  Mixed content makes segment starts that are not cuts, read-limit
