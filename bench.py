@@ -370,9 +370,10 @@ def main(argv=None):
     ap.add_argument("--device-map", default=None,
                     help="rehearsal only: comma-separated device per local rank (e.g. 0,0 runs two ranks on one "
                          "GPU); default: device = LOCAL_RANK")
-    ap.add_argument("--fetch-at", default="first", choices=["first", "end"],
-                    help="where inside the W warm-up steps the results are fetched once (capacity re-runs settle "
-                         "there): after the first step (default) or after the last, right before the timed region")
+    ap.add_argument("--fetch-at", default="after", choices=["first", "end", "after"],
+                    help="where the results are first fetched (capacity re-runs settle there): after the timed "
+                         "region (default: no host gap anywhere between the first warm-up step and the timed "
+                         "steps; re-timed if that fetch had to re-run), after warm-up step 1, or after the last")
     ap.add_argument("--dev-lib", action="store_true",
                     help="tools/ only: run against libsyncr_cdc_dev.so (variants / ablations by env)")
     args = ap.parse_args(argv)
@@ -445,22 +446,42 @@ def main(argv=None):
     # step keeps the host-side gap (D2H + host work) away from the timed
     # region: on MI355X the shader clock dips for ~20 launches whenever the
     # scan load resumes after a gap (profiles/r02_v2_dispatches.json)
-    if args.fetch_at == "first" and args.warmup > 0:
-        run_steps(1, 1)
+    def warm_and_time(fetch_at):
+        if fetch_at == "first" and args.warmup > 0:
+            run_steps(1, 1)
+            ch.fetch(hashed=head_hashed)
+            run_steps(1, args.warmup - 1)
+        elif fetch_at == "after":
+            run_steps(1, args.warmup)
+        else:
+            run_steps(1, args.warmup)
+            ch.fetch(hashed=head_hashed)
+        d.barrier()
+        ch.synchronize()
+        ch.set_timing(True, scan_only=True)       # HIP events around the scan kernel, on its stream
+        t0 = time.perf_counter()
+        run_steps(1, args.steps)                  # the timed region: one batch in flight
+        dt = time.perf_counter() - t0
+        d.barrier()
+        kms, nl = ch.kernel_times()
+        ch.set_timing(False)
+        return dt, kms, nl
+
+    # The host-side fetch (D2H + list building) is a gap of the device's load,
+    # and on MI355X the shader clock dips whenever the scan load resumes after a
+    # gap (§4.2): by default nothing is fetched between the first warm-up step
+    # and the timed steps (profiles/r03_ab_fetch_gap.log: +0.8-1.3 %).  The
+    # first fetch comes after the timed region; if it had to re-run a launch
+    # with grown capacities, the timed launches ran with the smaller ones, so the
+    # region is timed again (now with settled capacities, fetch after step 1).
+    fetch_mode = args.fetch_at
+    dt, kms, nl = warm_and_time(fetch_mode)
+    retimed = False
+    if fetch_mode == "after":
         ch.fetch(hashed=head_hashed)
-        run_steps(1, args.warmup - 1)
-    else:
-        run_steps(1, args.warmup)
-        ch.fetch(hashed=head_hashed)
-    d.barrier()
-    ch.synchronize()
-    ch.set_timing(True, scan_only=True)       # HIP events around the scan kernel, on its stream
-    t0 = time.perf_counter()
-    run_steps(1, args.steps)                  # the timed region: one batch in flight
-    dt = time.perf_counter() - t0
-    d.barrier()
-    kms, nl = ch.kernel_times()
-    ch.set_timing(False)
+        if d.reduce(float(ch.fetch_reruns()), "max") > 0:
+            fetch_mode, retimed = "first", True
+            dt, kms, nl = warm_and_time(fetch_mode)
     # diagnostics outside the timed region: every phase bracketed by events
     ch.set_timing(True)
     run_steps(1, min(args.steps, 5))
@@ -653,8 +674,11 @@ def main(argv=None):
                             "GPU, no collective"),
             "launcher": os.environ.get("SYNCR_BENCH_LAUNCHER", "torchrun/env" if world > 1 else "none"),
             "device_map": args.device_map or "device = LOCAL_RANK",
-            "warmup_fetch": f"results fetched after warm-up step {1 if args.fetch_at == 'first' else args.warmup} "
-                            f"of {args.warmup}",
+            "warmup_fetch": ("results first fetched after the timed region (no host gap from warm-up step 1 "
+                             "through the timed steps); no capacity re-run was needed" if fetch_mode == "after" else
+                             f"results fetched after warm-up step {1 if fetch_mode == 'first' else args.warmup} of "
+                             f"{args.warmup}" + ("; re-timed: the first fetch had to re-run with grown capacities"
+                                                  if retimed else "")),
             "slots_agree_rank0": slots_agree,
             "cuts_rank0": ncuts, "coverage_ok_rank0": covered,
             "candidates_rank0": int(stats["candidates"]), "dense_tiles_rank0": int(stats["dense_tiles"]),

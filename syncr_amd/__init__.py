@@ -56,7 +56,7 @@ EXPORTED_SYMBOLS = (
     "syncr_cache_open", "syncr_cache_get", "syncr_cache_put", "syncr_cache_sync", "syncr_cache_stats",
     "syncr_cache_close", "syncr_ingest_set_cache", "syncr_ingest_cache_hits",
     "syncr_ingest_open_multi", "syncr_ingest_device_stats", "syncr_cache_get_params",
-    "syncr_ingest_set_read_fault",
+    "syncr_ingest_set_read_fault", "syncr_cdc_fetch_reruns",
 )
 
 ABI_VERSION = 3
@@ -149,6 +149,7 @@ def library():
             "syncr_cdc_kernel_times": ([_vp, ctypes.POINTER(ctypes.c_double), _pu64], _i32),
             "syncr_cdc_last_stats": ([_vp, _pu64], _i32),
             "syncr_cdc_split_stats": ([_vp, _pu64], _i32),
+            "syncr_cdc_fetch_reruns": ([_vp, _pu64], _i32),
             "syncr_cdc_get_info": ([_vp, _pu64], _i32),
             "syncr_cdc_chunk_host_hashed": ([_vp, _vp, _u64, _vp, _u64, _pu64], _i32),
             "syncr_cdc_chunk_batch_host_hashed": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u64, _vp, _pu64], _i32),
@@ -344,6 +345,12 @@ class Chunker:
         st = (ctypes.c_uint64 * 4)()
         _check(library().syncr_cdc_last_stats(self._h, st), "syncr_cdc_last_stats")
         return {"candidates": st[0], "dense_tiles": st[1], "tiles": st[2], "flags": st[3]}
+
+    def fetch_reruns(self) -> int:
+        """Capacity re-runs the last fetch performed (syncr_cdc_fetch_reruns)."""
+        n = ctypes.c_uint64(0)
+        _check(library().syncr_cdc_fetch_reruns(self._h, ctypes.byref(n)), "syncr_cdc_fetch_reruns")
+        return int(n.value)
 
     def split_stats(self) -> dict:
         """Split walks of long files in the last fetched launch (syncr_cdc_split_stats)."""

@@ -108,6 +108,7 @@ struct syncr_cdc {
     const uint8_t *last_bytes = nullptr;
     hipStream_t last_stream = nullptr;
     uint64_t stats[4] = {0, 0, 0, 0};
+    uint64_t reruns = 0;                // capacity re-runs of the last fetch
     bool split_launched = false;        // the last launch started split workers
     uint64_t split_stats[6] = {0, 0, 0, 0, 0, 0};
 
@@ -744,6 +745,7 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
     if (hashed && !h->hash_on) return SYNCR_CDC_ESTATE;
     try {
         CHECK_HIP(hipSetDevice(h->device));
+        h->reruns = 0;
         for (int attempt = 0; attempt < 8; attempt++) {
             CHECK_HIP(hipStreamSynchronize(h->last_stream));
             uint32_t ctr[4];
@@ -802,6 +804,7 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
             if (rerun) {
                 int32_t rc = do_launch(h, h->last_bytes, h->last_stream);
                 if (rc) return rc;
+                h->reruns++;
                 continue;
             }
             h->stats[0] = ncand;
@@ -1115,6 +1118,12 @@ int32_t syncr_cdc_kernel_times_ex(syncr_cdc *h, double *ms, uint32_t n, uint64_t
 int32_t syncr_cdc_split_stats(syncr_cdc *h, uint64_t *stats6) {
     if (!h || !stats6) return SYNCR_CDC_EINVAL;
     for (int k = 0; k < 6; k++) stats6[k] = h->split_stats[k];
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_fetch_reruns(syncr_cdc *h, uint64_t *reruns) {
+    if (!h || !reruns) return SYNCR_CDC_EINVAL;
+    *reruns = h->reruns;
     return SYNCR_CDC_OK;
 }
 
