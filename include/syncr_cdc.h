@@ -292,10 +292,10 @@ int32_t syncr_cdc_last_stats(syncr_cdc *h, uint64_t *stats4);
  * waits only for file walkers to publish their segments; it gives up (and
  * leaves the rest to the file walkers, which never wait) after ~100 ms. */
 int32_t syncr_cdc_split_stats(syncr_cdc *h, uint64_t *stats6);
-/* Capacity re-runs the last fetch performed before its results were complete
- * (0: the launch it read fitted every capacity). A caller timing launches it
- * has not yet fetched checks this: launches before a re-run ran with the
- * smaller capacities. */
+/* Capacity re-runs the fetches since the handle's last launch performed before
+ * their results were complete (0: that launch fitted every capacity). A caller
+ * timing launches it has not yet fetched checks this: launches before a re-run
+ * ran with the smaller capacities. */
 int32_t syncr_cdc_fetch_reruns(syncr_cdc *h, uint64_t *reruns);
 /* Engine geometry: [run_bytes, tile_bytes, scan_grid, compute_units,
  * scan_blocks_per_cu, lds_bytes_per_scan_block, device, abi_version]. */

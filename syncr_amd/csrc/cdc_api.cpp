@@ -723,6 +723,7 @@ int32_t syncr_cdc_launch(syncr_cdc *h, const uint8_t *d_bytes, void *stream) {
     if (((uintptr_t)d_bytes & 15u) != 0) return SYNCR_CDC_EINVAL;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     h->hash_on = false;
+    h->reruns = 0;                         // re-runs are counted from the caller's launch on
     return do_launch(h, d_bytes, s);
 }
 
@@ -733,6 +734,7 @@ int32_t syncr_cdc_launch_hashed(syncr_cdc *h, const uint8_t *d_bytes, void *stre
     if (((uintptr_t)d_bytes & 15u) != 0) return SYNCR_CDC_EINVAL;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     h->hash_on = true;
+    h->reruns = 0;                         // re-runs are counted from the caller's launch on
     return do_launch(h, d_bytes, s);
 }
 
@@ -745,7 +747,6 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
     if (hashed && !h->hash_on) return SYNCR_CDC_ESTATE;
     try {
         CHECK_HIP(hipSetDevice(h->device));
-        h->reruns = 0;
         for (int attempt = 0; attempt < 8; attempt++) {
             CHECK_HIP(hipStreamSynchronize(h->last_stream));
             uint32_t ctr[4];

@@ -596,3 +596,30 @@ def test_split_workers_give_up(bits, mx, cap):
     assert got == _split_oracle(data, offs, lens, bits, mx, cap)
     assert sp["workers"] > 0 and sp["files_split"] >= 1, sp
     assert sp["giveups"] == sp["workers"] and sp["walked"] == 0 and sp["adopted"] == 0, sp
+
+
+def test_fetch_reruns_reported():
+    """syncr_cdc_fetch_reruns: a first launch whose capacities are too small
+    (periodic data: a candidate every 64 bytes) is re-run inside the fetch and
+    says so; the next launch, with the grown capacities, needs none.  bench.py
+    re-times its region when its first fetch reports a re-run."""
+    import bench
+    data = np.resize(bench.periodic_pattern(), 6 * M + 5)
+    with syncr_amd.Chunker(20, 16 << 20, 2 << 20) as ch:
+        buf = syncr_amd.DeviceBuffer(ch, data.size)
+        try:
+            buf.upload(data)
+            offs = np.array([0], np.uint64)
+            lens = np.array([data.size], np.uint64)
+            ch.plan(offs, lens, data.size)
+            ch.launch(buf.ptr)
+            first = ch.fetch()
+            assert ch.fetch_reruns() > 0
+            ch.fetch()                                   # a second fetch of the same launch: still counted
+            assert ch.fetch_reruns() > 0
+            ch.launch(buf.ptr)
+            again = ch.fetch()
+            assert ch.fetch_reruns() == 0
+            assert ends_of(first[0]) == ends_of(again[0]) == O.chunk_production_window(data).tolist()
+        finally:
+            buf.free()
