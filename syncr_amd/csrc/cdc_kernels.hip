@@ -2622,21 +2622,26 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
         const uint64_t a = (uint64_t)part * per, e = min((uint64_t)j.n, a + per);
         DevCut *dst = T.cuts + T.cut_base[i] + rel;
         const uint64_t lim = cap > rel ? cap - rel : 0ull;
-        for (uint64_t t = a + (uint64_t)lane; t < e; t += 256) {
-            uint64_t pk[4], pp[4];
+        // one load per cut: the previous candidate comes from the lane before
+        // (DPP) or the previous 64 (readlane); eight 64-candidate blocks in flight
+        constexpr int U = 8;
+        for (uint64_t t0 = a; t0 < e; t0 += 64u * U) {
+            uint64_t pk[U];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint64_t k = j.a + min(t + 64u * u, (uint64_t)j.n - 1);
+            for (int u = 0; u < U; ++u) {
+                const uint64_t k = j.a + min(t0 + 64u * u + (uint64_t)lane, (uint64_t)j.n - 1);
                 pk[u] = T.cand[k] & CAND_POS_MASK;
-                pp[u] = T.cand[k - 1] & CAND_POS_MASK;
             }
+            const uint64_t before = T.cand[j.a + t0 - 1] & CAND_POS_MASK;     // the cut before this block
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint64_t tt = t + 64u * u;
+            for (int u = 0; u < U; ++u) {
+                const uint64_t up = ((uint64_t)up1((uint32_t)(pk[u] >> 32)) << 32) | up1((uint32_t)pk[u]);
+                const uint64_t pp = lane ? up : (u ? readlane64(pk[u - 1], 63) : before);
+                const uint64_t tt = t0 + 64u * u + (uint64_t)lane;
                 if (tt < e && tt < lim) {
                     DevCut d;
-                    d.offset = pp[u] + 1 - g0;
-                    d.len = (uint32_t)(pk[u] - pp[u]);
+                    d.offset = pp + 1 - g0;
+                    d.len = (uint32_t)(pk[u] - pp);
                     d.file = i;
                     dst[tt] = d;
                 }
