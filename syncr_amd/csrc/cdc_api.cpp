@@ -218,7 +218,9 @@ Tables make_tables(syncr_cdc *h) {
     t.dense_cap = h->dense_cap;
     t.dense_bits = h->dense_bits.as<uint32_t>();
     t.cand = h->cand.as<uint64_t>();
-    t.linkw = h->linkw.as<uint64_t>();
+    // chain links only while the handle splits (periodic / low-entropy data):
+    // random data never chains, and its fix-ups skip the link work
+    t.linkw = h->split_hint ? h->linkw.as<uint64_t>() : nullptr;
     t.cand_cap = h->cand_cap;
     t.cuts = h->cuts.as<DevCut>();
     t.counts = h->counts.as<uint64_t>();

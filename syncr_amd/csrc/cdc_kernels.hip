@@ -1073,11 +1073,11 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
         // chain links (CAND_LINK): empty fix-up, next candidate 64 .. gapmax past
         const uint64_t gapmax = P.read_cap && P.read_cap < P.max_chunk ? P.read_cap : P.max_chunk;
         bool lA = false, lB = false;
-        if (2 * q + 1 < n) {
+        if (T.linkw && 2 * q + 1 < n) {
             const uint64_t d = aB - aA;                       // positions 2q+1 and 2q
             lA = fA == 0u && d >= 64u && d <= gapmax;
         }
-        if (2 * q + 2 < n) {
+        if (T.linkw && 2 * q + 2 < n) {
             const uint64_t d = (T.cand[2 * q + 2] & CAND_POS_MASK) - (aB - 1);
             lB = fB == 0u && d >= 64u && d <= gapmax;
         }
@@ -1089,11 +1089,13 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
             else if (i < items) T.gfix[i - n] = (uint8_t)f;
         }
         // the wave's 128 consecutive candidates (lane l: 2l, 2l+1) as two link words
+        if (T.linkw) {
         const unsigned long long E = __ballot(lA), O = __ballot(lB);
         const uint64_t q0 = q - (threadIdx.x & 63u);
-        if ((threadIdx.x & 63u) == 0u && 2 * q0 < n && T.linkw) {
+        if ((threadIdx.x & 63u) == 0u && 2 * q0 < n) {
             T.linkw[q0 / 32] = spread32((uint32_t)E) | (spread32((uint32_t)O) << 1);
             T.linkw[q0 / 32 + 1] = spread32((uint32_t)(E >> 32)) | (spread32((uint32_t)(O >> 32)) << 1);
+        }
         }
     }
 }
@@ -1757,17 +1759,20 @@ __device__ __forceinline__ void split_setup(const KParams &P, const Tables &T, u
 // walk of segment record `spec`, from that segment's start state into scratch,
 // until it lands on a later boundary with that boundary's start state (link),
 // reaches the file end, or passes two boundaries without landing (abort).
-template <typename Off, int PF>
+template <typename Off, int PF, bool SPLIT>
 __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, const KParams &P,
                                              const Tables &T, uint32_t i, uint64_t F, uint64_t g0, int lane,
                                              bool elig, uint32_t spec, const uint64_t *ring) {
     constexpr Off OMAX = (Off)~(Off)0;
-    const bool is_spec = spec != SPLIT_END;
+    // SPLIT = false: a launch without split workers (no segment records, no
+    // run skips, no deferral): the random-data walk, without the long-walk
+    // machinery's registers
+    const bool is_spec = SPLIT && spec != SPLIT_END;
     DevCut *out = is_spec ? T.seg_cuts + (uint64_t)spec * T.seg_scap : T.cuts + T.cut_base[i];
     uint64_t cap = is_spec ? (uint64_t)T.seg_scap : (uint64_t)T.cut_cap[i];
     // runs deferred to the copy launch (only while it runs: split workers
     // launched); a segment walk defers at most one, its scratch skipping it
-    const bool defer = T.runs_cap && !P.resolve_nosplit;
+    const bool defer = SPLIT && T.runs_cap && !P.resolve_nosplit;
     uint32_t run_pre = 0, run_len = 0;
     const Off Fo = (Off)F;
     const Off MAX = (Off)min<uint64_t>(P.max_chunk, (uint64_t)OMAX);
@@ -1780,7 +1785,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
     const bool dbgw = elig && T.order[0] == i;              // (development timeline: the largest file)
     (void)dbgw;
     if (dbgw) DBG_STAMP(T, DBG_W_ENTRY);
-    if (elig) {
+    if (SPLIT && elig) {
         uint32_t first, nseg;
         split_setup(P, T, i, F, g0, ncand, lane, first, nseg);
         if (dbgw) DBG_STAMP(T, DBG_W_SETUP);
@@ -1938,7 +1943,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
     if (is_spec) start_at_lane0((Off)seg_ld(T.segs[spec].s0), (Off)seg_ld(T.segs[spec].R0));
     uint32_t link = SPLIT_END;          // segment walk: the record it linked at / SPLIT_END / SPLIT_ABORT
     while (s < R) {                                          // :747
-        if (s >= sb) {
+        if (SPLIT && s >= sb) {
             // at or past boundary brec: a landing with the boundary's start state
             // links (segment walk) or adopts the boundary's segment walk (file walker)
             bool stop = false;
@@ -2080,7 +2085,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                     // window ring at the run's last cut.  The run stops at the next
                     // split boundary's candidate (a landing there is decided above)
                     // and at the file's last candidate.
-                    if (T.linkw && !P.no_skip && ncand && __ballot((uint32_t)lane >= (uint32_t)jlast && !(wk & 0x200u)) == 0ull) {
+                    if (SPLIT && T.linkw && !P.no_skip && ncand && __ballot((uint32_t)lane >= (uint32_t)jlast && !(wk & 0x200u)) == 0ull) {
                         const uint64_t ci = wb + (uint64_t)jlast;               // the last cut's candidate
                         uint64_t lim = ncand - 1;
                         if (sbi < lim) lim = sbi;
@@ -2480,7 +2485,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
         T.counts[i] = (uint64_t)cnt;
         if ((uint64_t)cnt > cap) atomicOr(&T.ctr[CTR_FLAGS], FLAG_CUT_OVERFLOW);
     }
-    if (elig && bend) {                                      // adoptions before the done count
+    if (SPLIT && elig && bend) {                             // adoptions before the done count
         __threadfence();
         if (lane == 0) atomicAdd(&T.split[SPL_DONE], 1u);
     }
@@ -2563,7 +2568,7 @@ __device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P,
             __hip_atomic_store(&T.segs[q].res, seg_res(SEG_WALKING, 0u, 0u), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         if (q < DBG_NREC) DBG_STAMP(T, DBG_REC + 2 * q);
-        resolve_walk<uint32_t, PF>(data, P, T, i, T.flen[i], T.foff[i], lane, false, q, ring);
+        resolve_walk<uint32_t, PF, true>(data, P, T, i, T.flen[i], T.foff[i], lane, false, q, ring);
         if (q < DBG_NREC) DBG_STAMP(T, DBG_REC + 2 * q + 1);
     }
 }
@@ -2654,7 +2659,7 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
 // the file walkers' (launched only when a file is eligible) are split workers.
 // (Their walk is a separate inlined copy: sharing one with the file walkers
 // made the file walk spill scalar registers.)
-template <int PF>
+template <int PF, bool SPLIT>
 __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__restrict__ data,
                                                                KParams P, Tables T) {
     const int lane = threadIdx.x & 63;
@@ -2669,7 +2674,7 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
     // files had published their segments and waited (their waits are bounded,
     // and the file walkers never wait on a worker that has not started)
     const uint32_t b = P.split_first ? (blockIdx.x >= nwork ? blockIdx.x - nwork : nmain + blockIdx.x) : blockIdx.x;
-    if (b >= nmain) {
+    if (SPLIT && b >= nmain) {
         const uint32_t widx = __builtin_amdgcn_readfirstlane((b - nmain) * 4u + (threadIdx.x >> 6));
         split_worker<PF>(data, P, T, lane, ring, widx, 4u * nwork);
         return;
@@ -2681,11 +2686,11 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
     const bool elig = kf < T.n_elig;
     if (kf == 0) DBG_STAMP(T, 7);
     if (F <= 0xFFFFFF00ull) {
-        resolve_walk<uint32_t, PF>(data, P, T, i, F, g0, lane, elig, SPLIT_END, ring);
+        resolve_walk<uint32_t, PF, SPLIT>(data, P, T, i, F, g0, lane, elig, SPLIT_END, ring);
         if (kf < DBG_NFW) DBG_STAMP(T, DBG_FW + kf);
     } else {
         if (elig && lane == 0) atomicAdd(split_pub(T), 1ull);            // counted, never split
-        resolve_walk<uint64_t, PF>(data, P, T, i, F, g0, lane, false, SPLIT_END, ring);
+        resolve_walk<uint64_t, PF, SPLIT>(data, P, T, i, F, g0, lane, false, SPLIT_END, ring);
     }
 }
 
@@ -3016,16 +3021,19 @@ hipError_t launch_resolve(const uint8_t *d, const KParams &p, const Tables &t, h
 #ifdef SYNCR_CDC_DEV
         if (p.resolve_pf && p.resolve_pf != RESOLVE_PF) {           // (development A/B: SYNCR_CDC_RESOLVE_PF)
             switch (p.resolve_pf) {
-                case 2: hipLaunchKernelGGL(cdc_resolve_wave_kernel<2>, grid, dim3(256), 0, s, d, p, t); break;
-                case 4: hipLaunchKernelGGL(cdc_resolve_wave_kernel<4>, grid, dim3(256), 0, s, d, p, t); break;
-                case 8: hipLaunchKernelGGL(cdc_resolve_wave_kernel<8>, grid, dim3(256), 0, s, d, p, t); break;
-                case 16: hipLaunchKernelGGL(cdc_resolve_wave_kernel<16>, grid, dim3(256), 0, s, d, p, t); break;
-                case 32: hipLaunchKernelGGL(cdc_resolve_wave_kernel<32>, grid, dim3(256), 0, s, d, p, t); break;
+                case 2: hipLaunchKernelGGL((cdc_resolve_wave_kernel<2, true>), grid, dim3(256), 0, s, d, p, t); break;
+                case 4: hipLaunchKernelGGL((cdc_resolve_wave_kernel<4, true>), grid, dim3(256), 0, s, d, p, t); break;
+                case 8: hipLaunchKernelGGL((cdc_resolve_wave_kernel<8, true>), grid, dim3(256), 0, s, d, p, t); break;
+                case 16: hipLaunchKernelGGL((cdc_resolve_wave_kernel<16, true>), grid, dim3(256), 0, s, d, p, t); break;
+                case 32: hipLaunchKernelGGL((cdc_resolve_wave_kernel<32, true>), grid, dim3(256), 0, s, d, p, t); break;
                 default: return hipErrorInvalidValue;
             }
         } else
 #endif
-        hipLaunchKernelGGL(cdc_resolve_wave_kernel<RESOLVE_PF>, grid, dim3(256), 0, s, d, p, t);
+        if (split)
+            hipLaunchKernelGGL((cdc_resolve_wave_kernel<RESOLVE_PF, true>), grid, dim3(256), 0, s, d, p, t);
+        else
+            hipLaunchKernelGGL((cdc_resolve_wave_kernel<RESOLVE_PF, false>), grid, dim3(256), 0, s, d, p, t);
         if (split) hipLaunchKernelGGL(cdc_split_copy_kernel, dim3(1024), dim3(256), 0, s, t);
     }
     return hipGetLastError();
