@@ -97,6 +97,10 @@ struct syncr_cdc {
     // periodic or low-entropy data: thousands per MiB).  Off until a fetch has
     // seen that, so the common case launches no split workers at all.
     bool split_hint = false;
+    // the dense pass runs only once a fetched launch of this handle held a dense
+    // tile (low-entropy / periodic data); until then its launch is skipped, and a
+    // launch that turns out to hold dense tiles is re-run by fetch with it
+    bool dense_hint = false, last_dense_off = false;
 
     // two per-launch zeroed blocks (Tables::znext): launch k uses block zpar; the
     // resolve of launch k zeroes the other one for launch k+1
@@ -243,6 +247,7 @@ Tables make_tables(syncr_cdc *h) {
     t.znext_vec = (uint32_t)(zstride(h) / 16);
     t.hzero = nullptr;
     t.dbg = h->dbg.p ? h->dbg.as<uint64_t>() : nullptr;
+    t.dense_off = (!h->dense_hint && !scan_dense_inline(h->geom, h->kp)) ? 1u : 0u;
     // SplitSeg records outlive a launch: a record is ready for this launch only
     // when its ready word holds this launch's id (records are zeroed when allocated)
     static std::atomic<uint32_t> epochs{0};
@@ -434,6 +439,7 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     // just the two around the scan
     const bool phases = h->timing && !h->timing_scan_only;
     CHECK_HIP(launch_post(d_bytes, kp, t, s, scan_dense_inline(h->geom, kp)));
+    h->last_dense_off = t.dense_off != 0u;
     if (phases) CHECK_HIP(hipEventRecord(pt.ev[2], s));
     CHECK_HIP(launch_resolve(d_bytes, kp, t, s));
     h->split_launched = resolve_splits(kp, t);
@@ -780,6 +786,10 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
             }
 #endif
             bool rerun = false;
+            if (h->last_dense_off && ctr[CTR_DENSE]) {       // dense tiles the launch left unpassed
+                h->dense_hint = true;
+                rerun = true;
+            }
             if (ctr[CTR_FLAGS] & FLAG_DENSE_OVERFLOW) {
                 // the counter includes the slots of every wave's last chunk: enough
                 const uint64_t need = (uint64_t)ctr[CTR_DENSE] + ctr[CTR_DENSE] / 4 + 16;

@@ -207,6 +207,8 @@ struct Tables {
     uint32_t seg_segc, seg_scap;   // candidates per segment, scratch cuts per segment walk
     uint32_t split_blocks;         // extra resolve blocks (split workers)
     uint32_t *split;               // [SPL_WORDS] counters                    (zeroed per launch)
+    uint32_t dense_off;            // 1: no dense pass this launch (the handle has not seen a dense tile);
+                                   //   the compaction counts dense tiles as empty and fetch re-runs if any
     RunJob *runs;                  // [runs_cap] deferred runs (only while split workers run)
     uint32_t runs_cap;
     uint32_t epoch;                // this launch's id (!= 0, unique in the process): SplitSeg::ready

@@ -1416,6 +1416,7 @@ __device__ __forceinline__ uint64_t word_prefix(const Tables &T, uint32_t w, int
 // dense tile (grid-stride over the dense list): a word of 64 dense tiles on
 // one wave was 64 dependent bitmap passes (dense1: 330 us for 2.1 M candidates).
 __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t wid, uint32_t nw_waves) {
+    if (T.dense_off) return;                                 // (no blocks are launched for it then)
     const uint32_t nd = min(T.ctr[CTR_DENSE], T.dense_cap);
     const uint32_t nw = T.tile / 32;
     for (uint32_t idx = wid; idx < nd; idx += nw_waves) {
@@ -1489,7 +1490,7 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
         meta = T.tile_meta[tile];
         if (meta & DENSE_BIT) {
             const uint32_t idx = meta & ~DENSE_BIT;
-            c = idx < T.dense_cap ? T.dense_cnt[idx] : 0u;
+            c = (!T.dense_off && idx < T.dense_cap) ? T.dense_cnt[idx] : 0u;
         } else {
             c = meta;
         }
@@ -2988,6 +2989,8 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
     const uint32_t dblocks = t.dense_cap < 2048u ? (t.dense_cap ? t.dense_cap : 1u) : 2048u;
     if (dense_inline) {
         // (development A/B) the scan passed its dense tiles itself
+    } else if (t.dense_off) {
+        // no dense tile seen yet on this handle: no dense launch (fetch re-runs if needed)
     } else if (t.tile == (uint32_t)tile_bytes(DEFAULT_RUN)) {
         hipLaunchKernelGGL(cdc_dense_packed_kernel<DEFAULT_RUN>, dim3(dblocks), dim3(64), buf_bytes(DEFAULT_RUN), s,
                            d, p, t);
@@ -2999,7 +3002,7 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
     // + up to 2048 blocks (one wave per dense tile) that expand dense tiles; they
     // exit at once when there are none.  (256 blocks left ~33 serial tile
     // expansions per wave on the dense workload: 0.2 ms.)
-    const uint32_t dgb = std::min<uint32_t>((t.dense_cap + 3) / 4, 2048u);
+    const uint32_t dgb = t.dense_off ? 0u : std::min<uint32_t>((t.dense_cap + 3) / 4, 2048u);
     hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4 + dgb), dim3(256), 0, s, t);
     const uint64_t want = (t.cand_cap + t.ngrid + 511) / 512;       // two items per thread
     const uint32_t blocks = (uint32_t)(want < 2048 ? (want ? want : 1) : 2048);
