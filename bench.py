@@ -314,20 +314,30 @@ def run_legs(args, dev_id: int, dbuf, offs, lens, idx, rank_span: int, out: dict
     parity["blake3_vectors"] = timed("blake3_vectors", L.blake3_vectors_leg, dev_id)
     parity["dense_subset"] = timed("dense_subset", L.dense_subset_leg, dev_id)
     k, w = args.steps, max(args.warmup, 2)
+    if args.workload == "zipf10k":
+        # BASELINE config 4's per-rank batch (zipf10k / 8, LPT) timed on this GPU
+        out["shard8"] = timed("shard8", L.shard_leg, dev_id, k, w, 8)
     if args.workload != "uniform1k":
         out["uniform1k"] = timed("uniform1k", L.uniform1k_leg, dev_id, k, w)
     if args.workload != "dedup":
         out["dedup"] = timed("dedup", L.dedup_leg, dev_id, k, w)
     if args.workload != "dense":
         out["dense"] = timed("dense", L.dense_leg, dev_id, k, w)
+    out["h2d_probe"] = timed("h2d_probe", L.h2d_probe, dev_id)
     if host is not None:
         out["ingest"] = timed("ingest", L.ingest_leg, host, offs, lens, idx, dev_id)
         parity["ingest_multi_device"] = out["ingest"].get("multi_device", {}).get("parity")
+        out["ingest_files"] = timed("ingest_files", L.ingest_files_leg, host, offs, lens, idx, dev_id)
+        h2d = out["h2d_probe"].get("h2d", {}).get("best_gbs")
+        for key in ("ingest", "ingest_files"):
+            v = out[key].get("value")
+            if h2d and v:          # the end-to-end rate on its link ceiling (GiB/s -> GB/s)
+                out[key]["frac_of_h2d"] = round(v * 2**30 / 1e9 / h2d, 4)
     del host
     # one summary: every parity check of the line
     checks = []
     for name, p in list(parity.items()) + [(f"{s}.parity", out.get(s, {}).get("parity")) for s in
-                                            ("uniform1k", "dedup", "dense", "ingest")] + \
+                                            ("shard8", "uniform1k", "dedup", "dense", "ingest", "ingest_files")] + \
             [(f"{s}.parity_hashed", out.get(s, {}).get("parity_hashed")) for s in ("dedup", "dense")]:
         if isinstance(p, dict) and "mismatches" in p:
             checks.append((name, p.get("files", p.get("cases", 0)), p["mismatches"] + p.get("hash_mismatches", 0)))

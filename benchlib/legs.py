@@ -98,6 +98,7 @@ def kat_leg(device: int = 0) -> dict:
             h.close()
     out = {"cases": len(cases), "adversarial_head_cases": sum(c["name"].startswith("adversarial_head")
                                                               for c in cases),
+           "adversarial_head_b20_cases": sum(c["name"].startswith("adversarial_head_b20") for c in cases),
            "mismatches": bad, "chunk_hashes_checked": nhash, "hash_mismatches": hbad,
            "fixture": "tests/golden/kat_cases.json"}
     if names:
@@ -197,6 +198,89 @@ def uniform1k_leg(device: int, steps: int, warmup: int) -> dict:
     out.update({"config": "SURVEY §8d config 2: 1024 x 1 MiB random files, 1 GiB, production semantics",
                 "parity": {"files": len(cuts), "chunks": int(sum(c.size for c in cuts)), "mismatches": int(bad),
                            "fixture": "tests/golden/corpus_uniform_1024x1MiB.json (every cut)"}})
+    return out
+
+
+def shard_leg(device: int, steps: int, warmup: int, nshards: int = 8) -> dict:
+    """BASELINE config 4's per-rank work on this one GPU: zipf10k LPT-sharded
+    per file into `nshards` shards (exactly what bench.py --gpus N --scaling
+    strong gives each rank), each shard generated in HBM and timed as its own
+    planned batch (W warm-up + K one-in-flight steps), one shard after another.
+    Every shard's files are checked against the golden digests.  The projected
+    N-GPU aggregate is the corpus bytes / the slowest shard's step: a one-GPU
+    projection, not a measured scaling point (files are independent,
+    file_operations.rs:599-605,721-788, so ranks share nothing but the clock)."""
+    import syncr_amd
+    sizes = WL.zipf_sizes()
+    shards = WL.lpt_shard(sizes, nshards)
+    biggest = max(int(sizes[s].sum()) for s in shards)
+    per, mism, nfiles = [], 0, 0
+    with syncr_amd.Chunker(device=device) as ch:
+        b = syncr_amd.DeviceBuffer(ch, biggest)
+        try:
+            for r, sh in enumerate(shards):
+                lens = sizes[sh]
+                offs = WL.offsets_of(lens)
+                span = int(lens.sum())
+                b.gen_corpus(offs, lens, indices=sh.astype(np.uint64))
+                ch.plan(offs, lens, span)
+                t = time_steps(ch, b.ptr, span, steps, warmup)
+                p = G.check_files("zipf10k", ch.fetch(), sh)
+                mism += p["mismatches"]
+                nfiles += p["files"]
+                per.append({"shard": r, "files": int(sh.size), "bytes": span, "ms_per_step": t["ms_per_step"],
+                            "scan_ms": t["scan_ms"], "scan_frac": t["scan_frac"],
+                            "step_frac": round(span / (t["ms_per_step"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                            "dense_ms": t["dense_ms"], "resolve_ms": t["resolve_ms"],
+                            "parity_mismatches": p["mismatches"]})
+        finally:
+            b.free()
+    total = int(sizes.sum())
+    worst = max(x["ms_per_step"] for x in per)
+    return {"nshards": nshards, "shards": per, "total_bytes": total,
+            "max_ms_per_step": worst,
+            "projected_value": round(total / (worst / 1e3) / 2**30, 3), "unit": "GiB/s",
+            "projected_note": (f"one-GPU projection of the N={nshards} strong-scaling aggregate (BASELINE config 4): "
+                               "corpus bytes / the slowest shard's step, each shard timed alone on this GPU; no "
+                               "multi-GPU scaling was measured"),
+            "mean_step_frac": round(sum(x["step_frac"] for x in per) / len(per), 4),
+            "mean_scan_frac": round(sum(x["scan_frac"] for x in per) / len(per), 4),
+            "load_balance_max_over_mean_ms": round(worst / (sum(x["ms_per_step"] for x in per) / len(per)), 4),
+            "parity": {"files": nfiles, "mismatches": mism, "fixture": "tests/golden/zipf10k_digests.npz",
+                       "semantics": "production"}}
+
+
+def h2d_probe(device: int, nbytes: int = 256 << 20, reps: int = 10) -> dict:
+    """The end-to-end path's link ceiling: pinned host memory -> device with
+    hipMemcpyAsync (syncr_cdc_memcpy_h2d on the handle's stream), `reps` copies
+    of `nbytes`, each timed by the host around a stream synchronisation; and
+    the same device -> pinned host."""
+    import ctypes
+    import syncr_amd
+    L = syncr_amd.library()
+    out = {}
+    with syncr_amd.Chunker(device=device) as ch:
+        hp = ctypes.c_void_p()
+        syncr_amd._check(L.syncr_cdc_host_alloc_pinned(ch.handle, nbytes, ctypes.byref(hp)), "host_alloc_pinned")
+        d = syncr_amd.DeviceBuffer(ch, nbytes)
+        try:
+            ctypes.memset(hp, 0x5A, nbytes)
+            for name, fn, dst, src in (("h2d", L.syncr_cdc_memcpy_h2d, d.ptr, hp.value),
+                                       ("d2h", L.syncr_cdc_memcpy_d2h, hp.value, d.ptr)):
+                ts = []
+                for _ in range(reps + 1):
+                    t0 = time.perf_counter()
+                    syncr_amd._check(fn(ch.handle, dst, src, nbytes, None), name)
+                    ch.synchronize()
+                    ts.append(time.perf_counter() - t0)
+                ts = ts[1:]                                       # the first copy maps the pages
+                out[name] = {"best_gbs": round(nbytes / min(ts) / 1e9, 2),
+                             "mean_gbs": round(nbytes / (sum(ts) / len(ts)) / 1e9, 2)}
+        finally:
+            d.free()
+            L.syncr_cdc_host_free_pinned(ch.handle, hp)
+    out.update({"bytes_per_copy": nbytes, "copies": reps,
+                "path": "hipHostMalloc'd (pinned) buffer <-> device, hipMemcpyAsync on one stream, host-timed per copy"})
     return out
 
 
@@ -376,6 +460,55 @@ def ingest_leg(host: np.ndarray, offs, lens, idx, device: int, reps: int = 2, mu
     out["multi_device"] = {"devices": [device, device], "per_device_files": [d["files"] for d in ds],
                            "parity": G.check_files("zipf10k", got, idx[:nm], hashed=True)}
     return out
+
+
+def ingest_files_leg(host: np.ndarray, offs, lens, idx, device: int, gib: float = 2.0, reps: int = 2) -> dict:
+    """End to end FROM FILES, as the reference reads them (File::open + reads,
+    file_operations.rs:737-745,776): the first zipf10k files up to `gib` GiB
+    are written to local disk (a temporary directory), then every file goes
+    through syncr_ingest_submit_file (pread straight into pinned staging ->
+    H2D -> chunk + BLAKE3 -> per-file ChunkInfo callbacks); every file is
+    checked against the golden digests.  The files were just written, so they
+    are served from the page cache (this process cannot drop it)."""
+    import shutil
+    import tempfile
+    import syncr_amd
+    take, tot = [], 0
+    for j in range(lens.size):
+        if tot >= gib * 2**30:
+            break
+        take.append(j)
+        tot += int(lens[j])
+    d = tempfile.mkdtemp(prefix="syncr_ingest_files_")
+    res: dict = {}
+    try:
+        paths = []
+        for j in take:
+            pth = os.path.join(d, f"f{j:05d}.bin")
+            with open(pth, "wb") as f:
+                f.write(host[int(offs[j]): int(offs[j] + lens[j])].tobytes())
+            paths.append(pth)
+        best = None
+        with syncr_amd.Ingest(device=device, batch_bytes=256 << 20, depth=3, copy_threads=16,
+                              on_file=lambda t, st, a: res.__setitem__(t, (st, a))) as g:
+            for _ in range(reps):
+                res.clear()
+                t0 = time.perf_counter()
+                for k, pth in enumerate(paths):
+                    g.submit_file(pth, k)
+                g.flush()
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    got = [res[k][1] for k in range(len(take))]
+    return {"value": round(tot / best / 2**30, 3), "unit": "GiB/s", "seconds": round(best, 4), "bytes": tot,
+            "files": len(take),
+            "path": "files on local disk (page-cache resident: just written) -> syncr_ingest_submit_file (pread "
+                    "into pinned staging, 16 threads) -> H2D -> chunk + BLAKE3 -> per-file ChunkInfo; best of %d "
+                    "passes" % reps,
+            "status_nonzero": int(sum(res[k][0] != 0 for k in range(len(take)))),
+            "parity": G.check_files("zipf10k", got, idx[np.array(take, np.int64)], hashed=True)}
 
 
 def ingest_multi_leg(device: int = 0, max_file: int = 4 * M, nfiles: int = 1500) -> dict:

@@ -120,10 +120,25 @@ int32_t syncr_cdc_chunk_batch_host_hashed(syncr_cdc *h, const uint8_t *data, uin
  * Synchronous; reusable for any number of launches. */
 int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *file_len,
                        uint32_t nfiles, uint64_t span);
-/* launch: scan + resolve on `stream`, asynchronous, no host sync, no allocation
- * (graph-capturable).  d_bytes must be 16-byte aligned device memory. */
+/* launch: scan + resolve on `stream`, asynchronous: no host synchronisation and
+ * no allocation.  d_bytes must be 16-byte aligned device memory.
+ * Buffer lifetime: the bytes at [d_bytes, d_bytes + span) must stay resident
+ * and UNMODIFIED until the fetch of this launch returns -- fetch may launch the
+ * scan again over the same bytes (a capacity re-run, see
+ * syncr_cdc_fetch_reruns), so e.g. the next batch's H2D copy into the same
+ * buffer must be ordered after that fetch, not merely after this launch.
+ * Streams: all launches of one handle share its device tables.  A launch on a
+ * stream other than the previous launch's waits (on the device) for all work
+ * enqueued on that previous stream, so launches of one handle never overlap,
+ * whatever streams the caller alternates between; a stream passed here must
+ * stay valid until the next launch or fetch of the handle.  Because results
+ * are only known to be complete at fetch time (re-runs happen inside fetch), a
+ * launch captured into a HIP graph still needs syncr_cdc_fetch afterwards; the
+ * engine makes no claim beyond that. */
 int32_t syncr_cdc_launch(syncr_cdc *h, const uint8_t *d_bytes, void *stream);
-/* fetch: wait for the last launch, copy cuts to the host (file by file). */
+/* fetch: wait for the last launch, copy cuts to the host (file by file).  May
+ * re-run the launch on its stream first (grown capacities), reading d_bytes
+ * again. */
 int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap,
                         uint64_t *per_file_count, uint64_t *n_out);
 /* launch_hashed: launch, then BLAKE3 of every chunk on the same stream

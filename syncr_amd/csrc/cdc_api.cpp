@@ -24,9 +24,15 @@ using namespace cdc;
 
 namespace {
 
+// A device allocation owned by its holder: released by its destructor, so a
+// buffer added to syncr_cdc can never be missed by syncr_cdc_close.
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
         if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
@@ -110,7 +116,8 @@ struct syncr_cdc {
     // launch
     bool launched = false;
     const uint8_t *last_bytes = nullptr;
-    hipStream_t last_stream = nullptr;
+    hipStream_t last_stream = nullptr;  // stream of the last launch (nullptr: none since open)
+    hipEvent_t xstream_ev = nullptr;    // orders a launch after the previous one on another stream
     uint64_t stats[4] = {0, 0, 0, 0};
     uint64_t reruns = 0;                // capacity re-runs of the last fetch
     bool split_launched = false;        // the last launch started split workers
@@ -413,6 +420,18 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
         // event would stall the queue and perturb the kernels being timed)
         for (int k = 0; k < pt.nev; k++) CHECK_HIP(hipEventCreateWithFlags(&pt.ev[k], hipEventDisableSystemFence));
     }
+    // All launches of a handle share its tables (counter blocks, candidate
+    // list, cuts, hash work lists).  On the same stream they are ordered; when
+    // the caller switches streams, this launch first waits for everything
+    // enqueued on the previous launch's stream (an event recorded there now),
+    // so no two launches of one handle ever overlap -- and the block the
+    // previous resolve zeroed (zclean) is zero by the time this scan starts.
+    if (h->last_stream && s != h->last_stream) {
+        if (!h->xstream_ev)
+            CHECK_HIP(hipEventCreateWithFlags(&h->xstream_ev, hipEventDisableTiming | hipEventDisableSystemFence));
+        CHECK_HIP(hipEventRecord(h->xstream_ev, h->last_stream));
+        CHECK_HIP(hipStreamWaitEvent(s, h->xstream_ev, 0));
+    }
     const uint32_t par = h->zpar;
     if (!h->zclean[par]) CHECK_HIP(hipMemsetAsync(zblock(h, par), 0, zeroed_bytes(h), s));
     h->zclean[par] = false;
@@ -601,15 +620,9 @@ void syncr_cdc_close(syncr_cdc *h) {
         so.open--;
         (void)hipEventDestroy(h->scan_done);
     }
-    DevBuf *bufs[] = {&h->fstart, &h->foff, &h->flen, &h->order, &h->cut_base, &h->cut_cap,
-                      &h->tile_meta, &h->slots, &h->zeroed, &h->dense_list,
-                      &h->dense_cnt, &h->dense_bits, &h->super_off, &h->cand, &h->cuts,
-                      &h->counts, &h->stage, &h->hctr, &h->items, &h->trees, &h->gcv,
-                      &h->hashes, &h->packed, &h->tpieces, &h->pieces, &h->pcv, &h->gpos, &h->gend, &h->gfix, &h->gbase,
-                      &h->segs, &h->seg_cuts, &h->iblocks};
-    for (DevBuf *b : bufs) b->release();
+    if (h->xstream_ev) (void)hipEventDestroy(h->xstream_ev);
     (void)hipStreamDestroy(h->stream);
-    delete h;
+    delete h;                   // every DevBuf member frees its memory (on this device, set above)
 }
 
 int32_t syncr_cdc_get_params(const syncr_cdc *h, syncr_cdc_params *p) {
@@ -624,6 +637,8 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
     if (nfiles && (!file_off || !file_len)) return SYNCR_CDC_EINVAL;
     try {
         CHECK_HIP(hipSetDevice(h->device));
+        // the tables below are rewritten: a launch still running reads them
+        if (h->last_stream) CHECK_HIP(hipStreamSynchronize(h->last_stream));
         h->planned = false;
         h->launched = false;
         // validate: inside span, non-empty files must not overlap
@@ -821,13 +836,15 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
                 continue;
             }
             h->stats[0] = ncand;
-            h->stats[1] = ctr[CTR_DENSE];
             h->stats[2] = h->ntiles;
             h->stats[3] = ctr[CTR_FLAGS];
             {
                 uint32_t sp[SPL_WORDS];
                 CHECK_HIP(hipMemcpy(sp, zblock(h, h->zlast) + split_ctr_offset(h), sizeof sp,
                                     hipMemcpyDeviceToHost));
+                // dense tiles the dense pass rolled (the list counter also counts the
+                // unused slots of the scan waves' 8-slot chunks)
+                h->stats[1] = ctr[CTR_DENSE] ? sp[SPL_DENSE_TILES] : 0u;
                 h->split_stats[0] = h->split_launched ? 4ull * h->split_blocks : 0ull;   // worker waves
                 h->split_stats[1] = sp[SPL_PUB64 + 1];          // split files (high half of the 64-bit count)
                 h->split_stats[2] = std::min<uint32_t>(sp[SPL_RESERVED], h->seg_cap);

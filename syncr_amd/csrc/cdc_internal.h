@@ -114,9 +114,10 @@ constexpr uint32_t SPLIT_ABORT = 0xfffffffeu;           // (segment walk state: 
 // split[] words: a 64-bit count (split files << 32 | eligible walkers
 // published), so one relaxed read gives both; segment records reserved;
 // queue head; split walkers done; worker give-ups; segments walked by workers;
-// segments adopted by file walkers
+// segments adopted by file walkers; deferred runs; dense tiles the dense pass
+// rolled (ctr[CTR_DENSE] counts list slots, DENSE_HOLE padding included)
 enum { SPL_PUB64 = 0, SPL_RESERVED = 2, SPL_HEAD = 3, SPL_DONE = 4, SPL_GIVEUP = 5, SPL_WALKED = 6,
-       SPL_ADOPTED = 7, SPL_RUNS = 8, SPL_WORDS = 9 };
+       SPL_ADOPTED = 7, SPL_RUNS = 8, SPL_DENSE_TILES = 9, SPL_WORDS = 10 };
 struct SplitSeg {            // 64 bytes
     uint64_t cidx;           // candidate index of the segment's first candidate
     uint64_t out_off;        // adopted: first cut slot within the file's output
@@ -225,9 +226,14 @@ struct Tables {
 // dev timeline slots: resolve entry (min over waves), end (max); the largest
 // split file's walker: entry, after split setup, adoption blocks (start, end),
 // walk end; split workers: record q < DBG_NREC walk start / end; copy kernel
+// scan timeline: per scan wave (block) w < DBG_SCAN_N: entry, first tile landed,
+// exit, tiles rolled (DBG_SCAN + 4 w ...); per-tile ends of waves < DBG_TILE_W
+// (DBG_TILE + DBG_TILE_N w + k, k-th tile)
 enum { DBG_RES_START = 0, DBG_RES_END = 1, DBG_W_ENTRY = 2, DBG_W_SETUP = 3, DBG_W_END = 4, DBG_W_NBLK = 5,
        DBG_W_BLK = 8, DBG_MAXBLK = 120, DBG_COPY_START = 248, DBG_COPY_END = 249, DBG_REC = 256,
-       DBG_NREC = 1024, DBG_FW = DBG_REC + 2 * DBG_NREC, DBG_NFW = 1024, DBG_WORDS = DBG_FW + DBG_NFW };
+       DBG_NREC = 1024, DBG_FW = DBG_REC + 2 * DBG_NREC, DBG_NFW = 1024, DBG_SCAN = DBG_FW + DBG_NFW,
+       DBG_SCAN_N = 4096, DBG_TILE = DBG_SCAN + 4 * DBG_SCAN_N, DBG_TILE_W = 16, DBG_TILE_N = 128,
+       DBG_WORDS = DBG_TILE + DBG_TILE_W * DBG_TILE_N };
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------
 // A lane TASK is B3_LANE_LEAVES consecutive 1 KiB leaves of one chunk.  A chunk

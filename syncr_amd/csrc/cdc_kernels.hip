@@ -94,6 +94,14 @@ __device__ __forceinline__ uint64_t sload_u64(const void *p) {
     return v;
 }
 
+// development timeline of the scan (Tables::dbg, SYNCR_CDC_TRACE=1): lane 0
+// stores a value; compiled out of the product library, a no-op without tracing
+#ifdef SYNCR_CDC_DEV
+#define SCAN_STAMP(T, slot, v) do { if ((T).dbg && lane == 0) (T).dbg[(slot)] = (v); } while (0)
+#else
+#define SCAN_STAMP(T, slot, v) do { } while (0)
+#endif
+
 __device__ __forceinline__ void record(uint32_t *wcount, uint32_t *wlist, uint32_t rel) {
     const uint32_t idx = atomicAdd(wcount, 1u);
     if (idx < (uint32_t)LISTCAP) wlist[idx] = rel;
@@ -463,9 +471,14 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     uint32_t tile = blockIdx.x;
     if (tile >= T.ntiles) return;
     const int64_t span = (int64_t)T.span;
+    const bool stamp = blockIdx.x < (uint32_t)DBG_SCAN_N;
+    if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x, wall_clock64());
     issue_tile<RUN, (MODE & 4) != 0>(data, T.span, tile, lds0, lane);
     uint32_t gj = 0, pend = 0;
     DenseSlots dslots_alloc;
+#ifdef SYNCR_CDC_DEV
+    uint32_t ntile_done = 0;
+#endif
     for (uint32_t next; tile < T.ntiles; tile = next) {
         bool grabbed = false;
         uint32_t gjn = 0;
@@ -488,6 +501,12 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         const int64_t t0 = (int64_t)tile * TILE;
         if (lane == 0) { *wcount = 0u; *dcount = 0u; }
         wait_vmcnt<0>();                                             // this tile has landed
+#ifdef SYNCR_CDC_DEV
+        if (stamp && ntile_done == 0) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 1, wall_clock64());
+        if (blockIdx.x < (uint32_t)DBG_TILE_W && ntile_done < (uint32_t)DBG_TILE_N)
+            SCAN_STAMP(T, DBG_TILE + DBG_TILE_N * blockIdx.x + ntile_done, wall_clock64());
+        ++ntile_done;
+#endif
         uint32_t A[NQ * 4], B[NQ * 4];
         {
             const uint4 *la = (const uint4 *)(wl + lane * RUN);          // = run start - 64
@@ -530,6 +549,12 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         if (nd && nd <= (uint32_t)DIRTYCAP) rewalk_dirty<RUN>(P, lane, nd, dslots, lim_rel, wcount, wlist);
         publish_tile(data, P, T, tile, t0, wlist, wcount, lane, nd > (uint32_t)DIRTYCAP, dslots_alloc);
     }
+#ifdef SYNCR_CDC_DEV
+    if (stamp) {
+        SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 2, wall_clock64());
+        SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 3, (uint64_t)ntile_done);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1176,6 +1201,7 @@ __global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict
             T.dense_cnt[idx] = cnt;
             atomicAdd(&T.super_cnt[tile >> 6], cnt);
             atomicAdd(&T.coarse[(tile >> 12) * COARSE_STRIDE], cnt);
+            atomicAdd(&T.split[SPL_DENSE_TILES], 1u);
         }
     }
 }
@@ -1298,6 +1324,7 @@ __device__ __forceinline__ void scan_dense_tile(const uint8_t *__restrict__ data
         T.tile_meta[tile] = DENSE_BIT | idx;
         atomicAdd(&T.super_cnt[tile >> 6], cnt);
         atomicAdd(&T.coarse[(tile >> 12) * COARSE_STRIDE], cnt);
+        atomicAdd(&T.split[SPL_DENSE_TILES], 1u);
     }
 }
 
@@ -1343,7 +1370,7 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
         if (++idx >= iend) return;
         tile = sload_u32(&T.dense_list[idx]);
     }
-    uint32_t cur_c = tile >> 12, acc_c = 0;
+    uint32_t cur_c = tile >> 12, acc_c = 0, ndone = 0;
     issue_tile<RUN, true>(data, T.span, tile, lds0, lane);
     for (uint32_t next; idx < iend; idx = next) {
         next = idx + 1;
@@ -1376,6 +1403,7 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
             acc_c = 0;
         }
         acc_c += cnt;
+        ++ndone;
         if (lane == 0) {
             T.dense_cnt[idx] = cnt;
             atomicAdd(&T.super_cnt[tile >> 6], cnt);
@@ -1383,6 +1411,7 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
         tile = ntile;
     }
     if (lane == 0 && acc_c) atomicAdd(&T.coarse[cur_c * COARSE_STRIDE], acc_c);
+    if (lane == 0) atomicAdd(&T.split[SPL_DENSE_TILES], ndone);     // real tiles, for the stats
 }
 
 // Compact every tile's candidates into T.cand in position order (one wave per

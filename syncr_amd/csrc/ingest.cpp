@@ -187,24 +187,62 @@ void free_slot_buffers(Pipe *g, Slot &s) {
 // Grow a slot's buffers to `bytes`.  The new buffers are allocated before the
 // old ones are freed (device memory first: a file too big for the GPU fails
 // there without touching host memory), so a failed allocation for one
-// oversized file leaves the slot as it was and only that file fails.
+// oversized file leaves the slot as it was and only that file fails.  When
+// old + new do not fit together, the old buffers are freed and the allocation
+// is tried once more; if that fails too the slot is refilled at batch size
+// (or left empty, which the next ensure_slot retries) and the error is that
+// file's.
+int32_t alloc_slot(Pipe *g, uint64_t want, uint8_t **dev, uint8_t **host) {
+    *dev = *host = nullptr;
+    hipError_t e = hipSetDevice(g->device);
+    if (e == hipSuccess) e = hipMalloc((void **)dev, want);
+    if (e == hipSuccess) e = hipHostMalloc((void **)host, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();                            // the failure is this call's, not sticky
+        if (*dev) (void)hipFree(*dev);
+        *dev = *host = nullptr;
+    }
+    return hip_rc(e);
+}
+
 int32_t ensure_slot(Pipe *g, Slot &s, uint64_t bytes) {
     if (bytes <= s.cap && s.host) return SYNCR_CDC_OK;
     const uint64_t want = std::max<uint64_t>(bytes, 64);
     uint8_t *dev = nullptr, *host = nullptr;
-    hipError_t e = hipSetDevice(g->device);
-    if (e == hipSuccess) e = hipMalloc((void **)&dev, want);
-    if (e == hipSuccess) e = hipHostMalloc((void **)&host, want, hipHostMallocDefault);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();                            // the failure is this call's, not sticky
-        if (dev) (void)hipFree(dev);
-        return hip_rc(e);
+    int32_t rc = alloc_slot(g, want, &dev, &host);
+    if (rc && s.host) {                                    // old + new at once did not fit
+        free_slot_buffers(g, s);
+        rc = alloc_slot(g, want, &dev, &host);
+        if (rc) {
+            const uint64_t back = std::max<uint64_t>(g->batch, 64);
+            if (back < want && alloc_slot(g, back, &dev, &host) == SYNCR_CDC_OK) {
+                s.host = host;
+                s.dev = dev;
+                s.cap = back;
+            }
+            return rc;
+        }
     }
+    if (rc) return rc;
     free_slot_buffers(g, s);
     s.host = host;
     s.dev = dev;
     s.cap = want;
     return SYNCR_CDC_OK;
+}
+
+// A slot grown for one oversized file goes back to batch size once that
+// file's batch is delivered, so the pipeline's pinned and device memory stays
+// depth x batch_bytes between oversized files.
+void shrink_slot(Pipe *g, Slot &s) {
+    if (s.cap <= std::max<uint64_t>(g->batch, 64) || s.inflight || s.used) return;
+    uint8_t *dev = nullptr, *host = nullptr;
+    free_slot_buffers(g, s);
+    if (alloc_slot(g, std::max<uint64_t>(g->batch, 64), &dev, &host) == SYNCR_CDC_OK) {
+        s.host = host;
+        s.dev = dev;
+        s.cap = std::max<uint64_t>(g->batch, 64);
+    }
 }
 
 void par_copy(Pipe *g, uint8_t *dst, const uint8_t *src, uint64_t n) {
@@ -278,6 +316,7 @@ int32_t complete(Pipe *g, Slot &s) {
     s.ccount.clear();
     s.cbuf.clear();
     s.used = 0;
+    shrink_slot(g, s);
     return SYNCR_CDC_OK;
 }
 
@@ -306,7 +345,8 @@ int32_t room(Pipe *g, uint64_t len) {
     }
     int32_t rc = complete(g, *s);
     if (rc) return rc;
-    if (!s->used && len > s->cap) return ensure_slot(g, *s, len);   // a file bigger than a batch
+    // a file bigger than a batch, or a slot left without buffers by a failed growth
+    if (!s->used && (len > s->cap || !s->host)) return ensure_slot(g, *s, std::max<uint64_t>(len, g->batch));
     return SYNCR_CDC_OK;
 }
 
@@ -467,7 +507,8 @@ int32_t pipe_submit_file(Pipe *g, const char *path, uint64_t tag) {
             while (pos < e) {
                 const ssize_t r = pread(fd, dst + pos, (size_t)(e - pos), (off_t)pos);
                 if (r < 0 && errno == EINTR) continue;
-                if (r <= 0) break;
+                if (r < 0) { perr[i] = errno ? errno : EIO; break; }   // a real error before the fault
+                if (r == 0) break;                                     // EOF before the fault
                 pos += (uint64_t)r;
             }
             if (pos == e) perr[i] = fault_err;

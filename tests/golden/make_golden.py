@@ -46,6 +46,166 @@ def case(name, recipe, bits, max_chunk, cap, note=""):
             "ends": [int(e) for e in ends], "note": note}
 
 
+# ---------------------------------------------------------------------------
+# head fix-up cases at the PRODUCTION parameters (chunk_bits 20, MAX 16 MiB,
+# read caps 2 MiB and 0).  A fresh Bup per chunk (file_operations.rs:748) means
+# the 63 positions after a chunk start s see a window zeroed before s, unlike
+# the stream-global digest G.  Random data at bits 20 has a head event once per
+# ~16 000 cuts, so the cases are built, not searched for (SURVEY App. A kinds):
+#   (a) a chunk-local hit at p in [s, s+62] -- the next cut is p+1, a head-hit
+#       cut whose own chunk starts with a fresh window again;
+#   (b) a G-hit at p in [s+1, s+62] that is NOT chunk-local -- a scan that
+#       skipped the head fix-up would cut at p+1.
+# s is a content cut (a G-hit), the 2 MiB read-boundary cut after a constant
+# prefix (production), or a forced MAX cut (ideal).  Bytes are planted by
+# solving the last two window bytes (weights 2 and 1) for the W target, as
+# benchlib/workloads.py periodic_pattern does, and checking S.
+# ---------------------------------------------------------------------------
+W_TARGET = 0x17BF        # (124992 + W) & 0xffff == 0xffff
+S_TARGET = 15            # (1984 + S) & 0xf == 0xf (1984 = 124 * 16)
+
+
+def bup_hit(window, bits=20) -> bool:
+    """Exact Bup edge test for the bytes of a window, oldest first (bytes
+    before it read as 0): s1 = 1984 + S, s2 = 124992 + W, weight = age + 1."""
+    b = np.asarray(window, np.int64)
+    S = int(b.sum())
+    W = int((np.arange(b.size, 0, -1) * b).sum())
+    dg = ((((1984 + S) & 0xFFFF) << 16) | ((124992 + W) & 0xFFFF)) & 0xFFFFFFFF
+    mask = (1 << bits) - 1
+    return (dg & mask) == mask
+
+
+def solve_tail(rng, b: np.ndarray, weights: np.ndarray, free: np.ndarray):
+    """Re-draw the bytes b[free] (not the last two) until the last two bytes
+    (weights 2, 1) can make W = W_TARGET and S = S_TARGET mod 16; returns b."""
+    for _ in range(20000):
+        b[free] = rng.integers(0, 256, free.size)
+        rest_w = int((weights[:-2] * b[:-2]).sum())
+        rest_s = int(b[:-2].sum())
+        t = (W_TARGET - rest_w) % 65536                       # 2 x1 + x0 = t, 0 <= x0, x1 < 256
+        if t > 765:
+            continue
+        for x1 in range(max(0, (t - 255 + 1) // 2), min(255, t // 2) + 1):
+            x0 = t - 2 * x1
+            if 0 <= x0 < 256 and (rest_s + x1 + x0) % 16 == S_TARGET:
+                b[-2], b[-1] = x1, x0
+                return b
+    raise RuntimeError("no solution")
+
+
+def plant_local(rng, d, s, L):
+    """(a): bytes d[s : s+L] whose chunk-local window hits at p = s+L-1 and
+    nowhere before it in the chunk."""
+    for _ in range(1000):
+        b = solve_tail(rng, np.zeros(L, np.int64), np.arange(L, 0, -1), np.arange(L - 2))
+        if all(not bup_hit(b[:k + 1]) for k in range(L - 1)) and bup_hit(b):
+            d[s:s + L] = b
+            return s + L - 1
+    raise RuntimeError("plant_local")
+
+
+def plant_global(rng, d, s, p):
+    """(b): re-draw d[s : p+1] so that the stream-global 64-byte window at p
+    hits, no chunk-local position in [s, s+62] hits, and no G-hit lies in
+    [s, p) (so only the head fix-up tells the true walk from a wrong one)."""
+    assert s + 8 <= p <= s + 62
+    for _ in range(1000):
+        w = d[p - 63:p + 1].astype(np.int64)
+        free = np.arange(64 - (p - s + 1), 62)                   # window slots of bytes s .. p-2
+        w = solve_tail(rng, w, np.arange(64, 0, -1), free)
+        d[p - 63:p + 1] = w
+        ok = bup_hit(d[p - 63:p + 1]) and not bup_hit(d[s:p + 1])
+        ok = ok and all(not bup_hit(d[s:q + 1]) for q in range(s, min(s + 63, d.size)))
+        ok = ok and all(not bup_hit(d[q - 63:q + 1]) for q in range(s, p))
+        if ok:
+            return p
+    raise RuntimeError("plant_global")
+
+
+def first_content_cut(d, cap):
+    ends = O.chunk_production(d, 20, O.MAX_CHUNK_SIZE, cap) if cap else O.chunk_ideal(d, 20, O.MAX_CHUNK_SIZE)
+    for e in ends.tolist():
+        if not (cap and e % cap == 0) and e % O.MAX_CHUNK_SIZE and e + 200 < d.size:
+            return int(e)
+    raise RuntimeError("no content cut")
+
+
+def production_head_cases():
+    out = []
+    MX = O.MAX_CHUNK_SIZE
+    rng = np.random.default_rng(4242)
+
+    def emit(name, rec, d, cap, note):
+        patch = [[int(a), d[a:b].tobytes().hex()] for a, b in spans]
+        rec = dict(rec, patch=patch)
+        c = case(name, rec, 20, MX, cap, note)
+        data = make_input(rec)
+        assert np.array_equal(data, d)
+        bad = O.chunk_no_head_fixup(data, 20, MX, cap)
+        assert not np.array_equal(np.array(c["ends"], np.uint64), bad), name + ": fix-up does not matter"
+        out.append(c)
+
+    for cap, tag in ((O.TOKIO_READ_CAP, "prod"), (0, "ideal")):
+        for k, (kind, arg) in enumerate((("a", 63), ("a", 7), ("a", 33), ("b", 62), ("b", 20), ("aa", 45),
+                                        ("ab", 50))):
+            for seed in range(9_100_000 + 1000 * k + (0 if cap else 500), 9_100_000 + 1000 * k + 1000):
+                rec = {"kind": "xorshift", "seed": seed, "n": 5 * M + 333}
+                d = make_input(rec)
+                s = first_content_cut(d, cap)
+                if kind == "b":                          # the bytes before s must leave the W target reachable
+                    try:
+                        plant_global(rng, d.copy(), s, s + arg)
+                    except RuntimeError:
+                        continue
+                break
+            spans = []
+            if kind[0] == "a":
+                p = plant_local(rng, d, s, arg)
+                spans.append((s, p + 1))
+                assert (p + 1) in (O.chunk_production(d, 20, MX, cap) if cap else O.chunk_ideal(d, 20, MX)).tolist()
+                if kind == "aa":                              # a head-hit cut followed by another
+                    p2 = plant_local(rng, d, p + 1, 29)
+                    spans.append((p + 1, p2 + 1))
+                elif kind == "ab":                            # a head-hit cut followed by kind (b)
+                    p2 = plant_global(rng, d, p + 1, p + 1 + 40)
+                    spans.append((p2 - 63, p2 + 1))
+            else:
+                p = plant_global(rng, d, s, s + arg)
+                spans.append((p - 63, p + 1))
+            emit(f"adversarial_head_b20_{tag}_content_{kind}{arg}", rec, d, cap,
+                 f"bits 20 / 16 MiB, read_cap {cap}: kind ({kind}) planted after the content cut at {s}")
+    # after the 2 MiB read-boundary cut of a constant prefix (production grid point)
+    for k, (kind, arg) in enumerate((("a", 63), ("a", 12), ("b", 62), ("b", 24))):
+        rec = {"kind": "xorshift", "seed": 9_200_000 + k, "n": 6 * M + 77, "fill": [[0, 2 * M, 0x41]]}
+        d = make_input(rec)
+        s = 2 * M
+        spans = []
+        if kind == "a":
+            p = plant_local(rng, d, s, arg)
+            spans.append((s, p + 1))
+        else:
+            p = plant_global(rng, d, s, s + arg)
+            spans.append((p - 63, p + 1))
+        emit(f"adversarial_head_b20_prod_readcap_{kind}{arg}", rec, d, O.TOKIO_READ_CAP,
+             f"bits 20 / 16 MiB / 2 MiB reads: kind ({kind}) planted after the read-boundary cut at {s}")
+    # after a forced MAX cut (ideal semantics: 16 MiB of constant bytes)
+    for k, (kind, arg) in enumerate((("a", 50), ("b", 50))):
+        rec = {"kind": "xorshift", "seed": 9_300_000 + k, "n": MX + M + 5, "fill": [[0, MX, 0x58]]}
+        d = make_input(rec)
+        s = MX
+        spans = []
+        if kind == "a":
+            p = plant_local(rng, d, s, arg)
+            spans.append((s, p + 1))
+        else:
+            p = plant_global(rng, d, s, s + arg)
+            spans.append((p - 63, p + 1))
+        emit(f"adversarial_head_b20_ideal_max_{kind}{arg}", rec, d, 0,
+             f"bits 20 / 16 MiB, ideal: kind ({kind}) planted after the MAX cut at {s}")
+    return out
+
+
 def main():
     cases = []
     PROD, IDEAL = O.TOKIO_READ_CAP, 0
@@ -102,6 +262,7 @@ def main():
                               "head fix-up changes the cuts (chunk-local != file-global in [s, s+62])"))
             found += 1
     assert found >= 4, "no adversarial head cases found"
+    cases.extend(production_head_cases())
 
     with open(os.path.join(HERE, "kat_cases.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "oracle": "oracle/bup_oracle.c",

@@ -58,6 +58,11 @@ def make_input(recipe: dict) -> np.ndarray:
         if "zero" in recipe:
             a, b = recipe["zero"]
             d[a:b] = 0
+        for a, b, byte in recipe.get("fill", []):          # constant runs (no hits: read-cap / MAX cuts)
+            d[a:b] = byte
+        for off, hx in recipe.get("patch", []):            # planted bytes (tests/golden/make_golden.py)
+            p = np.frombuffer(bytes.fromhex(hx), dtype=np.uint8)
+            d[off:off + p.size] = p
         return d
     if k == "const":
         return np.full(recipe["n"], recipe["byte"], np.uint8)

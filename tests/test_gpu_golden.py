@@ -73,3 +73,39 @@ def test_memcpy_d2d():
         finally:
             a.free()
             b.free()
+
+
+@pytest.mark.parametrize("nshards", [2, 8])
+def test_strong_shards_vs_golden(nshards):
+    """BASELINE config 4's per-rank batches (bench.py --gpus N --scaling strong:
+    zipf10k LPT-sharded per file, benchlib/workloads.py lpt_shard) through the
+    product path, one shard at a time on this GPU: every file of every shard,
+    cuts and chunk hashes, against the golden digests; the shards together are
+    exactly the 10 000 files (file_operations.rs:599-605,721-788: files are
+    independent, so sharding cannot change a file's chunks)."""
+    sizes = WL.zipf_sizes()
+    shards = WL.lpt_shard(sizes, nshards)
+    assert np.array_equal(np.sort(np.concatenate(shards)), np.arange(sizes.size))
+    biggest = max(int(sizes[s].sum()) for s in shards)
+    files = 0
+    with syncr_amd.Chunker() as ch:
+        buf = syncr_amd.DeviceBuffer(ch, biggest)
+        try:
+            for sh in shards:
+                lens = sizes[sh]
+                offs = WL.offsets_of(lens)
+                buf.gen_corpus(offs, lens, indices=sh.astype(np.uint64))
+                ch.plan(offs, lens, int(lens.sum()))
+                ch.launch(buf.ptr, hashed=True)
+                p = G.check_files("zipf10k", ch.fetch(hashed=True), sh, hashed=True)
+                assert p["files"] == sh.size and p["mismatches"] == 0, p
+                files += p["files"]
+        finally:
+            buf.free()
+    assert files == sizes.size
+
+
+def test_shard_leg_reports_every_shard():
+    r = L.shard_leg(0, steps=2, warmup=1, nshards=8)
+    assert len(r["shards"]) == 8 and r["parity"]["files"] == 10000 and r["parity"]["mismatches"] == 0, r
+    assert r["projected_value"] > 0 and all(s["scan_frac"] for s in r["shards"])

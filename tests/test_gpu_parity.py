@@ -623,3 +623,41 @@ def test_fetch_reruns_reported():
             assert ends_of(first[0]) == ends_of(again[0]) == O.chunk_production_window(data).tolist()
         finally:
             buf.free()
+
+
+def test_launches_on_alternating_streams():
+    """One handle launched on two caller streams in turn with no fetch in
+    between (include/syncr_cdc.h: a launch on another stream waits for the
+    previous launch's stream), over a periodic + constant + random batch whose
+    first fetch must re-run the launch (dense tiles not yet seen, grown
+    capacities).  Cuts and chunk hashes against the oracle."""
+    from benchlib import legs as LG
+    from benchlib import workloads as WL
+    files = LG.dense_subset_files()[:6] + [O.xorshift_bytes(4321, 9 * M + 11)]
+    lens = np.array([f.size for f in files], np.uint64)
+    offs = WL.offsets_of(lens)
+    buf_h = np.concatenate(files)
+    want = [O.chunk_production_window(f).tolist() for f in files]
+    with syncr_amd.Chunker() as ch, syncr_amd.Chunker() as a1, syncr_amd.Chunker() as a2:
+        streams = (a1.stream, a2.stream)
+        assert streams[0] and streams[1] and streams[0] != streams[1]
+        d = syncr_amd.DeviceBuffer(ch, buf_h.size)
+        try:
+            d.upload(buf_h)
+            ch.plan(offs, lens, buf_h.size)
+            for rnd in range(2):
+                for k in range(7):
+                    ch.launch(d.ptr, stream=streams[k % 2], hashed=(k % 3 == 0))
+                got = ch.fetch(hashed=True)           # the last launch (k = 6) was hashed
+                if rnd == 0:
+                    assert ch.fetch_reruns() > 0      # the re-run happened inside fetch
+                for g, w, f in zip(got, want, files):
+                    assert ends_of(g) == w
+                    if g.size:
+                        h = O.blake3_batch(f, g["offset"].astype(np.uint64), g["len"].astype(np.uint64), nthreads=8)
+                        assert np.array_equal(g["hash"], h)
+                # the handle's own stream after the caller's
+                ch.launch(d.ptr)
+                assert all(ends_of(g) == w for g, w in zip(ch.fetch(), want))
+        finally:
+            d.free()

@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Where a scan launch's time goes (development library, SYNCR_CDC_TRACE=1).
+
+The dev scan kernel stamps wall_clock64 (100 MHz) per wave: entry, first tile
+landed, exit, tiles rolled (cdc_internal.h DBG_SCAN), and every tile's landing
+for the first DBG_TILE_W waves (DBG_TILE).  Printed per workload, for the last
+of W+K back-to-back launches (and for the first launch after a host gap):
+
+  entry spread     last wave's entry after the first (dispatch ramp)
+  first land       a wave's first tile landing after its entry (DMA ramp)
+  ends             wave exits (min / p10 / median / p90 / max) from the first entry
+  tile             per-tile time of the sampled waves (steady roll + wait)
+  resolve start    the resolve kernel's first stamp after the last scan wave's exit
+                   (dense pass, compaction, fix-ups and the launch gaps between)
+
+    python tools/scan_timeline.py [--workload uniform1k|shard8|zipf10k] [--shard R]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import syncr_amd  # noqa: E402
+from benchlib import workloads as WL  # noqa: E402
+
+syncr_amd.use_dev_library()
+
+DBG_REC, DBG_NREC, DBG_NFW = 256, 1024, 1024
+DBG_FW = DBG_REC + 2 * DBG_NREC
+DBG_SCAN, DBG_SCAN_N = DBG_FW + DBG_NFW, 4096
+DBG_TILE, DBG_TILE_W, DBG_TILE_N = DBG_SCAN + 4 * DBG_SCAN_N, 16, 128
+WORDS = DBG_TILE + DBG_TILE_W * DBG_TILE_N
+
+
+def table(name, shard):
+    sizes = WL.zipf_sizes()
+    if name == "uniform1k":
+        lens = np.full(1024, 1 << 20, np.uint64)
+        return lens, np.arange(1024, dtype=np.uint64)
+    if name == "shard8":
+        sh = WL.lpt_shard(sizes, 8)[shard]
+        return sizes[sh], sh.astype(np.uint64)
+    return sizes, np.arange(sizes.size, dtype=np.uint64)
+
+
+def summarize(d, grid):
+    sc = d[DBG_SCAN:DBG_SCAN + 4 * DBG_SCAN_N].reshape(-1, 4)[:grid].astype(np.int64)
+    have = sc[:, 0] > 0
+    sc = sc[have]
+    t0 = sc[:, 0].min()
+    us = lambda v: (v - t0) / 100.0                                  # noqa: E731
+    ends = us(sc[:, 2])
+    tiles = d[DBG_TILE:DBG_TILE + DBG_TILE_W * DBG_TILE_N].reshape(DBG_TILE_W, DBG_TILE_N).astype(np.int64)
+    per_tile = []
+    for w in range(DBG_TILE_W):
+        t = tiles[w][tiles[w] > 0]
+        if t.size > 2:
+            per_tile.extend(np.diff(t).tolist())
+    per_tile = np.array(per_tile, np.float64) / 100.0
+    res = int(d[0])
+    out = {
+        "waves": int(have.sum()),
+        "entry_spread_us": round(float(us(sc[:, 0]).max()), 2),
+        "first_land_us": {"median": round(float(np.median((sc[:, 1] - sc[:, 0]) / 100.0)), 2),
+                          "max": round(float(((sc[:, 1] - sc[:, 0]) / 100.0).max()), 2)},
+        "ends_us": {q: round(float(np.percentile(ends, p)), 2) for q, p in
+                    (("min", 0), ("p10", 10), ("median", 50), ("p90", 90), ("max", 100))},
+        "tiles_per_wave": {"min": int(sc[:, 3].min()), "max": int(sc[:, 3].max()),
+                           "mean": round(float(sc[:, 3].mean()), 2)},
+        "tile_us": ({"median": round(float(np.median(per_tile)), 3), "p10": round(float(np.percentile(per_tile, 10)), 3),
+                     "p90": round(float(np.percentile(per_tile, 90)), 3), "first": round(float(per_tile[0]), 3)}
+                    if per_tile.size else None),
+        "resolve_start_after_scan_us": round((res - sc[:, 2].max()) / 100.0, 2) if res else None,
+    }
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="uniform1k", choices=["uniform1k", "shard8", "zipf10k"])
+    ap.add_argument("--shard", type=int, default=0)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    os.environ["SYNCR_CDC_TRACE"] = "1"
+    lens, idx = table(args.workload, args.shard)
+    offs = WL.offsets_of(lens)
+    span = int(lens.sum())
+    L = syncr_amd.library()
+    L.syncr_cdc_dev_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+    L.syncr_cdc_dev_trace.restype = ctypes.c_int32
+    with syncr_amd.Chunker() as c:
+        buf = syncr_amd.DeviceBuffer(c, span)
+        try:
+            buf.gen_corpus(offs, lens, indices=idx)
+            c.plan(offs, lens, span)
+            info = c.info()
+            grid = min(info["scan_grid"], (span + info["tile_bytes"] - 1) // info["tile_bytes"])
+            c.launch(buf.ptr)
+            c.fetch()
+            d = np.zeros(WORDS, np.uint64)
+            c.launch(buf.ptr)                                       # the first launch after a host gap
+            assert L.syncr_cdc_dev_trace(c.handle, d.ctypes.data, WORDS) == 0
+            first = summarize(d, grid)
+            for _ in range(args.warmup + args.steps):
+                c.launch(buf.ptr)
+            assert L.syncr_cdc_dev_trace(c.handle, d.ctypes.data, WORDS) == 0
+            last = summarize(d, grid)
+        finally:
+            buf.free()
+    print(json.dumps({"workload": args.workload, "shard": args.shard if args.workload == "shard8" else None,
+                      "files": int(lens.size), "bytes": span, "scan_grid": grid, "tile_bytes": info["tile_bytes"],
+                      "first_after_gap": first, f"last_of_{args.warmup + args.steps}": last}))
+
+
+if __name__ == "__main__":
+    main()
