@@ -169,7 +169,7 @@ __device__ __forceinline__ void window_state(const uint32_t (&A)[(HALO + RUN) / 
 // bytes still in registers) and hands it to the side slots.  (A branch per
 // group cost 4 more VALU per group to materialise the flags and split the
 // run into basic blocks the scheduler could not interleave across.)
-template <int RUN, bool ROLL2 = false>
+template <int RUN, bool ROLL2 = false, bool NOWARM = false>
 __device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
                                           const uint32_t (&B)[(HALO + RUN) / 4], const KParams &P,
                                           int lane, bool recA, bool recB, uint32_t *dcount,
@@ -177,7 +177,12 @@ __device__ __forceinline__ void roll_fast(const uint32_t (&A)[(HALO + RUN) / 4],
     constexpr int NG = RUN / 16;
     uint32_t S;
     u16x2 Tv;
-    window_state<RUN>(A, B, P, 0, S, Tv);
+    if constexpr (NOWARM) {                 // development timing ablation: no closed-form warm-up
+        S = 0u;
+        Tv = as_u16x2(P.kk);
+    } else {
+        window_state<RUN>(A, B, P, 0, S, Tv);
+    }
     const uint32_t want = (recA ? 1u : 0u) | (recB ? 2u : 0u);
     bool zg[NG];
     bool anyz = false;
@@ -513,6 +518,11 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             const uint4 *lb = (const uint4 *)(wl + (lane + 64) * RUN);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
+                if ((MODE & 512) != 0 && q < HALO / 16) {         // development timing ablation: no halo
+                    A[4 * q + 0] = A[4 * q + 1] = A[4 * q + 2] = A[4 * q + 3] = 0u;
+                    B[4 * q + 0] = B[4 * q + 1] = B[4 * q + 2] = B[4 * q + 3] = 0u;
+                    continue;
+                }
                 const uint4 a = la[q], b = lb[q];
                 A[4 * q + 0] = a.x; A[4 * q + 1] = a.y; A[4 * q + 2] = a.z; A[4 * q + 3] = a.w;
                 B[4 * q + 0] = b.x; B[4 * q + 1] = b.y; B[4 * q + 2] = b.z; B[4 * q + 3] = b.w;
@@ -533,7 +543,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 #ifdef SYNCR_CDC_DEV
         if constexpr ((MODE & 64) != 0) roll_branchy<RUN>(A, B, P, lane, dcount, dslots); else
 #endif
-        roll_fast<RUN, (MODE & 16) != 0>(A, B, P, lane, true, true, dcount, dslots);
+        roll_fast<RUN, (MODE & 16) != 0, (MODE & 256) != 0>(A, B, P, lane, true, true, dcount, dslots);
         if constexpr ((MODE & 3) == 2) continue;                          // diagnostics: rolling only
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -551,8 +561,13 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     }
 #ifdef SYNCR_CDC_DEV
     if (stamp) {
+        // where the wave ran: HW_ID (wave, SIMD, CU, SH, SE) and the XCC id
+        uint32_t hwid, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
+                     : "=s"(hwid), "=s"(xcc));
         SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 2, wall_clock64());
-        SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 3, (uint64_t)ntile_done);
+        SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 3,
+                   (uint64_t)ntile_done | ((uint64_t)hwid << 32) | ((uint64_t)(xcc & 0xf) << 28));
     }
 #endif
 }
@@ -2902,6 +2917,11 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 12u)                                        // timing only: no closed-form warm-up
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 13u)                                        // timing only: no warm-up, no halo bytes
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256 | 512>), dim3(grid), dim3(64), lds, s, d,
+                           p, t);
     else if (p.ablate == 7u)                                         // A/B: product + 3 waves per SIMD hint
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, d, p,
                            t);

@@ -53,6 +53,14 @@ def summarize(d, grid):
     sc = d[DBG_SCAN:DBG_SCAN + 4 * DBG_SCAN_N].reshape(-1, 4)[:grid].astype(np.int64)
     have = sc[:, 0] > 0
     sc = sc[have]
+    meta = sc[:, 3].copy()
+    sc[:, 3] = meta & 0x0FFFFFFF                                    # tiles rolled
+    xcc = (meta >> 28) & 0xF
+    hw = (meta >> 32) & 0xFFFFFFFF
+    simd = (hw >> 4) & 3
+    cu = (hw >> 8) & 0xF
+    sh = (hw >> 12) & 1
+    se = (hw >> 13) & 7
     t0 = sc[:, 0].min()
     us = lambda v: (v - t0) / 100.0                                  # noqa: E731
     ends = us(sc[:, 2])
@@ -78,6 +86,24 @@ def summarize(d, grid):
                     if per_tile.size else None),
         "resolve_start_after_scan_us": round((res - sc[:, 2].max()) / 100.0, 2) if res else None,
     }
+    # per-wave rate (tiles per us of the wave's life) by placement: which waves are slow?
+    rate = sc[:, 3] / np.maximum((sc[:, 2] - sc[:, 0]) / 100.0, 1e-3)
+    def by(key, n):
+        return {int(k): [round(float(rate[key == k].mean()), 4), int((key == k).sum())] for k in range(n)
+                if (key == k).any()}
+    out["rate_tiles_per_us"] = {"all": [round(float(rate.mean()), 4), round(float(rate.min()), 4),
+                                        round(float(rate.max()), 4)],
+                                "by_xcc": by(xcc, 8), "by_simd": by(simd, 4), "by_se": by(se, 8),
+                                "by_sh": by(sh, 2), "by_cu": by(cu, 16)}
+    # waves per (xcc, se, sh, cu, simd) slot: co-residency of the slow ones
+    slot = (((xcc * 8 + se) * 2 + sh) * 16 + cu) * 4 + simd
+    _, cnt = np.unique(slot, return_counts=True)
+    out["waves_per_simd_hist"] = {int(k): int((cnt == k).sum()) for k in np.unique(cnt)}
+    cu_key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    _, ccnt = np.unique(cu_key, return_counts=True)
+    out["waves_per_cu_hist"] = {int(k): int((ccnt == k).sum()) for k in np.unique(ccnt)}
+    slow = rate < np.percentile(rate, 10)
+    out["slowest10pct_by_xcc"] = {int(k): int((xcc[slow] == k).sum()) for k in range(8)}
     return out
 
 
