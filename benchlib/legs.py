@@ -440,6 +440,7 @@ def ingest_leg(host: np.ndarray, offs, lens, idx, device: int, reps: int = 2, mu
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
         st = g.stats()
+        stages = g.timing()
     got = [res[i][1] for i in range(len(files))]
     out.update({"value": round(span / best / 2**30, 3), "unit": "GiB/s", "seconds": round(best, 4),
                 "bytes": span, "files": len(files), "batches_per_pass": st["batches"] // reps,
@@ -447,6 +448,11 @@ def ingest_leg(host: np.ndarray, offs, lens, idx, device: int, reps: int = 2, mu
                         "256 MiB batches, depth 3) -> hipMemcpyAsync H2D -> chunk + BLAKE3 -> per-file "
                         "ChunkInfo callbacks; best of %d passes" % reps,
                 "status_nonzero": int(sum(res[i][0] != 0 for i in range(len(files)))),
+                "host_stage_seconds": {k: round(v / reps, 4) for k, v in stages.items()},
+                "host_stage_note": ("syncr_ingest_timing per pass: copy (pageable -> pinned staging, %d threads), "
+                                    "seal (plan + H2D/kernel enqueue), wait (for a batch's results: H2D + kernels + "
+                                    "D2H still running), deliver; all on the caller's thread, so copy + seal + wait + "
+                                    "deliver ~= the pass: wait ~ 0 means the host side bounds the rate" % 16),
                 "parity": G.check_files("zipf10k", got, idx, hashed=True)})
     nm = min(multi_files, len(files))
     res.clear()
@@ -499,6 +505,7 @@ def ingest_files_leg(host: np.ndarray, offs, lens, idx, device: int, gib: float 
                 g.flush()
                 dt = time.perf_counter() - t0
                 best = dt if best is None else min(best, dt)
+            stages = g.timing()
     finally:
         shutil.rmtree(d, ignore_errors=True)
     got = [res[k][1] for k in range(len(take))]
@@ -508,6 +515,7 @@ def ingest_files_leg(host: np.ndarray, offs, lens, idx, device: int, gib: float 
                     "into pinned staging, 16 threads) -> H2D -> chunk + BLAKE3 -> per-file ChunkInfo; best of %d "
                     "passes" % reps,
             "status_nonzero": int(sum(res[k][0] != 0 for k in range(len(take)))),
+            "host_stage_seconds": {k: round(v / reps, 4) for k, v in stages.items()},
             "parity": G.check_files("zipf10k", got, idx[np.array(take, np.int64)], hashed=True)}
 
 

@@ -222,6 +222,13 @@ int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4);
 /* per sub-pipeline k: stats[4k..4k+3] = [device, files, bytes, batches];
  * SYNCR_CDC_ERANGE if n < 4 * ndevices */
 int32_t syncr_ingest_device_stats(const syncr_ingest *g, uint64_t *stats, uint32_t n);
+/* Host seconds spent so far, summed over sub-pipelines, per stage: sec[0] copying
+ * submitted bytes into pinned staging, [1] reading files into it (submit_file),
+ * [2] sealing batches (plan + H2D and kernel enqueue), [3] waiting for a batch's
+ * results (fetch: the device side -- H2D, kernels, D2H -- not yet done), [4]
+ * per-file delivery (callbacks).  Diagnostics of where an end-to-end run is
+ * bound; the first n entries are written. */
+int32_t syncr_ingest_timing(const syncr_ingest *g, double *sec, uint32_t n);
 /* Fault injection (tests of the read-error contract, file_operations.rs:
  * 727-744, 776-782): every later submit_file reads only the bytes before file
  * offset `offset`; the read that would cross it fails with errno `err`

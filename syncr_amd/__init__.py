@@ -56,7 +56,7 @@ EXPORTED_SYMBOLS = (
     "syncr_cache_open", "syncr_cache_get", "syncr_cache_put", "syncr_cache_sync", "syncr_cache_stats",
     "syncr_cache_close", "syncr_ingest_set_cache", "syncr_ingest_cache_hits",
     "syncr_ingest_open_multi", "syncr_ingest_device_stats", "syncr_cache_get_params",
-    "syncr_ingest_set_read_fault", "syncr_cdc_fetch_reruns",
+    "syncr_ingest_set_read_fault", "syncr_cdc_fetch_reruns", "syncr_ingest_timing",
 )
 
 ABI_VERSION = 3
@@ -172,6 +172,7 @@ def library():
                                          _INGEST_CB, _vp, ctypes.POINTER(_vp)], _i32),
             "syncr_ingest_device_stats": ([_vp, _pu64, _u32], _i32),
             "syncr_ingest_set_read_fault": ([_vp, _u64, _i32], _i32),
+            "syncr_ingest_timing": ([_vp, ctypes.POINTER(ctypes.c_double), _u32], _i32),
             "syncr_cache_get": ([_vp, ctypes.c_char_p, _u32, _u64, _vp, _u64, _pu64], _i32),
             "syncr_cache_put": ([_vp, ctypes.c_char_p, _u32, _u64, _vp, _u64], _i32),
             "syncr_cache_sync": ([_vp], _i32),
@@ -584,6 +585,12 @@ class Ingest:
         shrank). offset None turns it off."""
         off = 2**64 - 1 if offset is None else offset
         _check(library().syncr_ingest_set_read_fault(self._h, off, err), "syncr_ingest_set_read_fault")
+
+    def timing(self) -> dict:
+        """Host seconds per pipeline stage so far (syncr_ingest_timing)."""
+        t = (ctypes.c_double * 5)()
+        _check(library().syncr_ingest_timing(self._h, t, 5), "syncr_ingest_timing")
+        return dict(zip(("copy", "read", "seal", "wait", "deliver"), (round(x, 6) for x in t)))
 
     def device_stats(self) -> list[dict]:
         """Per sub-pipeline: device, files, bytes, batches."""

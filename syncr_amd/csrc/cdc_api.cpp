@@ -197,7 +197,8 @@ size_t coarse_offset(const syncr_cdc *h) { return (16 + (size_t)h->nwords * 12 +
 size_t split_ctr_offset(const syncr_cdc *h) {
     return coarse_offset(h) + (size_t)ncoarse(h) * COARSE_STRIDE * 4;
 }
-size_t zeroed_bytes(const syncr_cdc *h) { return split_ctr_offset(h) + SPL_WORDS * 4; }
+size_t sched_offset(const syncr_cdc *h) { return (split_ctr_offset(h) + SPL_WORDS * 4 + 127) & ~size_t(127); }
+size_t zeroed_bytes(const syncr_cdc *h) { return sched_offset(h) + (size_t)SCHED_REGIONS * COARSE_STRIDE * 4; }
 size_t zstride(const syncr_cdc *h) { return (zeroed_bytes(h) + 255) & ~size_t(255); }
 uint8_t *zblock(const syncr_cdc *h, uint32_t par) { return h->zeroed.as<uint8_t>() + par * zstride(h); }
 
@@ -250,6 +251,7 @@ Tables make_tables(syncr_cdc *h) {
     t.runs = h->runs.as<RunJob>();
     t.runs_cap = (h->n_elig && h->seg_cap) ? h->runs_cap : 0u;     // deferral only when the copy launch runs
     t.split = reinterpret_cast<uint32_t *>(zb + split_ctr_offset(h));
+    t.sched = reinterpret_cast<uint32_t *>(zb + sched_offset(h));
     t.znext = reinterpret_cast<uint4 *>(zblock(h, h->zpar ^ 1u));
     t.znext_vec = (uint32_t)(zstride(h) / 16);
     t.hzero = nullptr;

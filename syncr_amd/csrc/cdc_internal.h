@@ -20,6 +20,11 @@ constexpr uint32_t DENSE_BIT = 0x80000000u;
 // counters, and counters sharing a line serialise in one L2 channel.
 constexpr uint32_t COARSE_STRIDE = 32;
 constexpr uint64_t NONE = ~0ull;
+// The scan's fine schedule (cdc_scan_kernel MODE bit 1024): the tiles are cut
+// into SCHED_REGIONS contiguous regions, each with its own counter; a wave takes
+// one tile at a time from its region and moves on to the next region once its
+// own is exhausted.
+constexpr uint32_t SCHED_REGIONS = 16;
 constexpr int DEFAULT_RUN = 144;
 
 // MFMA scan (cdc_scan_mfma_kernel): a wave tile is 32 streams x NB blocks of
@@ -210,6 +215,8 @@ struct Tables {
     uint32_t *split;               // [SPL_WORDS] counters                    (zeroed per launch)
     uint32_t dense_off;            // 1: no dense pass this launch (the handle has not seen a dense tile);
                                    //   the compaction counts dense tiles as empty and fetch re-runs if any
+    uint32_t *sched;               // [SCHED_REGIONS * COARSE_STRIDE] per-region tile counters of the scan's
+                                   //   fine schedule, one per 128-byte line (zeroed per launch)
     RunJob *runs;                  // [runs_cap] deferred runs (only while split workers run)
     uint32_t runs_cap;
     uint32_t epoch;                // this launch's id (!= 0, unique in the process): SplitSeg::ready

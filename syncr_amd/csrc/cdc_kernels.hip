@@ -468,7 +468,15 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     // index; later ones come from a counter (CTR_CANDS_HI is free until the
     // prefix kernel writes it), grabbed at a group's first tile so the atomic
     // completes under the roll.
-    constexpr bool DYN = (MODE & 8) != 0;
+    constexpr bool DYN = (MODE & 8) != 0 && (MODE & 1024) == 0;
+    // MODE bit 10 (FINE): one tile per grab from per-region counters (T.sched):
+    // wave b starts in region b % NR at the region's tile b / NR, then takes the
+    // region's next free tile (the grab for the tile after next is issued when
+    // next's DMA is, so it returns under a whole roll); an exhausted region sends
+    // the wave to the next region (at most NR switches).  Waves run at different
+    // speeds (a factor of ~2 between placements, tools/scan_timeline.py), so
+    // every wave finishes within about one tile of the others.
+    constexpr bool FINE = (MODE & 1024) != 0;
     // zipf10k A/B (same process): groups of 4 -> 2.07 ms (one counter serialises ~69 M grabs/s), 8 -> 1.601,
     // 16 -> 1.635, 24 -> 1.651, 32 -> 1.633, 64 -> 1.669, static stride 1.657-1.694
     constexpr uint32_t DG = 8;
@@ -478,8 +486,37 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     const int64_t span = (int64_t)T.span;
     const bool stamp = blockIdx.x < (uint32_t)DBG_SCAN_N;
     if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x, wall_clock64());
+    // fine schedule: regions [rb(r), rb(r+1)); the first ns(r) tiles of a region
+    // are the static first tiles of its waves, the rest are handed out by its counter
+    const uint32_t NR = stride < SCHED_REGIONS ? stride : SCHED_REGIONS;
+    auto rb = [&](uint32_t r) { return (uint32_t)(((uint64_t)r * T.ntiles) / NR); };
+    auto ns = [&](uint32_t r) {
+        const uint32_t nw = (stride - r + NR - 1) / NR, sz = rb(r + 1) - rb(r);
+        return nw < sz ? nw : sz;
+    };
+    uint32_t reg = blockIdx.x % NR, switches = 0;
+    // the next free tile of another region, waited for here (only once a region is exhausted)
+    auto grab_elsewhere = [&]() -> uint32_t {
+        while (++switches < NR) {
+            reg = reg + 1 == NR ? 0u : reg + 1;
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(&T.sched[reg * COARSE_STRIDE], 1u);
+            wait_vmcnt<0>();
+            const uint32_t t = rb(reg) + ns(reg) + (uint32_t)__builtin_amdgcn_readfirstlane(v);
+            if (t < rb(reg + 1)) return t;
+        }
+        return 0xffffffffu;
+    };
+    if constexpr (FINE) {
+        tile = rb(reg) + blockIdx.x / NR;
+        if (tile >= rb(reg + 1)) tile = grab_elsewhere();
+        if (tile >= T.ntiles) return;
+    }
     issue_tile<RUN, (MODE & 4) != 0>(data, T.span, tile, lds0, lane);
     uint32_t gj = 0, pend = 0;
+    if constexpr (FINE) {
+        if (lane == 0) pend = atomicAdd(&T.sched[reg * COARSE_STRIDE], 1u);     // the tile after this one
+    }
     DenseSlots dslots_alloc;
 #ifdef SYNCR_CDC_DEV
     uint32_t ntile_done = 0;
@@ -500,12 +537,17 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 next = gbase(stride + (uint32_t)__builtin_amdgcn_readfirstlane(pend));
                 gjn = 0;
             }
-        } else {
+        } else if constexpr (!FINE) {
             next = tile + stride;
         }
         const int64_t t0 = (int64_t)tile * TILE;
         if (lane == 0) { *wcount = 0u; *dcount = 0u; }
         wait_vmcnt<0>();                                             // this tile has landed
+        if constexpr (FINE) {                                        // (and the pending grab has returned)
+            next = rb(reg) + ns(reg) + (uint32_t)__builtin_amdgcn_readfirstlane(pend);
+            if (next >= rb(reg + 1)) next = grab_elsewhere();
+            if (next > T.ntiles) next = T.ntiles;
+        }
 #ifdef SYNCR_CDC_DEV
         if (stamp && ntile_done == 0) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 1, wall_clock64());
         if (blockIdx.x < (uint32_t)DBG_TILE_W && ntile_done < (uint32_t)DBG_TILE_N)
@@ -533,6 +575,9 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         if constexpr (DYN) {
             if (gj == 0 && !grabbed && lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
             gj = gjn;
+        }
+        if constexpr (FINE) {
+            if (next < T.ntiles && lane == 0) pend = atomicAdd(&T.sched[reg * COARSE_STRIDE], 1u);
         }
         if constexpr ((MODE & 3) == 1) {                                   // diagnostics: staging only
 #pragma unroll
@@ -685,7 +730,15 @@ void cdc_scan3_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     constexpr int NQ = (HALO + RUN) / 16;
     constexpr int NG = RUN / 16;
     constexpr bool NT = (MODE & 4) != 0;
-    constexpr bool DYN = (MODE & 8) != 0;
+    constexpr bool DYN = (MODE & 8) != 0 && (MODE & 1024) == 0;
+    // MODE bit 10 (FINE): one tile per grab from per-region counters (T.sched):
+    // wave b starts in region b % NR at the region's tile b / NR, then takes the
+    // region's next free tile (the grab for the tile after next is issued when
+    // next's DMA is, so it returns under a whole roll); an exhausted region sends
+    // the wave to the next region (at most NR switches).  Waves run at different
+    // speeds (a factor of ~2 between placements, tools/scan_timeline.py), so
+    // every wave finishes within about one tile of the others.
+    constexpr bool FINE = (MODE & 1024) != 0;
     const int lane = threadIdx.x;
     uint8_t *wl = smem;
     uint32_t *drel = (uint32_t *)(smem + buf_bytes(RUN));
@@ -2917,6 +2970,8 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 14u)                                        // A/B: fine schedule (exact)
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 4 | 16 | 1024>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 12u)                                        // timing only: no closed-form warm-up
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 13u)                                        // timing only: no warm-up, no halo bytes

@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -168,6 +169,25 @@ struct Pipe {
     // offset with fault_err (0 = EOF there, as if the file shrank)
     std::atomic<uint64_t> fault_off{UINT64_MAX};
     std::atomic<int32_t> fault_err{0};
+    // host time (ns) spent in each stage (syncr_ingest_timing): copies into
+    // pinned staging, file reads into it, seal (plan + H2D and kernel enqueue),
+    // waiting for a batch's results (fetch), per-file delivery
+    std::atomic<uint64_t> tns[5] = {{0}, {0}, {0}, {0}, {0}};
+};
+
+enum { T_COPY = 0, T_READ = 1, T_SEAL = 2, T_WAIT = 3, T_DELIVER = 4 };
+
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// adds the time from construction to destruction to one stage counter
+struct StageTimer {
+    std::atomic<uint64_t> &acc;
+    uint64_t t0;
+    explicit StageTimer(std::atomic<uint64_t> &a) : acc(a), t0(now_ns()) {}
+    ~StageTimer() { acc += now_ns() - t0; }
 };
 
 int32_t hip_rc(hipError_t e) {
@@ -264,15 +284,20 @@ int32_t complete(Pipe *g, Slot &s) {
     const uint32_t nf = (uint32_t)s.off.size();
     s.counts.assign(std::max<uint32_t>(nf, 1), 0);
     uint64_t n = 0;
-    int32_t rc = syncr_cdc_fetch_hashed(s.h, nullptr, 0, s.counts.data(), &n);
-    if (rc == SYNCR_CDC_ERANGE || rc == SYNCR_CDC_OK) {
-        s.out.resize(std::max<uint64_t>(n, 1));
-        rc = syncr_cdc_fetch_hashed(s.h, s.out.data(), s.out.size(), s.counts.data(), &n);
+    int32_t rc;
+    {
+        StageTimer tw(g->tns[T_WAIT]);
+        rc = syncr_cdc_fetch_hashed(s.h, nullptr, 0, s.counts.data(), &n);
+        if (rc == SYNCR_CDC_ERANGE || rc == SYNCR_CDC_OK) {
+            s.out.resize(std::max<uint64_t>(n, 1));
+            rc = syncr_cdc_fetch_hashed(s.h, s.out.data(), s.out.size(), s.counts.data(), &n);
+        }
     }
     if (rc) {
         g->error = rc;
         return rc;
     }
+    StageTimer td(g->tns[T_DELIVER]);
     uint64_t o = 0;
     std::vector<uint64_t> ends;
     for (uint32_t i = 0; i < nf; i++) {
@@ -322,6 +347,7 @@ int32_t complete(Pipe *g, Slot &s) {
 
 int32_t seal(Pipe *g, Slot &s) {
     if (s.off.empty()) return SYNCR_CDC_OK;
+    StageTimer ts(g->tns[T_SEAL]);
     int32_t rc = syncr_cdc_plan(s.h, s.off.data(), s.len.data(), (uint32_t)s.off.size(), s.used);
     if (rc) return g->error = rc;
     void *stream = syncr_cdc_stream(s.h);
@@ -439,7 +465,10 @@ int32_t pipe_submit(Pipe *g, const uint8_t *data, uint64_t len, uint64_t tag) {
     uint8_t *dst = nullptr;
     int32_t rc = pipe_reserve(g, len, &dst);
     if (rc) return rc;
-    par_copy(g, dst, data, len);
+    {
+        StageTimer tc(g->tns[T_COPY]);
+        par_copy(g, dst, data, len);
+    }
     return pipe_commit(g, tag);
 }
 
@@ -524,8 +553,11 @@ int32_t pipe_submit_file(Pipe *g, const char *path, uint64_t tag) {
         }
         got[i] = pos - a;
     };
-    if (len > PAR_COPY && g->pool) g->pool->parallel(pieces, read_piece);
-    else for (unsigned i = 0; i < pieces; i++) read_piece(i);
+    {
+        StageTimer tr(g->tns[T_READ]);
+        if (len > PAR_COPY && g->pool) g->pool->parallel(pieces, read_piece);
+        else for (unsigned i = 0; i < pieces; i++) read_piece(i);
+    }
     close(fd);
     // the prefix read without a gap: the reference reads sequentially and
     // stops at the first failure or EOF
@@ -926,6 +958,17 @@ int32_t syncr_ingest_device_stats(const syncr_ingest *g, uint64_t *stats, uint32
         stats[4 * k + 1] = p->stats[0].load();           // files handled by this device
         stats[4 * k + 2] = p->stats[1].load();           // bytes
         stats[4 * k + 3] = p->stats[2].load();           // batches
+    }
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_ingest_timing(const syncr_ingest *g, double *sec, uint32_t n) {
+    if (!g || (n && !sec)) return SYNCR_CDC_EINVAL;
+    for (uint32_t k = 0; k < n; k++) {
+        uint64_t t = 0;
+        if (k < 5)
+            for (const Pipe *p : g->pipes) t += p->tns[k].load();
+        sec[k] = (double)t * 1e-9;
     }
     return SYNCR_CDC_OK;
 }
