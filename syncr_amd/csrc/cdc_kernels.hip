@@ -446,15 +446,32 @@ __host__ __device__ constexpr bool scan_dynamic(uint32_t ntiles, uint32_t grid) 
 
 // MODE bit 5: ask for 3 waves per SIMD (VGPRs <= 168; development A/B only).
 // MODE bit 6: the round-2 roll with a branch per group (development A/B only)
-template <int RUN, int MODE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((MODE & 32) ? 3 : 1)))
+// WPB > 1 (the CU schedule, MODE bit 11): one workgroup of WPB waves per CU,
+// each wave with its own LDS region as above; the CU takes the tiles
+// blockIdx.x + k * gridDim.x (every CU sweeps the batch in step with the
+// others) and its waves take the next k from one LDS counter, a tile at a time.
+// The two waves of a SIMD do not run at the same speed (the arbiter favours
+// one: per-wave rates differ up to 2x with the same mean on every XCC, SE, CU
+// and SIMD, tools/scan_timeline.py), so a static share per wave ends with the
+// slow waves alone on their SIMDs; an LDS counter balances them for ~100
+// cycles per tile, with no global atomics.
+template <int RUN, int MODE, int WPB = 1>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu((MODE & 32) ? 3 : 1)))
 void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int BUF = buf_bytes(RUN);
     constexpr int TILE = tile_bytes(RUN);
     constexpr int NQ = (HALO + RUN) / 16;
-    const int lane = threadIdx.x;
-    uint8_t *wl = smem;
+    constexpr bool CUS = WPB > 1;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = CUS ? (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
+    uint8_t *wl = smem + wid * (uint32_t)lds_wave_bytes(RUN);
+    __attribute__((address_space(3))) uint32_t *cu_next =
+        (__attribute__((address_space(3))) uint32_t *)(smem + WPB * lds_wave_bytes(RUN));
+    if constexpr (CUS) {
+        if (threadIdx.x == 0) *cu_next = (uint32_t)WPB;          // k = 0 .. WPB-1 are the waves' first tiles
+        __syncthreads();
+    }
     DirtySlot *dslots = (DirtySlot *)(smem + BUF);
     uint32_t *wlist = (uint32_t *)(smem + BUF + DIRTYCAP * sizeof(DirtySlot));
     uint32_t *wcount = wlist + LISTCAP;
@@ -481,11 +498,12 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     // 16 -> 1.635, 24 -> 1.651, 32 -> 1.633, 64 -> 1.669, static stride 1.657-1.694
     constexpr uint32_t DG = 8;
     auto gbase = [&](uint32_t k) { return (k / stride) * stride * DG + (k % stride); };
-    uint32_t tile = blockIdx.x;
+    uint32_t tile = CUS ? blockIdx.x + wid * stride : blockIdx.x;
     if (tile >= T.ntiles) return;
     const int64_t span = (int64_t)T.span;
-    const bool stamp = blockIdx.x < (uint32_t)DBG_SCAN_N;
-    if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x, wall_clock64());
+    const uint32_t wslot = blockIdx.x * WPB + wid;                 // timeline slot of this wave
+    const bool stamp = wslot < (uint32_t)DBG_SCAN_N;
+    if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * wslot, wall_clock64());
     // fine schedule: regions [rb(r), rb(r+1)); the first ns(r) tiles of a region
     // are the static first tiles of its waves, the rest are handed out by its counter
     const uint32_t NR = stride < SCHED_REGIONS ? stride : SCHED_REGIONS;
@@ -537,21 +555,25 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 next = gbase(stride + (uint32_t)__builtin_amdgcn_readfirstlane(pend));
                 gjn = 0;
             }
-        } else if constexpr (!FINE) {
+        } else if constexpr (!FINE && !CUS) {
             next = tile + stride;
         }
         const int64_t t0 = (int64_t)tile * TILE;
         if (lane == 0) { *wcount = 0u; *dcount = 0u; }
         wait_vmcnt<0>();                                             // this tile has landed
+        uint32_t nk = 0;
+        if constexpr (CUS) {                                         // the CU's next tile (read after the runs)
+            if (lane == 0) nk = __hip_atomic_fetch_add(cu_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         if constexpr (FINE) {                                        // (and the pending grab has returned)
             next = rb(reg) + ns(reg) + (uint32_t)__builtin_amdgcn_readfirstlane(pend);
             if (next >= rb(reg + 1)) next = grab_elsewhere();
             if (next > T.ntiles) next = T.ntiles;
         }
 #ifdef SYNCR_CDC_DEV
-        if (stamp && ntile_done == 0) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 1, wall_clock64());
-        if (blockIdx.x < (uint32_t)DBG_TILE_W && ntile_done < (uint32_t)DBG_TILE_N)
-            SCAN_STAMP(T, DBG_TILE + DBG_TILE_N * blockIdx.x + ntile_done, wall_clock64());
+        if (stamp && ntile_done == 0) SCAN_STAMP(T, DBG_SCAN + 4 * wslot + 1, wall_clock64());
+        if (wslot < (uint32_t)DBG_TILE_W && ntile_done < (uint32_t)DBG_TILE_N)
+            SCAN_STAMP(T, DBG_TILE + DBG_TILE_N * wslot + ntile_done, wall_clock64());
         ++ntile_done;
 #endif
         uint32_t A[NQ * 4], B[NQ * 4];
@@ -571,6 +593,10 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");           // runs are in registers
+        if constexpr (CUS) {
+            const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(nk);
+            next = (uint64_t)blockIdx.x + (uint64_t)k * stride < T.ntiles ? blockIdx.x + k * stride : T.ntiles;
+        }
         if (next < T.ntiles && (MODE & 3) != 2) issue_tile<RUN, (MODE & 4) != 0>(data, T.span, next, lds0, lane);
         if constexpr (DYN) {
             if (gj == 0 && !grabbed && lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
@@ -610,8 +636,8 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         uint32_t hwid, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
                      : "=s"(hwid), "=s"(xcc));
-        SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 2, wall_clock64());
-        SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 3,
+        SCAN_STAMP(T, DBG_SCAN + 4 * wslot + 2, wall_clock64());
+        SCAN_STAMP(T, DBG_SCAN + 4 * wslot + 3,
                    (uint64_t)ntile_done | ((uint64_t)hwid << 32) | ((uint64_t)(xcc & 0xf) << 28));
     }
 #endif
@@ -2903,6 +2929,23 @@ hipError_t launch_read_probe(const uint8_t *d, uint64_t bytes, bool nt, uint32_t
 // RUN sizes, the static-stride and timing-only ablations and the MFMA scan,
 // selected by environment variables that the product never reads.
 // ---------------------------------------------------------------------------
+// The CU schedule: one workgroup of SCAN_CU_WAVES waves per CU (grid = the
+// per-wave grid / SCAN_CU_WAVES), plus the LDS tile counter.
+constexpr int SCAN_CU_WAVES = 8;
+template <int RUN, int MODE>
+static void launch_scan_cu(uint32_t wave_grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
+    const size_t lds = (size_t)SCAN_CU_WAVES * lds_wave_bytes(RUN) + 16;
+    const void *f = (const void *)&cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>;
+    static bool attr = false;
+    if (!attr) {                                   // > 64 KB of dynamic LDS per workgroup
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    uint32_t grid = (wave_grid + SCAN_CU_WAVES - 1) / SCAN_CU_WAVES;
+    hipLaunchKernelGGL((cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>), dim3(grid), dim3(64 * SCAN_CU_WAVES), lds, s,
+                       d, p, t);
+}
+
 #ifdef SYNCR_CDC_DEV
 static bool valu_run_ok(int run) {
     return run == 48 || run == 80 || run == W3_RUN || run == 112 || run == 144 || run == 176;
@@ -2972,6 +3015,11 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 14u)                                        // A/B: fine schedule (exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 4 | 16 | 1024>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 15u) {                                      // A/B: CU schedule (exact)
+        launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s);
+    } else if (p.ablate == 16u) {                                    // timing only: CU schedule, no warm-up/halo
+        launch_scan_cu<RUN, 4 | 16 | 256 | 512>(grid, d, p, t, s);
+    }
     else if (p.ablate == 12u)                                        // timing only: no closed-form warm-up
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 13u)                                        // timing only: no warm-up, no halo bytes

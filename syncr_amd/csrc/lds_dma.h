@@ -20,6 +20,7 @@ template <int N> __device__ __forceinline__ void wait_vmcnt() {
 // ds_reads of the OTHER buffer; completion is tracked by hand (wait_vmcnt).
 template <bool NT>
 __device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds) {
+    lds = (uint32_t)__builtin_amdgcn_readfirstlane(lds);     // M0 takes an SGPR (wave-uniform by contract)
     uint32_t keep;
     if constexpr (NT)
         asm volatile(
@@ -62,6 +63,7 @@ __device__ __forceinline__ void dma4(const void *gsrc, uint32_t lds) {
 // NT: non-temporal policy (the bytes are read exactly once).
 template <bool NT>
 __device__ __forceinline__ void dma16_s(uint32_t voff, uint64_t sbase, uint32_t lds) {
+    lds = (uint32_t)__builtin_amdgcn_readfirstlane(lds);     // M0 takes an SGPR (wave-uniform by contract)
     uint32_t keep;
     if constexpr (NT)
         asm volatile(
