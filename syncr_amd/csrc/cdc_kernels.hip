@@ -472,8 +472,8 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         if (threadIdx.x == 0) *cu_next = (uint32_t)WPB;          // k = 0 .. WPB-1 are the waves' first tiles
         __syncthreads();
     }
-    DirtySlot *dslots = (DirtySlot *)(smem + BUF);
-    uint32_t *wlist = (uint32_t *)(smem + BUF + DIRTYCAP * sizeof(DirtySlot));
+    DirtySlot *dslots = (DirtySlot *)(wl + BUF);                     // this wave's side slots and list
+    uint32_t *wlist = (uint32_t *)(wl + BUF + DIRTYCAP * sizeof(DirtySlot));
     uint32_t *wcount = wlist + LISTCAP;
     uint32_t *dcount = wcount + 1;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
