@@ -802,6 +802,7 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
                 fprintf(stderr, "\n");
             }
 #endif
+            if (ctr[CTR_FLAGS] & FLAG_SCHED_STUCK) return SYNCR_CDC_EIO;   // (never: see cdc_internal.h)
             bool rerun = false;
             if (h->last_dense_off && ctr[CTR_DENSE]) {       // dense tiles the launch left unpassed
                 h->dense_hint = true;

@@ -66,7 +66,9 @@ __host__ __device__ constexpr int scan_lds_for_run(int run) {
 
 // ctr[] words (zeroed by the per-launch memset)
 enum { CTR_DENSE = 0, CTR_FLAGS = 1, CTR_CANDS_LO = 2, CTR_CANDS_HI = 3 };
-enum { FLAG_DENSE_OVERFLOW = 1u, FLAG_CUT_OVERFLOW = 2u, FLAG_CAND_OVERFLOW = 4u };
+// FLAG_SCHED_STUCK: a scan wave gave up waiting (~1 s) for its CU's next group
+// id -- cannot happen by construction; fetch reports SYNCR_CDC_EIO if it does
+enum { FLAG_DENSE_OVERFLOW = 1u, FLAG_CUT_OVERFLOW = 2u, FLAG_CAND_OVERFLOW = 4u, FLAG_SCHED_STUCK = 8u };
 
 // compacted candidate: bits 0..47 global position, 48..55 head fix-up (0..63),
 // bit 63 = fix-up known

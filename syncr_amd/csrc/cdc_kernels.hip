@@ -446,15 +446,18 @@ __host__ __device__ constexpr bool scan_dynamic(uint32_t ntiles, uint32_t grid) 
 
 // MODE bit 5: ask for 3 waves per SIMD (VGPRs <= 168; development A/B only).
 // MODE bit 6: the round-2 roll with a branch per group (development A/B only)
-// WPB > 1 (the CU schedule, MODE bit 11): one workgroup of WPB waves per CU,
-// each wave with its own LDS region as above; the CU takes the tiles
-// blockIdx.x + k * gridDim.x (every CU sweeps the batch in step with the
-// others) and its waves take the next k from one LDS counter, a tile at a time.
-// The two waves of a SIMD do not run at the same speed (the arbiter favours
-// one: per-wave rates differ up to 2x with the same mean on every XCC, SE, CU
-// and SIMD, tools/scan_timeline.py), so a static share per wave ends with the
-// slow waves alone on their SIMDs; an LDS counter balances them for ~100
-// cycles per tile, with no global atomics.
+// WPB > 1 (the CU schedule): one workgroup of WPB waves per CU, each wave with
+// its own LDS region as above.  The CU takes groups of CU_GROUP consecutive
+// tiles -- its first group is its block index, later ones come from one global
+// counter (T.sched[0]), fetched a group ahead -- and its waves take the group's
+// tiles one at a time from an LDS counter.  The two waves of a SIMD do not run
+// at the same speed (per-wave rates differ up to 2x with the same mean on every
+// XCC, SE, CU and SIMD, tools/scan_timeline.py): a static share per wave ends
+// with the slow waves alone on their SIMDs, a global counter per tile costs a
+// fabric round trip per tile; the LDS counter balances a CU's waves for ~100
+// cycles per tile and the group counter balances the CUs.
+constexpr uint32_t CU_GROUP = 32;            // tiles per group
+constexpr uint32_t CU_NSLOT = 8;             // group ring in LDS (local group j in slot j % CU_NSLOT)
 template <int RUN, int MODE, int WPB = 1>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu((MODE & 32) ? 3 : 1)))
 void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
@@ -466,10 +469,19 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     const int lane = threadIdx.x & 63;
     const uint32_t wid = CUS ? (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
     uint8_t *wl = smem + wid * (uint32_t)lds_wave_bytes(RUN);
-    __attribute__((address_space(3))) uint32_t *cu_next =
-        (__attribute__((address_space(3))) uint32_t *)(smem + WPB * lds_wave_bytes(RUN));
+    // CU schedule state after the waves' regions: the local tile counter, then
+    // the group ring (u64: local group index << 32 | global group id + 1)
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    typedef __attribute__((address_space(3))) uint64_t lds_u64;
+    lds_u32 *cu_next = (lds_u32 *)(smem + WPB * lds_wave_bytes(RUN));
+    lds_u64 *cu_grp = (lds_u64 *)(smem + WPB * lds_wave_bytes(RUN) + 16);
     if constexpr (CUS) {
-        if (threadIdx.x == 0) *cu_next = (uint32_t)WPB;          // k = 0 .. WPB-1 are the waves' first tiles
+        if (threadIdx.x == 0) {
+            *cu_next = (uint32_t)WPB;                                  // k < WPB: the waves' first tiles
+            cu_grp[0] = (uint64_t)blockIdx.x + 1;                     // group 0: the block's own
+            const uint32_t g1 = gridDim.x + atomicAdd(&T.sched[0], 1u);
+            cu_grp[1] = (1ull << 32) | ((uint64_t)g1 + 1);
+        }
         __syncthreads();
     }
     DirtySlot *dslots = (DirtySlot *)(wl + BUF);                     // this wave's side slots and list
@@ -498,8 +510,43 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     // 16 -> 1.635, 24 -> 1.651, 32 -> 1.633, 64 -> 1.669, static stride 1.657-1.694
     constexpr uint32_t DG = 8;
     auto gbase = [&](uint32_t k) { return (k / stride) * stride * DG + (k % stride); };
-    uint32_t tile = CUS ? blockIdx.x + wid * stride : blockIdx.x;
+    uint32_t tile = CUS ? blockIdx.x * CU_GROUP + wid : blockIdx.x;
     if (tile >= T.ntiles) return;
+    // CU schedule: a prefetch of local group pf_j's id is pending from this wave
+    // (issued when the wave took the first tile of group pf_j - 1); it is stored
+    // at the wave's next landing wait or when the wave exits, before the wave
+    // itself ever waits for a group id, so no wave waits on a wave that waits
+    bool pf_pending = false;
+    uint32_t pf_j = 0, pf_v = 0;
+    auto pf_store = [&]() {
+        if (pf_pending) {
+            const uint32_t g = gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pf_v);
+            if (lane == 0)
+                __hip_atomic_store(&cu_grp[pf_j % CU_NSLOT], ((uint64_t)pf_j << 32) | ((uint64_t)g + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            pf_pending = false;
+        }
+    };
+    // tile of local index k: group j = k / CU_GROUP (its id from the ring, written
+    // by the wave that took j's predecessor's first tile), then that group's
+    // tile k % CU_GROUP
+    auto cu_tile = [&](uint32_t k) -> uint32_t {
+        const uint32_t j = k / CU_GROUP;
+        uint64_t v = __hip_atomic_load(&cu_grp[j % CU_NSLOT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((uint32_t)(v >> 32) != j) {
+            const uint64_t dl = wall_clock64() + 100000000ull;      // ~1 s: bounded, never a hang
+            while ((uint32_t)(v >> 32) != j) {
+                __builtin_amdgcn_s_sleep(2);
+                v = __hip_atomic_load(&cu_grp[j % CU_NSLOT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (wall_clock64() > dl) {
+                    if (lane == 0) atomicOr(&T.ctr[CTR_FLAGS], FLAG_SCHED_STUCK);
+                    return T.ntiles;
+                }
+            }
+        }
+        const uint64_t t = (uint64_t)((uint32_t)v - 1u) * CU_GROUP + k % CU_GROUP;
+        return t < T.ntiles ? (uint32_t)t : T.ntiles;
+    };
     const int64_t span = (int64_t)T.span;
     const uint32_t wslot = blockIdx.x * WPB + wid;                 // timeline slot of this wave
     const bool stamp = wslot < (uint32_t)DBG_SCAN_N;
@@ -563,6 +610,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         wait_vmcnt<0>();                                             // this tile has landed
         uint32_t nk = 0;
         if constexpr (CUS) {                                         // the CU's next tile (read after the runs)
+            pf_store();
             if (lane == 0) nk = __hip_atomic_fetch_add(cu_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         if constexpr (FINE) {                                        // (and the pending grab has returned)
@@ -595,7 +643,12 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");           // runs are in registers
         if constexpr (CUS) {
             const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(nk);
-            next = (uint64_t)blockIdx.x + (uint64_t)k * stride < T.ntiles ? blockIdx.x + k * stride : T.ntiles;
+            if (k % CU_GROUP == 0u) {                                // first tile of local group j: fetch group j+1
+                if (lane == 0) pf_v = atomicAdd(&T.sched[0], 1u);
+                pf_pending = true;
+                pf_j = k / CU_GROUP + 1;
+            }
+            next = cu_tile(k);
         }
         if (next < T.ntiles && (MODE & 3) != 2) issue_tile<RUN, (MODE & 4) != 0>(data, T.span, next, lds0, lane);
         if constexpr (DYN) {
@@ -629,6 +682,12 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         }
         if (nd && nd <= (uint32_t)DIRTYCAP) rewalk_dirty<RUN>(P, lane, nd, dslots, lim_rel, wcount, wlist);
         publish_tile(data, P, T, tile, t0, wlist, wcount, lane, nd > (uint32_t)DIRTYCAP, dslots_alloc);
+    }
+    if constexpr (CUS) {
+        if (pf_pending) {                                            // readers may wait for it
+            wait_vmcnt<0>();
+            pf_store();
+        }
     }
 #ifdef SYNCR_CDC_DEV
     if (stamp) {
@@ -2934,7 +2993,7 @@ hipError_t launch_read_probe(const uint8_t *d, uint64_t bytes, bool nt, uint32_t
 constexpr int SCAN_CU_WAVES = 8;
 template <int RUN, int MODE>
 static void launch_scan_cu(uint32_t wave_grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    const size_t lds = (size_t)SCAN_CU_WAVES * lds_wave_bytes(RUN) + 16;
+    const size_t lds = (size_t)SCAN_CU_WAVES * lds_wave_bytes(RUN) + 16 + 8 * CU_NSLOT;
     const void *f = (const void *)&cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>;
     static bool attr = false;
     if (!attr) {                                   // > 64 KB of dynamic LDS per workgroup
