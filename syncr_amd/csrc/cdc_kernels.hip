@@ -497,21 +497,14 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     // index; later ones come from a counter (CTR_CANDS_HI is free until the
     // prefix kernel writes it), grabbed at a group's first tile so the atomic
     // completes under the roll.
-    constexpr bool DYN = (MODE & 8) != 0 && (MODE & 1024) == 0;
-    // MODE bit 10 (FINE): one tile per grab from per-region counters (T.sched):
-    // wave b starts in region b % NR at the region's tile b / NR, then takes the
-    // region's next free tile (the grab for the tile after next is issued when
-    // next's DMA is, so it returns under a whole roll); an exhausted region sends
-    // the wave to the next region (at most NR switches).  Waves run at different
-    // speeds (a factor of ~2 between placements, tools/scan_timeline.py), so
-    // every wave finishes within about one tile of the others.
-    constexpr bool FINE = (MODE & 1024) != 0;
+    constexpr bool DYN = (MODE & 8) != 0 && !CUS;
     // zipf10k A/B (same process): groups of 4 -> 2.07 ms (one counter serialises ~69 M grabs/s), 8 -> 1.601,
     // 16 -> 1.635, 24 -> 1.651, 32 -> 1.633, 64 -> 1.669, static stride 1.657-1.694
     constexpr uint32_t DG = 8;
     auto gbase = [&](uint32_t k) { return (k / stride) * stride * DG + (k % stride); };
-    uint32_t tile = CUS ? blockIdx.x * CU_GROUP + wid : blockIdx.x;
-    if (tile >= T.ntiles) return;
+    uint32_t tile = blockIdx.x;
+    if (!CUS && tile >= T.ntiles) return;
+    const int64_t span = (int64_t)T.span;
     // CU schedule: a prefetch of local group pf_j's id is pending from this wave
     // (issued when the wave took the first tile of group pf_j - 1); it is stored
     // at the wave's next landing wait or when the wave exits, before the wave
@@ -527,13 +520,26 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             pf_pending = false;
         }
     };
-    // tile of local index k: group j = k / CU_GROUP (its id from the ring, written
-    // by the wave that took j's predecessor's first tile), then that group's
-    // tile k % CU_GROUP
+    // Group g covers the tiles (g / NB) * NB * CU_GROUP + g % NB + i * NB, i <
+    // CU_GROUP (NB = the grid): the CUs sweep the batch together, each wave a
+    // tile NB apart from its CU's others.  A group whose first tile lies past
+    // the batch ends the CU's work (later groups start later); a tile past the
+    // batch inside an earlier group is skipped.
+    const uint32_t NB = gridDim.x;
+    auto gtile = [&](uint32_t g, uint32_t i) -> uint64_t {
+        return (uint64_t)(g / NB) * NB * CU_GROUP + g % NB + (uint64_t)i * NB;
+    };
+    // the tile of local index k (group j = k / CU_GROUP, id from the ring; the
+    // wave's own pending prefetch is stored before it ever waits on the ring),
+    // T.ntiles when the CU has no tile left, 0xffffffff for a skipped index
     auto cu_tile = [&](uint32_t k) -> uint32_t {
         const uint32_t j = k / CU_GROUP;
         uint64_t v = __hip_atomic_load(&cu_grp[j % CU_NSLOT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if ((uint32_t)(v >> 32) != j) {
+            if (pf_pending) {
+                wait_vmcnt<0>();
+                pf_store();
+            }
             const uint64_t dl = wall_clock64() + 100000000ull;      // ~1 s: bounded, never a hang
             while ((uint32_t)(v >> 32) != j) {
                 __builtin_amdgcn_s_sleep(2);
@@ -544,44 +550,49 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 }
             }
         }
-        const uint64_t t = (uint64_t)((uint32_t)v - 1u) * CU_GROUP + k % CU_GROUP;
-        return t < T.ntiles ? (uint32_t)t : T.ntiles;
+        const uint32_t g = (uint32_t)v - 1u;
+        if (gtile(g, 0) >= T.ntiles) return T.ntiles;
+        const uint64_t t = gtile(g, k % CU_GROUP);
+        return t < T.ntiles ? (uint32_t)t : 0xffffffffu;
     };
-    const int64_t span = (int64_t)T.span;
-    const uint32_t wslot = blockIdx.x * WPB + wid;                 // timeline slot of this wave
+    // local index k taken: the first tile of group j fetches group j+1's id
+    auto cu_took = [&](uint32_t k) {
+        if (k % CU_GROUP == 0u) {
+            if (pf_pending) {                                        // (one prefetch in flight per wave)
+                wait_vmcnt<0>();
+                pf_store();
+            }
+            if (lane == 0) pf_v = atomicAdd(&T.sched[0], 1u);
+            pf_pending = true;
+            pf_j = k / CU_GROUP + 1;
+        }
+    };
+    if constexpr (CUS) {
+        tile = (uint32_t)min<uint64_t>(gtile(blockIdx.x, wid), (uint64_t)T.ntiles);
+        if (tile >= T.ntiles) {                                      // (skipped or past the batch: tiny batch)
+            if (gtile(blockIdx.x, 0) >= T.ntiles) return;
+            for (;;) {                                               // a later tile of the CU, if any
+                uint32_t k = 0;
+                if (lane == 0) k = __hip_atomic_fetch_add(cu_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                k = (uint32_t)__builtin_amdgcn_readfirstlane(k);
+                cu_took(k);
+                tile = cu_tile(k);
+                if (tile != 0xffffffffu) break;
+            }
+            if (tile >= T.ntiles) {
+                if (pf_pending) {
+                    wait_vmcnt<0>();
+                    pf_store();
+                }
+                return;
+            }
+        }
+    }
+    const uint32_t wslot = blockIdx.x * WPB + wid;                 // timeline slot of this wave (dev)
     const bool stamp = wslot < (uint32_t)DBG_SCAN_N;
     if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * wslot, wall_clock64());
-    // fine schedule: regions [rb(r), rb(r+1)); the first ns(r) tiles of a region
-    // are the static first tiles of its waves, the rest are handed out by its counter
-    const uint32_t NR = stride < SCHED_REGIONS ? stride : SCHED_REGIONS;
-    auto rb = [&](uint32_t r) { return (uint32_t)(((uint64_t)r * T.ntiles) / NR); };
-    auto ns = [&](uint32_t r) {
-        const uint32_t nw = (stride - r + NR - 1) / NR, sz = rb(r + 1) - rb(r);
-        return nw < sz ? nw : sz;
-    };
-    uint32_t reg = blockIdx.x % NR, switches = 0;
-    // the next free tile of another region, waited for here (only once a region is exhausted)
-    auto grab_elsewhere = [&]() -> uint32_t {
-        while (++switches < NR) {
-            reg = reg + 1 == NR ? 0u : reg + 1;
-            uint32_t v = 0;
-            if (lane == 0) v = atomicAdd(&T.sched[reg * COARSE_STRIDE], 1u);
-            wait_vmcnt<0>();
-            const uint32_t t = rb(reg) + ns(reg) + (uint32_t)__builtin_amdgcn_readfirstlane(v);
-            if (t < rb(reg + 1)) return t;
-        }
-        return 0xffffffffu;
-    };
-    if constexpr (FINE) {
-        tile = rb(reg) + blockIdx.x / NR;
-        if (tile >= rb(reg + 1)) tile = grab_elsewhere();
-        if (tile >= T.ntiles) return;
-    }
     issue_tile<RUN, (MODE & 4) != 0>(data, T.span, tile, lds0, lane);
     uint32_t gj = 0, pend = 0;
-    if constexpr (FINE) {
-        if (lane == 0) pend = atomicAdd(&T.sched[reg * COARSE_STRIDE], 1u);     // the tile after this one
-    }
     DenseSlots dslots_alloc;
 #ifdef SYNCR_CDC_DEV
     uint32_t ntile_done = 0;
@@ -602,7 +613,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 next = gbase(stride + (uint32_t)__builtin_amdgcn_readfirstlane(pend));
                 gjn = 0;
             }
-        } else if constexpr (!FINE && !CUS) {
+        } else if constexpr (!CUS) {
             next = tile + stride;
         }
         const int64_t t0 = (int64_t)tile * TILE;
@@ -612,11 +623,6 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         if constexpr (CUS) {                                         // the CU's next tile (read after the runs)
             pf_store();
             if (lane == 0) nk = __hip_atomic_fetch_add(cu_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if constexpr (FINE) {                                        // (and the pending grab has returned)
-            next = rb(reg) + ns(reg) + (uint32_t)__builtin_amdgcn_readfirstlane(pend);
-            if (next >= rb(reg + 1)) next = grab_elsewhere();
-            if (next > T.ntiles) next = T.ntiles;
         }
 #ifdef SYNCR_CDC_DEV
         if (stamp && ntile_done == 0) SCAN_STAMP(T, DBG_SCAN + 4 * wslot + 1, wall_clock64());
@@ -642,21 +648,19 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");           // runs are in registers
         if constexpr (CUS) {
-            const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(nk);
-            if (k % CU_GROUP == 0u) {                                // first tile of local group j: fetch group j+1
-                if (lane == 0) pf_v = atomicAdd(&T.sched[0], 1u);
-                pf_pending = true;
-                pf_j = k / CU_GROUP + 1;
+            uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(nk);
+            for (;;) {
+                cu_took(k);
+                next = cu_tile(k);
+                if (next != 0xffffffffu) break;
+                if (lane == 0) k = __hip_atomic_fetch_add(cu_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                k = (uint32_t)__builtin_amdgcn_readfirstlane(k);
             }
-            next = cu_tile(k);
         }
         if (next < T.ntiles && (MODE & 3) != 2) issue_tile<RUN, (MODE & 4) != 0>(data, T.span, next, lds0, lane);
         if constexpr (DYN) {
             if (gj == 0 && !grabbed && lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
             gj = gjn;
-        }
-        if constexpr (FINE) {
-            if (next < T.ntiles && lane == 0) pend = atomicAdd(&T.sched[reg * COARSE_STRIDE], 1u);
         }
         if constexpr ((MODE & 3) == 1) {                                   // diagnostics: staging only
 #pragma unroll
@@ -815,15 +819,7 @@ void cdc_scan3_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     constexpr int NQ = (HALO + RUN) / 16;
     constexpr int NG = RUN / 16;
     constexpr bool NT = (MODE & 4) != 0;
-    constexpr bool DYN = (MODE & 8) != 0 && (MODE & 1024) == 0;
-    // MODE bit 10 (FINE): one tile per grab from per-region counters (T.sched):
-    // wave b starts in region b % NR at the region's tile b / NR, then takes the
-    // region's next free tile (the grab for the tile after next is issued when
-    // next's DMA is, so it returns under a whole roll); an exhausted region sends
-    // the wave to the next region (at most NR switches).  Waves run at different
-    // speeds (a factor of ~2 between placements, tools/scan_timeline.py), so
-    // every wave finishes within about one tile of the others.
-    constexpr bool FINE = (MODE & 1024) != 0;
+    constexpr bool DYN = (MODE & 8) != 0;
     const int lane = threadIdx.x;
     uint8_t *wl = smem;
     uint32_t *drel = (uint32_t *)(smem + buf_bytes(RUN));
@@ -3072,8 +3068,6 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 14u)                                        // A/B: fine schedule (exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 4 | 16 | 1024>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 15u) {                                      // A/B: CU schedule (exact)
         launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s);
     } else if (p.ablate == 16u) {                                    // timing only: CU schedule, no warm-up/halo
