@@ -434,10 +434,13 @@ __device__ __forceinline__ void issue_tile(const uint8_t *data, uint64_t span, u
 // the scan to 256 VGPRs (one wave per SIMD); out of line it needs 384 B of
 // scratch per lane and 254 VGPRs; the product keeps the separate launch.
 constexpr int SCAN_PRODUCT_MODE = 4 | 8 | 16;
-// Small batches use the static stride: a group of 8 tiles is ~46 us of one
-// wave's roll, and below ~80-100 tiles per wave the last groups' imbalance
-// costs more than the dynamic grab recovers (same process, ROLL2 in both,
-// tools/ab_bench.py: profiles/r02_ab_schedule.log).  scan_dynamic() picks.
+// Small batches do not use the dynamic groups: a group of 8 tiles is ~46 us of
+// one wave's roll, and below ~80-100 tiles per wave the last groups' imbalance
+// costs more than the dynamic grab recovers (profiles/r02_ab_schedule.log).
+// They run the CU schedule (cdc_scan_kernel<..., WPB = 8>, round 4): the static
+// stride they used before left a SIMD's slow wave alone at the end (per-wave
+// ends 113-229 us on uniform1k, profiles/r04b_*), the CU schedule ends every
+// wave within ~30 us (profiles/r04d_*, r04f_*).  scan_dynamic() picks.
 constexpr int SCAN_STATIC_MODE = 4 | 16;
 constexpr uint32_t SCAN_DYN_MIN_TILES_PER_WAVE = 96;
 __host__ __device__ constexpr bool scan_dynamic(uint32_t ntiles, uint32_t grid) {
@@ -3083,8 +3086,8 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
                            t);
     else if (p.nt && scan_dynamic(t.ntiles, grid))                   // product: nt loads + dynamic groups + ROLL2
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.nt)                                                   // product, small batch: static stride
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.nt)                                                   // product, small batch: CU schedule
+        launch_scan_cu<RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);
     else
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE & ~4>), dim3(grid), dim3(64), lds, s, d, p, t);
 }
@@ -3174,9 +3177,8 @@ hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParam
     if (scan_dynamic(t.ntiles, grid))
         hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
                            lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
-    else
-        hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64),
-                           lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
+    else                                          // small batch: the CU schedule (per-wave static shares end
+        launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);   // with the slow waves alone)
     return hipGetLastError();
 }
 #endif
