@@ -710,6 +710,338 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 }
 
 // ---------------------------------------------------------------------------
+// Stream-tile scan (round 4): the rolling window carries over between runs.
+//
+// The warm-up of every 144-byte run (64 v_dot4 for S and W of the 64 bytes
+// before it, 64 v_perm for their pairs, 208 bytes of LDS read per 144 rolled)
+// is ~13 % of the roll's VALU work, and in the shader-clock dip the scan is
+// VALU/energy bound: the same scan without warm-up and halo ran 8-10 % faster
+// in the driver's window (timing-only ablations, profiles/r04a_dip_ablation.jsonl).
+// A stream tile (ST) is ST_G consecutive tiles = 128 STREAMS of ST_G * RUN bytes
+// (stream s = bytes [s * ST_G * RUN, (s + 1) * ST_G * RUN) of the ST; lane l owns
+// streams l and l + 64, packed as in roll_fast).  Iteration g rolls segment g of
+// every stream: the 144 new bytes land in LDS by LDS-DMA (stream-major, no halo);
+// the window's state (S, T) and the 64 packed byte pairs it will drop (P) stay in
+// registers from segment g - 1.  Only segment 0 warms up (closed form), from the
+// 64 bytes before each stream, loaded into registers one iteration ahead.
+// Bookkeeping is unchanged: tile t of the ST = streams 16t .. 16t + 15 = one
+// contiguous TILE of the batch, its candidates collected over the ST_G
+// iterations and published when the ST ends.
+// Dirty groups: groups 0..3 of a segment drop the previous segment's bytes, kept
+// only as packed pairs in P: they are captured at a checkpoint after group 3
+// (before P is overwritten); groups 4.. drop this segment's own bytes and are
+// captured after the roll, as in roll_fast.  A slot stores the dropped bytes as
+// packed pairs.
+// ---------------------------------------------------------------------------
+constexpr int ST_G = 8;                       // segments per stream (tiles per ST)
+constexpr int ST_LISTCAP = 32;                // candidate slots per tile (more: dense)
+constexpr int ST_DIRTYCAP = 6;                // side slots per segment
+struct DirtySlotST {                          // 144 bytes
+    uint32_t dp[16];                          // dropped bytes, packed pairs (run A low, run B high)
+    uint32_t xp[16];                          // new bytes, packed pairs
+    uint32_t S0, T0;                          // packed state before the group
+    uint32_t relA;                            // ST-relative position of the group's first byte, run A
+    uint32_t pad;
+};
+static_assert(sizeof(DirtySlotST) == 144, "slot size");
+__host__ __device__ constexpr int st_lds_bytes(int run) {
+    return RUNS * run + ST_DIRTYCAP * (int)sizeof(DirtySlotST) + ST_G * ST_LISTCAP * 4 + ST_G * 4 + 16;
+}
+
+template <int RUN>
+__device__ __forceinline__ uint32_t xpair(const uint32_t (&XA)[RUN / 4], const uint32_t (&XB)[RUN / 4], int j) {
+    return __builtin_amdgcn_perm(XB[j >> 2], XA[j >> 2], 0x0C040C00u + (uint32_t)(j & 3) * 0x00010001u);
+}
+
+// packed (S, T) of the 64 bytes words[q0 .. q0 + 15] of both runs (window_state's closed form)
+template <int N>
+__device__ __forceinline__ void window_at(const uint32_t (&A)[N], const uint32_t (&B)[N], const KParams &P, int q0,
+                                          uint32_t &S, u16x2 &Tv) {
+    uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const uint32_t w = 0x3D3E3F40u - 0x04040404u * (uint32_t)m;
+        SA = __builtin_amdgcn_udot4(A[q0 + m], 0x01010101u, SA, false);
+        WA = __builtin_amdgcn_udot4(A[q0 + m], w, WA, false);
+        SB = __builtin_amdgcn_udot4(B[q0 + m], 0x01010101u, SB, false);
+        WB = __builtin_amdgcn_udot4(B[q0 + m], w, WB, false);
+    }
+    S = SA | (SB << 16);
+    const uint32_t tA = ((124993u + WA) * P.k) & 0xffffu;
+    const uint32_t tB = ((124993u + WB) * P.k) & 0xffffu;
+    Tv = as_u16x2(tA | (tB << 16));
+}
+
+// Publish one tile's list (n candidates, tile-relative positions) or mark it dense.
+__device__ __forceinline__ void publish_list(const Tables &T, uint32_t tile, const uint32_t *list, uint32_t n,
+                                             int lane, bool force_dense, DenseSlots &ds) {
+    if (n == 0u && !force_dense) return;
+    if (lane == 0) atomicOr(&T.nonempty[tile >> 6], 1ull << (tile & 63));
+    if (n > (uint32_t)ST_LISTCAP || force_dense) {
+        if (ds.lo == ds.hi) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&T.ctr[CTR_DENSE], DENSE_CHUNK);
+            base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
+            ds.lo = base;
+            ds.hi = base + DENSE_CHUNK;
+            if ((uint32_t)lane < DENSE_CHUNK && base + (uint32_t)lane < T.dense_cap)
+                T.dense_list[base + (uint32_t)lane] = DENSE_HOLE;
+        }
+        const uint32_t idx = ds.lo++;
+        if (lane == 0) {
+            if (idx < T.dense_cap) {
+                T.dense_list[idx] = tile;
+                T.tile_meta[tile] = DENSE_BIT | idx;
+            } else {
+                T.tile_meta[tile] = DENSE_BIT | 0x7fffffffu;
+                atomicOr(&T.ctr[CTR_FLAGS], FLAG_DENSE_OVERFLOW);
+            }
+        }
+        return;
+    }
+    const uint32_t e = (uint32_t)lane < n ? list[lane] : 0xffffffffu;
+    uint32_t rank = 0;
+    for (uint32_t m = 0; m < n; ++m) rank += list[m] < e;
+    if ((uint32_t)lane < n) T.slots[(size_t)tile * LISTCAP + rank] = make_uint2(e, 0u);
+    if (lane == 0) {
+        T.tile_meta[tile] = n;
+        atomicAdd(&T.super_cnt[tile >> 6], n);
+        atomicAdd(&T.coarse[(tile >> 12) * COARSE_STRIDE], n);
+    }
+}
+
+template <int RUN, int MODE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
+void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NW = RUN / 4;                  // words per segment and run
+    constexpr int NG = RUN / 16;                 // 16-byte groups per segment
+    constexpr int NP = RUNS * RUN / 16;          // 16-byte pieces per segment DMA (all streams)
+    constexpr int NQ = RUN / 16;                 // pieces per stream segment
+    constexpr uint32_t L = ST_G * RUN;           // stream bytes
+    constexpr uint32_t STB = RUNS * L;           // ST bytes
+    static_assert(NP % 64 == 0 && (RUN / 16) % 2 == 1, "DMA and conflict-free reads");
+    static_assert(ST_G * 16 == RUNS, "tile t of an ST = streams 16t .. 16t+15 = one batch tile");
+    const int lane = threadIdx.x;
+    uint8_t *wl = smem;
+    DirtySlotST *dslots = (DirtySlotST *)(smem + RUNS * RUN);
+    uint32_t *tlist = (uint32_t *)(smem + RUNS * RUN + ST_DIRTYCAP * sizeof(DirtySlotST));
+    uint32_t *tcnt = tlist + ST_G * ST_LISTCAP;
+    uint32_t *dcount = tcnt + ST_G;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
+    const uint32_t nst = (T.ntiles + ST_G - 1) / ST_G;
+    const int64_t span = (int64_t)T.span;
+    // per-lane DMA offsets: instruction i (i < 2 NQ... NP/64) moves piece c = 64 i + lane:
+    // stream c / NQ, piece c % NQ; instructions i and i + NQ differ by 64 streams
+    uint32_t off[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        const uint32_t c = 64u * (uint32_t)i + (uint32_t)lane;
+        off[i] = (c / NQ) * L + (c % NQ) * 16u;
+    }
+    auto issue_seg = [&](uint32_t st, uint32_t g) {
+        const uint64_t b0 = (uint64_t)st * STB + (uint64_t)g * RUN;
+        if (b0 + STB - (uint64_t)g * RUN <= (uint64_t)span) {                   // whole ST inside the batch
+#pragma unroll
+            for (int i = 0; i < NP / 64; ++i) {
+                const uint64_t sb = (uint64_t)(data + b0 + (uint64_t)(i / NQ) * 64u * L);
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
+                dma16_s<(MODE & 4) != 0>(off[i % NQ], ((uint64_t)hi << 32) | lo, lds0 + 1024u * (uint32_t)i);
+            }
+        } else {                                 // the batch's last ST: clamp (bytes past it are never recorded)
+            const int64_t last = (int64_t)((span - 1) & ~15ll);
+#pragma unroll
+            for (int i = 0; i < NP / 64; ++i) {
+                int64_t a = (int64_t)b0 + (int64_t)(i / NQ) * 64 * L + off[i % NQ];
+                a = a > last ? last : a;
+                dma16<(MODE & 4) != 0>(data + a, lds0 + 1024u * (uint32_t)i);
+            }
+        }
+    };
+    // the 64 bytes before each of this lane's two streams (segment 0's warm-up)
+    uint32_t HA[16], HB[16];
+    auto load_halo = [&](uint32_t st) {
+        const int64_t sa = (int64_t)st * STB + (int64_t)lane * L - 64, sbb = sa + 64 * (int64_t)L;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            uint4 va, vb;
+            const int64_t a = sa + 16 * m, b = sbb + 16 * m;
+            if (a >= 0 && a + 16 <= span) va = *(const uint4 *)(data + a); else va = make_uint4(0, 0, 0, 0);
+            if (b >= 0 && b + 16 <= span) vb = *(const uint4 *)(data + b); else vb = make_uint4(0, 0, 0, 0);
+            HA[4 * m] = va.x; HA[4 * m + 1] = va.y; HA[4 * m + 2] = va.z; HA[4 * m + 3] = va.w;
+            HB[4 * m] = vb.x; HB[4 * m + 1] = vb.y; HB[4 * m + 2] = vb.z; HB[4 * m + 3] = vb.w;
+        }
+    };
+    uint32_t st = blockIdx.x;
+    if (st >= nst) return;
+    issue_seg(st, 0);
+    load_halo(st);
+    uint32_t pend = 0, nextst = 0;
+    DenseSlots dslots_alloc;
+    uint32_t Pd[64];                               // packed pairs the window drops at positions 0..63
+    uint32_t Sc = 0;                               // carried state
+    u16x2 Tc = as_u16x2(0u);
+    for (;;) {
+#pragma unroll 1
+        for (uint32_t g = 0; g < (uint32_t)ST_G; ++g) {
+            if (g == 0u) {
+                if (lane < ST_G) tcnt[lane] = 0u;
+                if (lane == 0 && nst > gridDim.x) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);   // the next ST
+            }
+            if (lane == 0) *dcount = 0u;
+            wait_vmcnt<0>();                                         // segment g landed (and, at 0, the halo)
+            if (g == 0u) {                                           // warm-up from the halo
+                window_at<16>(HA, HB, P, 0, Sc, Tc);
+#pragma unroll
+                for (int j = 0; j < 64; ++j)
+                    Pd[j] = __builtin_amdgcn_perm(HB[j >> 2], HA[j >> 2], 0x0C040C00u + (uint32_t)(j & 3) * 0x00010001u);
+            }
+            uint32_t XA[NW], XB[NW];
+            {
+                const uint4 *la = (const uint4 *)(wl + lane * RUN);
+                const uint4 *lb = (const uint4 *)(wl + (lane + 64) * RUN);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const uint4 a = la[q], b = lb[q];
+                    XA[4 * q + 0] = a.x; XA[4 * q + 1] = a.y; XA[4 * q + 2] = a.z; XA[4 * q + 3] = a.w;
+                    XB[4 * q + 0] = b.x; XB[4 * q + 1] = b.y; XB[4 * q + 2] = b.z; XB[4 * q + 3] = b.w;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // segment in registers: buffer free
+            bool more = true;
+            if (g + 1 < (uint32_t)ST_G) {
+                issue_seg(st, g + 1);
+            } else {
+                nextst = nst > gridDim.x ? gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nst;
+                more = nextst < nst;
+                if (more) {
+                    issue_seg(nextst, 0);
+                    load_halo(nextst);
+                }
+            }
+            // ---- roll segment g: positions 0..63 drop Pd, later ones this segment's own pairs.
+            // A group whose minimum T has a zero half is captured right after it is rolled, from
+            // the packed pairs it added and dropped (still in registers then) and its entry
+            // state: no raw word or pair has to outlive its last use in the roll.
+            const int64_t lim_rel = span - (int64_t)st * STB;         // ST-relative positions >= lim: not bytes
+            const uint32_t relA0 = (uint32_t)lane * L + g * RUN;
+            uint32_t S = Sc;
+            u16x2 Tv = Tc;
+            bool dirty = false;                                      // (any dirty group: dense marking)
+            uint32_t xs[RUN];                                        // pairs of this segment (registers: unrolled)
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg) {
+                const uint32_t S0 = S;
+                const u16x2 T0 = Tv;
+                u16x2 acc = as_u16x2(0xffffffffu);
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj) {
+                    const int j = gg * 16 + jj;
+                    xs[j] = xpair<RUN>(XA, XB, j);
+                    const uint32_t d = j < 64 ? Pd[j < 64 ? j : 0] : xs[j >= 64 ? j - 64 : 0];
+                    S = S + xs[j] - d;
+                    const u16x2 V = pk_mad(d, 0xFFC0FFC0u, as_u16x2(S));
+                    Tv = pk_mad(as_u32(V), P.kk, Tv);
+                    acc = __builtin_elementwise_min(acc, Tv);
+                }
+                const uint32_t a = as_u32(acc);
+                const bool z = (a & 0xffffu) == 0u || (a >> 16) == 0u;
+                dirty = dirty || z;
+                const uint64_t bz = __ballot(z);
+                if (__builtin_expect(bz != 0ull, 0)) {
+                    const uint32_t have = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)dcount, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WAVEFRONT));
+                    if (have + (uint32_t)__builtin_popcountll(bz) > (uint32_t)ST_DIRTYCAP) {
+                        if (lane == 0) *dcount = have | 0x10000u;          // overflow: dense (below)
+                    } else if (z) {
+                        const uint32_t idx = atomicAdd(dcount, 1u);
+                        DirtySlotST &ds = dslots[idx];
+#pragma unroll
+                        for (int jj = 0; jj < 16; ++jj) {
+                            const int j = gg * 16 + jj;
+                            ds.dp[jj] = j < 64 ? Pd[j < 64 ? j : 0] : xs[j >= 64 ? j - 64 : 0];
+                            ds.xp[jj] = xs[j];
+                        }
+                        ds.S0 = S0;
+                        ds.T0 = as_u32(T0);
+                        ds.relA = relA0 + 16u * (uint32_t)gg;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                }
+            }
+            // carry the window: the pairs of positions RUN-64 .. RUN-1 are the next segment's dropped bytes
+#pragma unroll
+            for (int j = 0; j < 64; ++j) Pd[j] = xs[RUN - 64 + j];
+            Sc = S;
+            Tc = Tv;
+            // ---- exact re-walk of the captured groups; an overflow marks the dirty streams' tiles dense
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            const uint32_t dc = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)dcount, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WAVEFRONT));
+            if (__builtin_expect(dc != 0u, 0)) {
+                if (dc & 0x10000u) {
+                    // more dirty groups than slots: every tile holding a dirty stream goes to the
+                    // dense pass (lane l's streams l and l + 64 lie in tiles l / 16 and 4 + l / 16)
+                    const uint64_t bal = __ballot(dirty);
+                    uint32_t m = 0;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if ((bal >> (16 * t)) & 0xffffull) m |= (1u << t) | (1u << (t + 4));
+                    if (lane < ST_G && ((m >> lane) & 1u)) tcnt[lane] |= 0x80000000u;   // dense mark
+                }
+                const uint32_t nd = dc & 0xffffu;
+                if ((uint32_t)lane < nd) {
+                    const DirtySlotST &ds = dslots[lane];
+                    const u16x2 kk = as_u16x2(P.kk), km = as_u16x2(P.kmv);
+                    uint32_t s = ds.S0;
+                    u16x2 t = as_u16x2(ds.T0);
+                    const uint32_t relA = ds.relA, relB = ds.relA + 64u * L;
+                    for (int jj = 0; jj < 16; ++jj) {
+                        const uint32_t x = ds.xp[jj];
+                        const uint32_t d = ds.dp[jj];
+                        s = s + x - d;
+                        t = as_u16x2(s) * kk + t;
+                        t = as_u16x2(d) * km + t;
+                        if (t.x == 0 && ((1984u + (s & 0xffffu)) & P.m1) == P.m1 && (int64_t)(relA + jj) < lim_rel) {
+                            const uint32_t p = relA + jj, tt = p / (uint32_t)tile_bytes(RUN);
+                            const uint32_t idx = atomicAdd(&tcnt[tt], 1u) & 0x7fffffffu;
+                            if (idx < (uint32_t)ST_LISTCAP) tlist[tt * ST_LISTCAP + idx] = p - tt * (uint32_t)tile_bytes(RUN);
+                        }
+                        if (t.y == 0 && ((1984u + (s >> 16)) & P.m1) == P.m1 && (int64_t)(relB + jj) < lim_rel) {
+                            const uint32_t p = relB + jj, tt = p / (uint32_t)tile_bytes(RUN);
+                            const uint32_t idx = atomicAdd(&tcnt[tt], 1u) & 0x7fffffffu;
+                            if (idx < (uint32_t)ST_LISTCAP) tlist[tt * ST_LISTCAP + idx] = p - tt * (uint32_t)tile_bytes(RUN);
+                        }
+                    }
+                }
+            }
+            if (g + 1 == (uint32_t)ST_G) {                           // the ST's tiles are complete: publish
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll 1
+                for (uint32_t t = 0; t < (uint32_t)ST_G; ++t) {
+                    const uint32_t tile = st * ST_G + t;
+                    if (tile >= T.ntiles) break;
+                    const uint32_t c = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)&tcnt[t], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WAVEFRONT));
+                    publish_list(T, tile, tlist + t * ST_LISTCAP, c & 0x7fffffffu, lane, (c >> 31) != 0u,
+                                 dslots_alloc);
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (!more) return;
+        }
+        st = nextst;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Three-waves-per-SIMD scan (cdc_scan3_kernel, RUN = W3_RUN = 96).
 //
 // At two waves per SIMD a wave issues a VALU instruction at most every ~8
@@ -3071,6 +3403,8 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.ablate == 17u)                                        // A/B: stream-tile scan (exact)
+        hipLaunchKernelGGL((cdc_scan_st_kernel<RUN, 4>), dim3(grid), dim3(64), st_lds_bytes(RUN), s, d, p, t);
     else if (p.ablate == 15u) {                                      // A/B: CU schedule (exact)
         launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s);
     } else if (p.ablate == 16u) {                                    // timing only: CU schedule, no warm-up/halo
