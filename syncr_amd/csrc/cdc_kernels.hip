@@ -710,32 +710,38 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 }
 
 // ---------------------------------------------------------------------------
-// Stream-tile scan (round 4): the rolling window carries over between runs.
+// Stream-tile scan (round 4): the rolling window carries over between segments.
 //
-// The warm-up of every 144-byte run (64 v_dot4 for S and W of the 64 bytes
-// before it, 64 v_perm for their pairs, 208 bytes of LDS read per 144 rolled)
-// is ~13 % of the roll's VALU work, and in the shader-clock dip the scan is
-// VALU/energy bound: the same scan without warm-up and halo ran 8-10 % faster
-// in the driver's window (timing-only ablations, profiles/r04a_dip_ablation.jsonl).
-// A stream tile (ST) is ST_G consecutive tiles = 128 STREAMS of ST_G * RUN bytes
-// (stream s = bytes [s * ST_G * RUN, (s + 1) * ST_G * RUN) of the ST; lane l owns
-// streams l and l + 64, packed as in roll_fast).  Iteration g rolls segment g of
-// every stream: the 144 new bytes land in LDS by LDS-DMA (stream-major, no halo);
-// the window's state (S, T) and the 64 packed byte pairs it will drop (P) stay in
-// registers from segment g - 1.  Only segment 0 warms up (closed form), from the
-// 64 bytes before each stream, loaded into registers one iteration ahead.
-// Bookkeeping is unchanged: tile t of the ST = streams 16t .. 16t + 15 = one
-// contiguous TILE of the batch, its candidates collected over the ST_G
-// iterations and published when the ST ends.
-// Dirty groups: groups 0..3 of a segment drop the previous segment's bytes, kept
-// only as packed pairs in P: they are captured at a checkpoint after group 3
-// (before P is overwritten); groups 4.. drop this segment's own bytes and are
-// captured after the roll, as in roll_fast.  A slot stores the dropped bytes as
-// packed pairs.
+// The warm-up of every 144-byte run of cdc_scan_kernel (64 v_dot4 for S and W
+// of the 64 bytes before it, 64 v_perm for their pairs, 208 bytes of LDS read
+// per 144 rolled) is ~13 % of the roll's VALU work, and in the shader-clock dip
+// the scan is VALU / energy bound: the same scan without warm-up and halo ran
+// 8-10 % faster in the driver's window (timing-only ablations,
+// profiles/r04a_dip_ablation.jsonl).  A stream tile (ST) is 8 consecutive tiles
+// (147 456 bytes) cut into 128 STREAMS of ST_SEGS segments of 128 bytes (stream
+// s = bytes [1152 s, 1152 (s + 1)) of the ST; lane l owns streams l and l + 64,
+// packed as in roll_fast).  Iteration g rolls segment g of every stream: its
+// bytes land in LDS by LDS-DMA, one whole 128-byte line per stream (segments are
+// line-aligned: a 144-byte segment straddled lines, and the nt policy re-read
+// the shared lines from HBM, 1.7x slower); the window's state (S, T) and the
+// 64 packed byte pairs it drops next (Pd) stay in registers from segment g - 1.
+// Only segment 0 warms up (closed form) from the 64 bytes before each stream,
+// loaded into registers an iteration ahead.  Tile t of the ST = streams
+// 16 t .. 16 t + 15 = one 18 432-byte tile of the batch: the bookkeeping is the
+// scan's, each tile's candidates collected over the segments and published
+// when the ST ends.  LDS: piece q (16 B) of stream s sits at 16-byte slot
+// 8 s + (q ^ (s & 7)) (an XOR swizzle: a lane-stride of 128 B would put every
+// lane of a ds_read_b128 group in the same banks).  A dirty group is captured
+// right after it is rolled, from the packed pairs it added and dropped (still
+// in registers then) and its entry state.
 // ---------------------------------------------------------------------------
-constexpr int ST_G = 8;                       // segments per stream (tiles per ST)
+constexpr int ST_RUN = 128;                   // bytes per segment and stream
+constexpr int ST_SEGS = 9;                    // segments per stream: 1152-byte streams
+constexpr int ST_TILES = 8;                   // batch tiles per ST
 constexpr int ST_LISTCAP = 32;                // candidate slots per tile (more: dense)
 constexpr int ST_DIRTYCAP = 6;                // side slots per segment
+constexpr uint32_t ST_L = ST_SEGS * ST_RUN;   // stream bytes
+static_assert(16 * ST_L == (uint32_t)tile_bytes(DEFAULT_RUN), "16 streams = one batch tile");
 struct DirtySlotST {                          // 144 bytes
     uint32_t dp[16];                          // dropped bytes, packed pairs (run A low, run B high)
     uint32_t xp[16];                          // new bytes, packed pairs
@@ -744,32 +750,12 @@ struct DirtySlotST {                          // 144 bytes
     uint32_t pad;
 };
 static_assert(sizeof(DirtySlotST) == 144, "slot size");
-__host__ __device__ constexpr int st_lds_bytes(int run) {
-    return RUNS * run + ST_DIRTYCAP * (int)sizeof(DirtySlotST) + ST_G * ST_LISTCAP * 4 + ST_G * 4 + 16;
+__host__ __device__ constexpr int st_lds_bytes() {
+    return RUNS * ST_RUN + ST_DIRTYCAP * (int)sizeof(DirtySlotST) + ST_TILES * ST_LISTCAP * 4 + ST_TILES * 4 + 16;
 }
 
-template <int RUN>
-__device__ __forceinline__ uint32_t xpair(const uint32_t (&XA)[RUN / 4], const uint32_t (&XB)[RUN / 4], int j) {
+__device__ __forceinline__ uint32_t xpair32(const uint32_t (&XA)[ST_RUN / 4], const uint32_t (&XB)[ST_RUN / 4], int j) {
     return __builtin_amdgcn_perm(XB[j >> 2], XA[j >> 2], 0x0C040C00u + (uint32_t)(j & 3) * 0x00010001u);
-}
-
-// packed (S, T) of the 64 bytes words[q0 .. q0 + 15] of both runs (window_state's closed form)
-template <int N>
-__device__ __forceinline__ void window_at(const uint32_t (&A)[N], const uint32_t (&B)[N], const KParams &P, int q0,
-                                          uint32_t &S, u16x2 &Tv) {
-    uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        const uint32_t w = 0x3D3E3F40u - 0x04040404u * (uint32_t)m;
-        SA = __builtin_amdgcn_udot4(A[q0 + m], 0x01010101u, SA, false);
-        WA = __builtin_amdgcn_udot4(A[q0 + m], w, WA, false);
-        SB = __builtin_amdgcn_udot4(B[q0 + m], 0x01010101u, SB, false);
-        WB = __builtin_amdgcn_udot4(B[q0 + m], w, WB, false);
-    }
-    S = SA | (SB << 16);
-    const uint32_t tA = ((124993u + WA) * P.k) & 0xffffu;
-    const uint32_t tB = ((124993u + WB) * P.k) & 0xffffu;
-    Tv = as_u16x2(tA | (tB << 16));
 }
 
 // Publish one tile's list (n candidates, tile-relative positions) or mark it dense.
@@ -810,50 +796,47 @@ __device__ __forceinline__ void publish_list(const Tables &T, uint32_t tile, con
     }
 }
 
-template <int RUN, int MODE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
+template <int MODE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int RUN = ST_RUN;
     constexpr int NW = RUN / 4;                  // words per segment and run
     constexpr int NG = RUN / 16;                 // 16-byte groups per segment
-    constexpr int NP = RUNS * RUN / 16;          // 16-byte pieces per segment DMA (all streams)
-    constexpr int NQ = RUN / 16;                 // pieces per stream segment
-    constexpr uint32_t L = ST_G * RUN;           // stream bytes
+    constexpr uint32_t L = ST_L;
     constexpr uint32_t STB = RUNS * L;           // ST bytes
-    static_assert(NP % 64 == 0 && (RUN / 16) % 2 == 1, "DMA and conflict-free reads");
-    static_assert(ST_G * 16 == RUNS, "tile t of an ST = streams 16t .. 16t+15 = one batch tile");
+    constexpr int NDMA = RUNS * RUN / 1024;      // DMA instructions per segment (8 streams each)
     const int lane = threadIdx.x;
     uint8_t *wl = smem;
     DirtySlotST *dslots = (DirtySlotST *)(smem + RUNS * RUN);
     uint32_t *tlist = (uint32_t *)(smem + RUNS * RUN + ST_DIRTYCAP * sizeof(DirtySlotST));
-    uint32_t *tcnt = tlist + ST_G * ST_LISTCAP;
-    uint32_t *dcount = tcnt + ST_G;
+    uint32_t *tcnt = tlist + ST_TILES * ST_LISTCAP;
+    uint32_t *dcount = tcnt + ST_TILES;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
-    const uint32_t nst = (T.ntiles + ST_G - 1) / ST_G;
+    const uint32_t nst = (T.ntiles + ST_TILES - 1) / ST_TILES;
     const int64_t span = (int64_t)T.span;
-    // per-lane DMA offsets: instruction i (i < 2 NQ... NP/64) moves piece c = 64 i + lane:
-    // stream c / NQ, piece c % NQ; instructions i and i + NQ differ by 64 streams
-    uint32_t off[NQ];
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-        const uint32_t c = 64u * (uint32_t)i + (uint32_t)lane;
-        off[i] = (c / NQ) * L + (c % NQ) * 16u;
-    }
+    // DMA instruction i, lane l fills slot 64 i + l = stream 8 i + l / 8, physical piece l % 8,
+    // which holds logical piece (l % 8) ^ ((l / 8) & 7): a per-lane offset fixed for the kernel
+    const uint32_t dmaoff = ((uint32_t)lane >> 3) * L + ((((uint32_t)lane & 7u) ^ (((uint32_t)lane >> 3) & 7u)) << 4);
+    // this lane's stream (l) reads its piece q at byte 128 l + 16 (q ^ (l & 7)); stream l + 64 at + 8192
+    const uint32_t rbase = (uint32_t)lane * RUN, rsw = ((uint32_t)lane & 7u) << 4;
     auto issue_seg = [&](uint32_t st, uint32_t g) {
         const uint64_t b0 = (uint64_t)st * STB + (uint64_t)g * RUN;
-        if (b0 + STB - (uint64_t)g * RUN <= (uint64_t)span) {                   // whole ST inside the batch
+        if ((uint64_t)st * STB + STB <= (uint64_t)span) {            // whole ST inside the batch
 #pragma unroll
-            for (int i = 0; i < NP / 64; ++i) {
-                const uint64_t sb = (uint64_t)(data + b0 + (uint64_t)(i / NQ) * 64u * L);
+            for (int i = 0; i < NDMA; ++i) {
+                const uint64_t sb = (uint64_t)(data + b0 + (uint64_t)i * 8u * L);
                 const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb);
                 const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
-                dma16_s<(MODE & 4) != 0>(off[i % NQ], ((uint64_t)hi << 32) | lo, lds0 + 1024u * (uint32_t)i);
+                dma16_s<(MODE & 4) != 0>(dmaoff, ((uint64_t)hi << 32) | lo, lds0 + 1024u * (uint32_t)i);
             }
         } else {                                 // the batch's last ST: clamp (bytes past it are never recorded)
             const int64_t last = (int64_t)((span - 1) & ~15ll);
 #pragma unroll
-            for (int i = 0; i < NP / 64; ++i) {
-                int64_t a = (int64_t)b0 + (int64_t)(i / NQ) * 64 * L + off[i % NQ];
+            for (int i = 0; i < NDMA; ++i) {
+                uint32_t o = dmaoff;
+                asm volatile("" : "+v"(o));          // keep the 16 lane addresses out of the hot loop's registers
+                int64_t a = (int64_t)b0 + (int64_t)i * 8 * L + o;
                 a = a > last ? last : a;
                 dma16<(MODE & 4) != 0>(data + a, lds0 + 1024u * (uint32_t)i);
             }
@@ -879,38 +862,48 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     load_halo(st);
     uint32_t pend = 0, nextst = 0;
     DenseSlots dslots_alloc;
+    // (a ping-pong of two carried arrays, segments unrolled in pairs to drop the 64 moves
+    // below, measured slower: 3 copies of the roll overflow the instruction cache)
     uint32_t Pd[64];                               // packed pairs the window drops at positions 0..63
     uint32_t Sc = 0;                               // carried state
     u16x2 Tc = as_u16x2(0u);
     for (;;) {
 #pragma unroll 1
-        for (uint32_t g = 0; g < (uint32_t)ST_G; ++g) {
-            if (g == 0u) {
-                if (lane < ST_G) tcnt[lane] = 0u;
+        for (uint32_t g = 0; g < (uint32_t)ST_SEGS; ++g) {
+            const bool first = g == 0u;
+            if (first) {
+                if (lane < ST_TILES) tcnt[lane] = 0u;
                 if (lane == 0 && nst > gridDim.x) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);   // the next ST
             }
             if (lane == 0) *dcount = 0u;
             wait_vmcnt<0>();                                         // segment g landed (and, at 0, the halo)
-            if (g == 0u) {                                           // warm-up from the halo
-                window_at<16>(HA, HB, P, 0, Sc, Tc);
+            if (first) {                                             // warm-up from the halo (closed form)
+                uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) {
+                    const uint32_t w = 0x3D3E3F40u - 0x04040404u * (uint32_t)m;
+                    SA = __builtin_amdgcn_udot4(HA[m], 0x01010101u, SA, false);
+                    WA = __builtin_amdgcn_udot4(HA[m], w, WA, false);
+                    SB = __builtin_amdgcn_udot4(HB[m], 0x01010101u, SB, false);
+                    WB = __builtin_amdgcn_udot4(HB[m], w, WB, false);
+                }
+                Sc = SA | (SB << 16);
+                Tc = as_u16x2((((124993u + WA) * P.k) & 0xffffu) | ((((124993u + WB) * P.k) & 0xffffu) << 16));
 #pragma unroll
                 for (int j = 0; j < 64; ++j)
                     Pd[j] = __builtin_amdgcn_perm(HB[j >> 2], HA[j >> 2], 0x0C040C00u + (uint32_t)(j & 3) * 0x00010001u);
             }
             uint32_t XA[NW], XB[NW];
-            {
-                const uint4 *la = (const uint4 *)(wl + lane * RUN);
-                const uint4 *lb = (const uint4 *)(wl + (lane + 64) * RUN);
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const uint4 a = la[q], b = lb[q];
-                    XA[4 * q + 0] = a.x; XA[4 * q + 1] = a.y; XA[4 * q + 2] = a.z; XA[4 * q + 3] = a.w;
-                    XB[4 * q + 0] = b.x; XB[4 * q + 1] = b.y; XB[4 * q + 2] = b.z; XB[4 * q + 3] = b.w;
-                }
+            for (int q = 0; q < NW / 4; ++q) {
+                const uint32_t off = rbase + (((uint32_t)q << 4) ^ rsw);
+                const uint4 a = *(const uint4 *)(wl + off), b = *(const uint4 *)(wl + off + 64u * RUN);
+                XA[4 * q + 0] = a.x; XA[4 * q + 1] = a.y; XA[4 * q + 2] = a.z; XA[4 * q + 3] = a.w;
+                XB[4 * q + 0] = b.x; XB[4 * q + 1] = b.y; XB[4 * q + 2] = b.z; XB[4 * q + 3] = b.w;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // segment in registers: buffer free
             bool more = true;
-            if (g + 1 < (uint32_t)ST_G) {
+            if (g + 1 < (uint32_t)ST_SEGS) {
                 issue_seg(st, g + 1);
             } else {
                 nextst = nst > gridDim.x ? gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nst;
@@ -920,16 +913,13 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                     load_halo(nextst);
                 }
             }
-            // ---- roll segment g: positions 0..63 drop Pd, later ones this segment's own pairs.
-            // A group whose minimum T has a zero half is captured right after it is rolled, from
-            // the packed pairs it added and dropped (still in registers then) and its entry
-            // state: no raw word or pair has to outlive its last use in the roll.
+            // ---- roll segment g: positions 0..63 drop Pd, later ones this segment's own pairs
             const int64_t lim_rel = span - (int64_t)st * STB;         // ST-relative positions >= lim: not bytes
             const uint32_t relA0 = (uint32_t)lane * L + g * RUN;
             uint32_t S = Sc;
             u16x2 Tv = Tc;
-            bool dirty = false;                                      // (any dirty group: dense marking)
-            uint32_t xs[RUN];                                        // pairs of this segment (registers: unrolled)
+            bool dirty = false;
+            uint32_t xs[RUN];
 #pragma unroll
             for (int gg = 0; gg < NG; ++gg) {
                 const uint32_t S0 = S;
@@ -938,7 +928,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 #pragma unroll
                 for (int jj = 0; jj < 16; ++jj) {
                     const int j = gg * 16 + jj;
-                    xs[j] = xpair<RUN>(XA, XB, j);
+                    xs[j] = xpair32(XA, XB, j);
                     const uint32_t d = j < 64 ? Pd[j < 64 ? j : 0] : xs[j >= 64 ? j - 64 : 0];
                     S = S + xs[j] - d;
                     const u16x2 V = pk_mad(d, 0xFFC0FFC0u, as_u16x2(S));
@@ -992,7 +982,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 #pragma unroll
                     for (int t = 0; t < 4; ++t)
                         if ((bal >> (16 * t)) & 0xffffull) m |= (1u << t) | (1u << (t + 4));
-                    if (lane < ST_G && ((m >> lane) & 1u)) tcnt[lane] |= 0x80000000u;   // dense mark
+                    if (lane < ST_TILES && ((m >> lane) & 1u)) tcnt[lane] |= 0x80000000u;   // dense mark
                 }
                 const uint32_t nd = dc & 0xffffu;
                 if ((uint32_t)lane < nd) {
@@ -1001,6 +991,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                     uint32_t s = ds.S0;
                     u16x2 t = as_u16x2(ds.T0);
                     const uint32_t relA = ds.relA, relB = ds.relA + 64u * L;
+                    constexpr uint32_t TB = (uint32_t)tile_bytes(DEFAULT_RUN);
                     for (int jj = 0; jj < 16; ++jj) {
                         const uint32_t x = ds.xp[jj];
                         const uint32_t d = ds.dp[jj];
@@ -1008,24 +999,24 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                         t = as_u16x2(s) * kk + t;
                         t = as_u16x2(d) * km + t;
                         if (t.x == 0 && ((1984u + (s & 0xffffu)) & P.m1) == P.m1 && (int64_t)(relA + jj) < lim_rel) {
-                            const uint32_t p = relA + jj, tt = p / (uint32_t)tile_bytes(RUN);
+                            const uint32_t p = relA + jj, tt = p / TB;
                             const uint32_t idx = atomicAdd(&tcnt[tt], 1u) & 0x7fffffffu;
-                            if (idx < (uint32_t)ST_LISTCAP) tlist[tt * ST_LISTCAP + idx] = p - tt * (uint32_t)tile_bytes(RUN);
+                            if (idx < (uint32_t)ST_LISTCAP) tlist[tt * ST_LISTCAP + idx] = p - tt * TB;
                         }
                         if (t.y == 0 && ((1984u + (s >> 16)) & P.m1) == P.m1 && (int64_t)(relB + jj) < lim_rel) {
-                            const uint32_t p = relB + jj, tt = p / (uint32_t)tile_bytes(RUN);
+                            const uint32_t p = relB + jj, tt = p / TB;
                             const uint32_t idx = atomicAdd(&tcnt[tt], 1u) & 0x7fffffffu;
-                            if (idx < (uint32_t)ST_LISTCAP) tlist[tt * ST_LISTCAP + idx] = p - tt * (uint32_t)tile_bytes(RUN);
+                            if (idx < (uint32_t)ST_LISTCAP) tlist[tt * ST_LISTCAP + idx] = p - tt * TB;
                         }
                     }
                 }
             }
-            if (g + 1 == (uint32_t)ST_G) {                           // the ST's tiles are complete: publish
+            if (g + 1 == (uint32_t)ST_SEGS) {                        // the ST's tiles are complete: publish
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll 1
-                for (uint32_t t = 0; t < (uint32_t)ST_G; ++t) {
-                    const uint32_t tile = st * ST_G + t;
+                for (uint32_t t = 0; t < (uint32_t)ST_TILES; ++t) {
+                    const uint32_t tile = st * ST_TILES + t;
                     if (tile >= T.ntiles) break;
                     const uint32_t c = __builtin_amdgcn_readfirstlane(
                         __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)&tcnt[t], __ATOMIC_RELAXED,
@@ -3404,7 +3395,7 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
     else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 17u)                                        // A/B: stream-tile scan (exact)
-        hipLaunchKernelGGL((cdc_scan_st_kernel<RUN, 4>), dim3(grid), dim3(64), st_lds_bytes(RUN), s, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else if (p.ablate == 15u) {                                      // A/B: CU schedule (exact)
         launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s);
     } else if (p.ablate == 16u) {                                    // timing only: CU schedule, no warm-up/halo
