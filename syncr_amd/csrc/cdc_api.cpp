@@ -81,7 +81,7 @@ struct syncr_cdc {
     std::vector<uint64_t> h_foff, h_flen, h_cut_base;
     std::vector<uint32_t> h_cut_cap;
     DevBuf fstart, foff, flen, order, cut_base, cut_cap, tile_meta, slots, zeroed,
-        dense_list, dense_cnt, dense_bits, super_off, cand, linkw, cuts, counts;
+        dense_list, dense_cnt, dense_bits, dense_fix, super_off, cand, linkw, cuts, counts;
     // BLAKE3 of every chunk (launch_hashed)
     bool hash_on = false;
     uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 3, b3_nosplit = 0, b3_nouni = 0;     // dev A/B knobs; coop 3 = the product (LD_PAIR + quad merges)
@@ -229,6 +229,7 @@ Tables make_tables(syncr_cdc *h) {
     t.dense_cnt = h->dense_cnt.as<uint32_t>();
     t.dense_cap = h->dense_cap;
     t.dense_bits = h->dense_bits.as<uint32_t>();
+    t.dense_fix = h->dense_fix.as<uint8_t>();
     t.cand = h->cand.as<uint64_t>();
     // chain links only while the handle splits (periodic / low-entropy data):
     // random data never chains, and its fix-ups skip the link work
@@ -346,6 +347,7 @@ int32_t ensure_dense(syncr_cdc *h, uint32_t cap) {
     CHECK_HIP(h->dense_list.ensure(std::max<size_t>(cap, 1) * 4));
     CHECK_HIP(h->dense_cnt.ensure(std::max<size_t>(cap, 1) * 4));
     CHECK_HIP(h->dense_bits.ensure(std::max<size_t>(cap, 1) * (size_t)(scan_tile_bytes(h->geom) / 32) * 4));
+    CHECK_HIP(h->dense_fix.ensure(std::max<size_t>(cap, 1) * (size_t)FIXCAP));
     return SYNCR_CDC_OK;
 }
 
@@ -539,6 +541,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
             khz = 100000;
         h->kp.split_patience = (prm.flags & SYNCR_CDC_FLAG_SPLIT_NOWAIT) ? 0ull : 100ull * (uint64_t)khz;
     }
+    h->kp.dense_fuse = 1u;                      // dense pass computes its candidates' head fix-ups
 #ifdef SYNCR_CDC_DEV
     // Development library only (libsyncr_cdc_dev.so, used by tools/): variants
     // and timing-only ablations chosen by environment variables.  The product
@@ -555,6 +558,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_CDC_RESOLVE_PF")) h->kp.resolve_pf = (uint32_t)atoi(a);      // A/B only
     if (const char *a = getenv("SYNCR_CDC_SPLIT_FIRST")) h->kp.split_first = (uint32_t)atoi(a) != 0; // A/B only
     if (const char *a = getenv("SYNCR_CDC_NOSKIP")) h->kp.no_skip = atoi(a) != 0;                    // A/B only
+    if (const char *a = getenv("SYNCR_CDC_DENSE_FUSE")) h->kp.dense_fuse = atoi(a) != 0;           // A/B only
     if (const char *a = getenv("SYNCR_CDC_TRACE"))                                              // timeline
         if (atoi(a)) CHECK_HIP(h->dbg.ensure(DBG_WORDS * sizeof(uint64_t)));
     if (const char *a = getenv("SYNCR_CDC_SPLIT_SEGC")) h->split_segc = std::max(256, atoi(a));        // A/B only

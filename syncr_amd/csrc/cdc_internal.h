@@ -15,16 +15,24 @@ constexpr int RUNS = 128;                // runs per wave tile
 constexpr int HALO = 64;                 // window warm-up bytes before the tile
 constexpr int LISTCAP = 64;              // candidate slots per tile
 constexpr uint32_t DENSE_BIT = 0x80000000u;
+// dense pass with fused head fix-ups (cdc_dense_packed_kernel<RUN, true>): up to
+// FIXCAP fix-ups per dense tile, by candidate rank, in Tables::dense_fix; a tile
+// whose fix-ups are there has DENSE_FIXED in its dense_cnt word.  The LDS
+// buffer holds DENSE_TAIL bytes past the tile (the last candidates' windows).
+constexpr uint32_t FIXCAP = 1024;
+constexpr uint32_t FIX_RMAX = 6;
+constexpr uint32_t DENSE_FIXED = 0x80000000u;
+constexpr int DENSE_TAIL = 80;
 // Tables::coarse keeps one counter per 128-byte line: the waves of a launch
 // work through a window of nearby tiles, so their atomics meet on a few
 // counters, and counters sharing a line serialise in one L2 channel.
 constexpr uint32_t COARSE_STRIDE = 32;
 constexpr uint64_t NONE = ~0ull;
-// The scan's fine schedule (cdc_scan_kernel MODE bit 1024): the tiles are cut
-// into SCHED_REGIONS contiguous regions, each with its own counter; a wave takes
-// one tile at a time from its region and moves on to the next region once its
-// own is exhausted.
-constexpr uint32_t SCHED_REGIONS = 16;
+// Work counters zeroed per launch, one per 128-byte line (Tables::sched):
+// SCHED_SCAN_GROUP is the CU scan schedule's group counter, SCHED_DENSE_CHUNK
+// the dense pass's list-chunk counter.
+constexpr uint32_t SCHED_REGIONS = 4;
+enum { SCHED_SCAN_GROUP = 0, SCHED_DENSE_CHUNK = 1 };
 constexpr int DEFAULT_RUN = 144;
 
 // MFMA scan (cdc_scan_mfma_kernel): a wave tile is 32 streams x NB blocks of
@@ -50,6 +58,7 @@ struct ScanGeom {
 
 __host__ __device__ constexpr int tile_bytes(int run) { return run * RUNS; }
 __host__ __device__ constexpr int buf_bytes(int run) { return HALO + run * RUNS; }
+__host__ __device__ constexpr int dense_buf_bytes(int run, bool fuse) { return buf_bytes(run) + (fuse ? DENSE_TAIL : 0); }
 // LDS per wave: one tile landing buffer + 16 dirty-group slots (80 B) +
 // candidate list + counters
 __host__ __device__ constexpr int lds_wave_bytes(int run) { return buf_bytes(run) + 16 * 80 + LISTCAP * 4 + 16; }
@@ -99,6 +108,8 @@ struct KParams {
                                //   SYNCR_CDC_FLAG_SPLIT_NOWAIT)
     uint32_t split_first;      // 1: split workers take the resolve grid's first blocks (dev A/B: SYNCR_CDC_SPLIT_FIRST)
     uint32_t no_skip;          // 1: no run skips in the resolve walk (dev A/B: SYNCR_CDC_NOSKIP)
+    uint32_t dense_fuse;       // 1: the dense pass computes its candidates' head fix-ups (product; dev A/B:
+                               //   SYNCR_CDC_DENSE_FUSE=0)
     uint32_t resolve_pf;       // development library only (SYNCR_CDC_RESOLVE_PF): candidate windows
                                //   the resolve walk loads ahead (0: RESOLVE_PF)
 };
@@ -193,6 +204,7 @@ struct Tables {
     uint32_t *dense_cnt;           // [dense_cap] candidates per dense tile
     uint32_t dense_cap;
     uint32_t *dense_bits;          // [dense_cap * tile/32] candidate bitmaps
+    uint8_t *dense_fix;            // [dense_cap * FIXCAP] head fix-ups of dense tiles' candidates, by rank
     uint64_t *cand;                // [cand_cap] compacted sorted candidates
     uint64_t *linkw;               // [cand_cap / 64 + 4] CAND_LINK bits, 64 candidates per word (cdc_fix_kernel)
     uint64_t cand_cap;
@@ -217,8 +229,8 @@ struct Tables {
     uint32_t *split;               // [SPL_WORDS] counters                    (zeroed per launch)
     uint32_t dense_off;            // 1: no dense pass this launch (the handle has not seen a dense tile);
                                    //   the compaction counts dense tiles as empty and fetch re-runs if any
-    uint32_t *sched;               // [SCHED_REGIONS * COARSE_STRIDE] per-region tile counters of the scan's
-                                   //   fine schedule, one per 128-byte line (zeroed per launch)
+    uint32_t *sched;               // [SCHED_REGIONS * COARSE_STRIDE] work counters (SCHED_*), one per
+                                   //   128-byte line (zeroed per launch)
     RunJob *runs;                  // [runs_cap] deferred runs (only while split workers run)
     uint32_t runs_cap;
     uint32_t epoch;                // this launch's id (!= 0, unique in the process): SplitSeg::ready

@@ -328,11 +328,67 @@ struct DenseSlots {
     uint32_t lo = 0, hi = 0;       // the wave's unused slots [lo, hi) (wave-uniform)
 };
 
+// The product scan defers its dense tiles' list slots: a wave keeps up to
+// DPEND dense tiles in a register (lane i: the i-th) and takes their slots with
+// one atomic when the register is full or the wave ends.  Taking slots at the
+// tile (DenseSlots, 8 at a time) put a returning atomic on one counter in the
+// roll loop: its wait also drained the next tile's DMA, and on all-dense data
+// (dense1) the grid's first grabs queued on that one address (scan 81 us for
+// 128 MiB, 13 us per tile; tools/scan_timeline.py).  No slot is left unused.
+constexpr uint32_t DPEND = 64;
+struct DensePend {
+    uint32_t tile = 0;             // lane i < n: the wave's i-th pending dense tile
+    uint32_t n = 0;                // (wave-uniform)
+};
+__device__ __forceinline__ void dense_pend_flush(const Tables &T, DensePend &dp, int lane) {
+    if (dp.n == 0u) return;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&T.ctr[CTR_DENSE], dp.n);
+    base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
+    if ((uint32_t)lane < dp.n) {
+        const uint32_t idx = base + (uint32_t)lane;
+        if (idx < T.dense_cap) {
+            T.dense_list[idx] = dp.tile;
+            T.tile_meta[dp.tile] = DENSE_BIT | idx;
+        } else {
+            T.tile_meta[dp.tile] = DENSE_BIT | 0x7fffffffu;
+        }
+    }
+    if (lane == 0 && base + dp.n > T.dense_cap) atomicOr(&T.ctr[CTR_FLAGS], FLAG_DENSE_OVERFLOW);
+    dp.n = 0u;
+}
+__device__ __forceinline__ void dense_mark(const Tables &T, uint32_t tile, int lane, DensePend &dp) {
+    if ((uint32_t)lane == dp.n) dp.tile = tile;
+    if (++dp.n == DPEND) dense_pend_flush(T, dp, lane);
+}
+__device__ __forceinline__ void dense_mark(const Tables &T, uint32_t tile, int lane, DenseSlots &ds) {
+    if (ds.lo == ds.hi) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&T.ctr[CTR_DENSE], DENSE_CHUNK);
+        base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
+        ds.lo = base;
+        ds.hi = base + DENSE_CHUNK;
+        if ((uint32_t)lane < DENSE_CHUNK && base + (uint32_t)lane < T.dense_cap)
+            T.dense_list[base + (uint32_t)lane] = DENSE_HOLE;
+    }
+    const uint32_t idx = ds.lo++;
+    if (lane == 0) {
+        if (idx < T.dense_cap) {
+            T.dense_list[idx] = tile;
+            T.tile_meta[tile] = DENSE_BIT | idx;
+        } else {
+            T.tile_meta[tile] = DENSE_BIT | 0x7fffffffu;
+            atomicOr(&T.ctr[CTR_FLAGS], FLAG_DENSE_OVERFLOW);
+        }
+    }
+}
+
 // Publish this tile's candidates (sorted, with head fix-ups) or mark it dense.
+template <class DS>
 __device__ __forceinline__ void publish_tile(const uint8_t *__restrict__ data, const KParams &P,
                                              const Tables &T, uint32_t tile, int64_t t0,
                                              uint32_t *wlist, uint32_t *wcount, int lane,
-                                             bool force_dense, DenseSlots &ds) {
+                                             bool force_dense, DS &ds) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     // LDS-typed read: a generic (flat) read would wait vmcnt(0) on the tile DMA.
@@ -342,25 +398,7 @@ __device__ __forceinline__ void publish_tile(const uint8_t *__restrict__ data, c
     if (n == 0u && !force_dense) return;
     if (lane == 0) atomicOr(&T.nonempty[tile >> 6], 1ull << (tile & 63));
     if (n > (uint32_t)LISTCAP || force_dense) {
-        if (ds.lo == ds.hi) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&T.ctr[CTR_DENSE], DENSE_CHUNK);
-            base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
-            ds.lo = base;
-            ds.hi = base + DENSE_CHUNK;
-            if ((uint32_t)lane < DENSE_CHUNK && base + (uint32_t)lane < T.dense_cap)
-                T.dense_list[base + (uint32_t)lane] = DENSE_HOLE;
-        }
-        const uint32_t idx = ds.lo++;
-        if (lane == 0) {
-            if (idx < T.dense_cap) {
-                T.dense_list[idx] = tile;
-                T.tile_meta[tile] = DENSE_BIT | idx;
-            } else {
-                T.tile_meta[tile] = DENSE_BIT | 0x7fffffffu;
-                atomicOr(&T.ctr[CTR_FLAGS], FLAG_DENSE_OVERFLOW);
-            }
-        }
+        dense_mark(T, tile, lane, ds);
         return;
     }
     const uint32_t e = (uint32_t)lane < n ? wlist[lane] : 0xffffffffu;
@@ -452,7 +490,7 @@ __host__ __device__ constexpr bool scan_dynamic(uint32_t ntiles, uint32_t grid) 
 // WPB > 1 (the CU schedule): one workgroup of WPB waves per CU, each wave with
 // its own LDS region as above.  The CU takes groups of CU_GROUP consecutive
 // tiles -- its first group is its block index, later ones come from one global
-// counter (T.sched[0]), fetched a group ahead -- and its waves take the group's
+// counter (T.sched, SCHED_SCAN_GROUP), fetched a group ahead -- and its waves take the group's
 // tiles one at a time from an LDS counter.  The two waves of a SIMD do not run
 // at the same speed (per-wave rates differ up to 2x with the same mean on every
 // XCC, SE, CU and SIMD, tools/scan_timeline.py): a static share per wave ends
@@ -482,7 +520,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         if (threadIdx.x == 0) {
             *cu_next = (uint32_t)WPB;                                  // k < WPB: the waves' first tiles
             cu_grp[0] = (uint64_t)blockIdx.x + 1;                     // group 0: the block's own
-            const uint32_t g1 = gridDim.x + atomicAdd(&T.sched[0], 1u);
+            const uint32_t g1 = gridDim.x + atomicAdd(&T.sched[SCHED_SCAN_GROUP * COARSE_STRIDE], 1u);
             cu_grp[1] = (1ull << 32) | ((uint64_t)g1 + 1);
         }
         __syncthreads();
@@ -565,7 +603,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 wait_vmcnt<0>();
                 pf_store();
             }
-            if (lane == 0) pf_v = atomicAdd(&T.sched[0], 1u);
+            if (lane == 0) pf_v = atomicAdd(&T.sched[SCHED_SCAN_GROUP * COARSE_STRIDE], 1u);
             pf_pending = true;
             pf_j = k / CU_GROUP + 1;
         }
@@ -596,7 +634,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * wslot, wall_clock64());
     issue_tile<RUN, (MODE & 4) != 0>(data, T.span, tile, lds0, lane);
     uint32_t gj = 0, pend = 0;
-    DenseSlots dslots_alloc;
+    DensePend dslots_alloc;
 #ifdef SYNCR_CDC_DEV
     uint32_t ntile_done = 0;
 #endif
@@ -690,6 +728,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         if (nd && nd <= (uint32_t)DIRTYCAP) rewalk_dirty<RUN>(P, lane, nd, dslots, lim_rel, wcount, wlist);
         publish_tile(data, P, T, tile, t0, wlist, wcount, lane, nd > (uint32_t)DIRTYCAP, dslots_alloc);
     }
+    dense_pend_flush(T, dslots_alloc, lane);
     if constexpr (CUS) {
         if (pf_pending) {                                            // readers may wait for it
             wait_vmcnt<0>();
@@ -1471,16 +1510,26 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
 //   S += x; T += k S                    (T = ((s2 + 1) k) mod 2^16, s2 = 124992 + W)
 //   Z = ((S + 1985) & m1) | T           zero iff the digest test passes
 //   acc = 2 acc + sat(1 - Z)            16-position hit masks, first position in bit 15
-// and the first hit is the leading one of the 63-bit mask (clz).  ~3.5 VALU per
-// item-byte against ~9.5 for one item per thread with an exit per byte; the
-// dense workload has a candidate every 64 bytes (7.5 M per launch).
+// and the first hit is the leading one of the 63-bit mask (clz).  A T-only pass
+// (min of T over the 63 positions: 2 VALU per item-byte) runs first; only items
+// with a zero T (any at all: 63 / 2^16 at bits >= 16, 63 / 2^bits below) take
+// the exact pass (~3.5 VALU per item-byte).  The dense workload has a
+// candidate every 64 bytes (7.5 M per launch).
 // (Fusing fix-ups into the dense and gather launches -- no separate launch --
 // measured 8 us SLOWER per step on zipf10k: the per-lane serial fix-ups
 // lengthen the gather's critical path; profiles/r02_ab_run_fusefix.log.)
-__device__ __forceinline__ void fix_item(const Tables &T, uint64_t n, uint64_t i, uint64_t &a, uint32_t &cnt) {
+// known = the fix-up the dense pass already stored with a candidate (CAND_KNOWN), else ~0u
+__device__ __forceinline__ void fix_item(const Tables &T, uint64_t n, uint64_t i, uint64_t &a, uint32_t &cnt,
+                                         uint32_t &known) {
+    known = ~0u;
     if (i < n) {                                          // a candidate e: chunk starts at e + 1
-        a = (T.cand[i] & CAND_POS_MASK) + 1;
+        const uint64_t w = T.cand[i];
+        a = (w & CAND_POS_MASK) + 1;
         cnt = (uint32_t)min<uint64_t>(63ull, T.span > a ? T.span - a : 0ull);
+        if (w & CAND_KNOWN) {
+            known = (uint32_t)(w >> 48) & 0xffu;
+            cnt = 0u;
+        }
     } else if (i < n + T.ngrid) {                         // a grid point p: chunk starts at p, ends by the file's end
         a = T.gpos[i - n];
         const uint64_t end = T.gend[i - n];
@@ -1529,47 +1578,79 @@ __device__ __forceinline__ uint64_t spread32(uint32_t x) {
     return v;
 }
 
+// Head fix-ups of two items (A: the low halves, B: the high halves): the first
+// chunk-local hit among the first nA / nB of the 63 bytes in A[] / B[], + 1, or 0.
+__device__ __forceinline__ void fix_pair(const uint32_t (&A)[16], const uint32_t (&B)[16], uint32_t nA, uint32_t nB,
+                                         const KParams &P, uint32_t &fA, uint32_t &fB) {
+    const uint32_t m1x2 = P.m1 | (P.m1 << 16);
+    const uint32_t t0 = ((124993u * P.k) & 0xffffu) * 0x00010001u;   // T of an empty window, both halves
+    fA = 0u;
+    fB = 0u;
+    // fast pass: only T (the s2 test, exact for masks of <= 16 bits and the rarer half of
+    // wider ones) -- 4 VALU per position pair; a zero T anywhere sends the item to the
+    // exact pass (P(some T == 0 in 63) = 63 / 2^16 per item at bits >= 16)
+    {
+        uint32_t S = 0;
+        u16x2 Tv = as_u16x2(t0), mn = as_u16x2(0xffffffffu);
+#pragma unroll
+        for (int k = 0; k < 63; ++k) {
+            const uint32_t x = __builtin_amdgcn_perm(B[k >> 2], A[k >> 2], 0x0C040C00u + (uint32_t)(k & 3) * 0x00010001u);
+            S += x;
+            Tv = pk_mad(S, P.kk, Tv);
+            mn = __builtin_elementwise_min(mn, Tv);
+        }
+        const uint32_t m = as_u32(mn);
+        if (__builtin_expect((m & 0xffffu) == 0u || (m >> 16) == 0u, 0)) {
+            uint32_t acc[4];
+            S = 0;
+            Tv = as_u16x2(t0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                uint32_t mm = 0;
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj) {
+                    const int k = 16 * g + jj;
+                    if (k < 63) {
+                        const uint32_t x = __builtin_amdgcn_perm(B[k >> 2], A[k >> 2],
+                                                                 0x0C040C00u + (uint32_t)(k & 3) * 0x00010001u);
+                        S += x;                                       // halves < 2^15: no carry
+                        Tv = pk_mad(S, P.kk, Tv);                     // T += k S
+                        const uint32_t U = as_u32(as_u16x2(S) + (u16x2){(unsigned short)1985, (unsigned short)1985});
+                        const uint32_t Z = (U & m1x2) | as_u32(Tv);
+                        uint32_t h;
+                        asm volatile("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(h) : "s"(0x00010001u), "v"(Z));
+                        mm = as_u32(pk_mad(mm, 0x00020002u, as_u16x2(h)));   // mm = 2 mm + h
+                    } else {
+                        mm = as_u32(pk_mad(mm, 0x00020002u, as_u16x2(0u)));  // position 63: none
+                    }
+                }
+                acc[g] = mm;
+            }
+            fA = fix_first(acc[0] & 0xffffu, acc[1] & 0xffffu, acc[2] & 0xffffu, acc[3] & 0xffffu, nA);
+            fB = fix_first(acc[0] >> 16, acc[1] >> 16, acc[2] >> 16, acc[3] >> 16, nB);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict__ data, KParams P,
                                                       Tables T) {
     const uint64_t total = (uint64_t)T.ctr[CTR_CANDS_LO] | ((uint64_t)T.ctr[CTR_CANDS_HI] << 32);
     const uint64_t n = total < T.cand_cap ? total : T.cand_cap;
     const uint64_t items = n + T.ngrid;
-    const uint32_t m1x2 = P.m1 | (P.m1 << 16);
-    const uint32_t t0 = ((124993u * P.k) & 0xffffu) * 0x00010001u;   // T of an empty window, both halves
     for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; 2 * q < items; q += (uint64_t)gridDim.x * 256) {
         uint64_t aA, aB;
-        uint32_t nA, nB;
-        fix_item(T, n, 2 * q, aA, nA);
-        fix_item(T, n, 2 * q + 1, aB, nB);
-        uint32_t A[16], B[16];
-        fix_load(data, T.span, aA, nA, A);
-        fix_load(data, T.span, aB, nB, B);
-        uint32_t S = 0, acc[4];
-        u16x2 Tv = as_u16x2(t0);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            uint32_t m = 0;
-#pragma unroll
-            for (int jj = 0; jj < 16; ++jj) {
-                const int k = 16 * g + jj;
-                if (k < 63) {
-                    const uint32_t x = __builtin_amdgcn_perm(B[k >> 2], A[k >> 2],
-                                                             0x0C040C00u + (uint32_t)(k & 3) * 0x00010001u);
-                    S += x;                                               // halves < 2^15: no carry
-                    Tv = pk_mad(S, P.kk, Tv);                             // T += k S
-                    const uint32_t U = as_u32(as_u16x2(S) + (u16x2){(unsigned short)1985, (unsigned short)1985});
-                    const uint32_t Z = (U & m1x2) | as_u32(Tv);
-                    uint32_t h;
-                    asm volatile("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(h) : "s"(0x00010001u), "v"(Z));
-                    m = as_u32(pk_mad(m, 0x00020002u, as_u16x2(h)));     // m = 2 m + h
-                } else {
-                    m = as_u32(pk_mad(m, 0x00020002u, as_u16x2(0u)));    // position 63: none
-                }
-            }
-            acc[g] = m;
+        uint32_t nA, nB, kA, kB;
+        fix_item(T, n, 2 * q, aA, nA, kA);
+        fix_item(T, n, 2 * q + 1, aB, nB, kB);
+        uint32_t fA = 0u, fB = 0u;
+        if (__ballot(nA != 0u || nB != 0u)) {             // (candidates of the dense pass's tiles come known)
+            uint32_t A[16], B[16];
+            fix_load(data, T.span, aA, nA, A);
+            fix_load(data, T.span, aB, nB, B);
+            fix_pair(A, B, nA, nB, P, fA, fB);
         }
-        const uint32_t fA = fix_first(acc[0] & 0xffffu, acc[1] & 0xffffu, acc[2] & 0xffffu, acc[3] & 0xffffu, nA);
-        const uint32_t fB = fix_first(acc[0] >> 16, acc[1] >> 16, acc[2] >> 16, acc[3] >> 16, nB);
+        if (kA != ~0u) fA = kA;
+        if (kB != ~0u) fB = kB;
         // chain links (CAND_LINK): empty fix-up, next candidate 64 .. gapmax past
         const uint64_t gapmax = P.read_cap && P.read_cap < P.max_chunk ? P.read_cap : P.max_chunk;
         bool lA = false, lB = false;
@@ -1821,11 +1902,95 @@ __device__ __forceinline__ uint32_t sload_u32(const uint32_t *p) {
     return v;
 }
 
+// Head fix-ups of a dense tile's candidates from its bytes in the dense pass's
+// LDS buffer (see cdc_dense_packed_kernel): round k takes each lane's k-th
+// candidate of run A and of run B (rr: the roll's group masks, run A high), loads
+// the 63 bytes after each from LDS (17 aligned words + v_alignbyte) and rolls
+// them as the halves of packed registers (fix_pair).  Candidate ranks in the
+// tile: run order (runs 0..63 are the lanes' A, 64..127 their B), then position.
+// Returns false (nothing stored) when the tile is past FIXCAP candidates or a
+// run past FIX_RMAX.
 template <int RUN>
+__device__ __forceinline__ bool dense_fixups(const uint8_t *dbuf, const KParams &P, const Tables &T,
+                                             const uint32_t (&rr)[RUN / 16], uint32_t cnt, uint32_t idx, int64_t t0,
+                                             int lane) {
+    constexpr int NG = RUN / 16;
+    uint32_t cA = 0, cB = 0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        cA += (uint32_t)__builtin_popcount(rr[g] >> 16);
+        cB += (uint32_t)__builtin_popcount(rr[g] & 0xffffu);
+    }
+    uint32_t mx = cA > cB ? cA : cB;
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)mx, off);
+        mx = o > mx ? o : mx;
+    }
+    mx = (uint32_t)__builtin_amdgcn_readfirstlane(mx);
+    if (cnt > FIXCAP || mx > FIX_RMAX) return false;
+    const uint32_t iA = wave_incl_scan(cA, lane), iB = wave_incl_scan(cB, lane);
+    const uint32_t totA = (uint32_t)__builtin_amdgcn_readlane((int)iA, 63);
+    const uint32_t preA = iA - cA, preB = totA + iB - cB;
+    // the runs' masks, position j of the run = bit j
+    uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+    uint32_t a2 = 0, b2 = 0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const uint64_t ha = rr[g] >> 16, hb = rr[g] & 0xffffu;
+        if (g < 4) { a0 |= ha << (16 * g); b0 |= hb << (16 * g); }
+        else if (g < 8) { a1 |= ha << (16 * (g - 4)); b1 |= hb << (16 * (g - 4)); }
+        else { a2 |= (uint32_t)ha << (16 * (g - 8)); b2 |= (uint32_t)hb << (16 * (g - 8)); }
+    }
+    auto take = [](uint64_t &m0, uint64_t &m1, uint32_t &m2) -> int {
+        if (m0) { const int o = __builtin_ctzll(m0); m0 &= m0 - 1; return o; }
+        if (m1) { const int o = 64 + __builtin_ctzll(m1); m1 &= m1 - 1; return o; }
+        if (m2) { const int o = 128 + __builtin_ctz(m2); m2 &= m2 - 1; return o; }
+        return -1;
+    };
+    uint8_t *fx = T.dense_fix + (size_t)idx * FIXCAP;
+    const int64_t span = (int64_t)T.span;
+    auto window = [&](int run, int o, uint32_t &n, uint32_t (&w)[16]) {
+        const uint32_t rel = (uint32_t)(run * RUN + o + 1);              // tile-relative chunk start
+        const uint32_t off = o < 0 ? 0u : (uint32_t)HALO + rel;         // its LDS byte
+        const int64_t left = span - (t0 + (int64_t)rel);
+        n = o < 0 ? 0u : (uint32_t)(left >= 63 ? 63 : (left > 0 ? left : 0));
+        const uint32_t *src = (const uint32_t *)(dbuf + (off & ~3u));
+        const uint32_t sh = off & 3u;
+        uint32_t W[17];
+#pragma unroll
+        for (int i = 0; i < 17; ++i) W[i] = src[i];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_alignbyte(W[i + 1], W[i], sh);
+    };
+    for (uint32_t k = 0; k < mx; ++k) {
+        const int oA = take(a0, a1, a2), oB = take(b0, b1, b2);
+        uint32_t XA[16], XB[16], nA, nB, fA, fB;
+        window(lane, oA, nA, XA);
+        window(lane + 64, oB, nB, XB);
+        fix_pair(XA, XB, nA, nB, P, fA, fB);
+        if (oA >= 0) fx[preA + k] = (uint8_t)fA;
+        if (oB >= 0) fx[preB + k] = (uint8_t)fB;
+    }
+    return true;
+}
+
+// FUSE (the product, round 4): the head fix-ups of the tile's candidates are
+// computed here, from the tile's bytes still in LDS, and stored by rank
+// (dense_fix, DENSE_FIXED in dense_cnt); cdc_gather_kernel writes them into the
+// candidates (CAND_KNOWN) and cdc_fix_kernel skips them.  The fix kernel had
+// re-read 63 bytes per candidate from HBM (0.40 GB per launch of the dense
+// workload, 0.84x its periodic bytes: profiles/r04jdense_pmc_traffic.json).
+// The buffer then holds 80 bytes past the tile (the windows of its last
+// candidates), and the next tile's DMA is issued after the fix-ups: the
+// other wave of the SIMD covers its latency.  A tile with more than FIXCAP
+// candidates, or a run with more than FIX_RMAX, keeps the separate fix-ups
+// (the rounds below go by the fullest run: ~0.4 us per round).
+template <int RUN, bool FUSE>
 __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__restrict__ data, KParams P,
                                                               Tables T) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t dbuf[];   // [HALO + tile]
+    extern __shared__ __attribute__((aligned(16))) uint8_t dbuf[];   // [HALO + tile (+ DENSE_TAIL)]
     constexpr int TILE = tile_bytes(RUN), NQ = (HALO + RUN) / 16, NG = RUN / 16;
+    constexpr int BUFD = dense_buf_bytes(RUN, FUSE);
     const int lane = threadIdx.x;
     const uint32_t nd = min(sload_u32(&T.ctr[CTR_DENSE]), T.dense_cap);
     // Block b takes the contiguous list range [b*per, (b+1)*per): the list is
@@ -1846,7 +2011,7 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
         tile = sload_u32(&T.dense_list[idx]);
     }
     uint32_t cur_c = tile >> 12, acc_c = 0, ndone = 0;
-    issue_tile<RUN, true>(data, T.span, tile, lds0, lane);
+    issue_buf<BUFD, TILE, true>(data, T.span, tile, lds0, lane);
     for (uint32_t next; idx < iend; idx = next) {
         next = idx + 1;
         uint32_t ntile = DENSE_HOLE;
@@ -1864,14 +2029,22 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // runs are in registers
-        if (next < iend) issue_tile<RUN, true>(data, T.span, ntile, lds0, lane);
+        if (!FUSE && next < iend) issue_buf<BUFD, TILE, true>(data, T.span, ntile, lds0, lane);
         const int64_t t0 = (int64_t)tile * TILE;
         uint16_t *bm = (uint16_t *)(T.dense_bits + (size_t)idx * (TILE / 32));
+        uint32_t rr[NG];
         uint32_t cnt = dense_roll<RUN>(A, B, P, lane, span - t0, [&](int g, uint32_t r) {
             bm[lane * NG + g] = (uint16_t)(r >> 16);
             bm[(lane + 64) * NG + g] = (uint16_t)r;
+            rr[g] = r;
         });
         for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+        bool fixed = false;
+        if constexpr (FUSE) {
+            fixed = dense_fixups<RUN>(dbuf, P, T, rr, cnt, idx, t0, lane);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // the fix-ups' LDS reads are done
+            if (next < iend) issue_buf<BUFD, TILE, true>(data, T.span, ntile, lds0, lane);
+        }
         if ((tile >> 12) != cur_c) {
             if (lane == 0 && acc_c) atomicAdd(&T.coarse[cur_c * COARSE_STRIDE], acc_c);
             cur_c = tile >> 12;
@@ -1880,7 +2053,7 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
         acc_c += cnt;
         ++ndone;
         if (lane == 0) {
-            T.dense_cnt[idx] = cnt;
+            T.dense_cnt[idx] = cnt | (fixed ? DENSE_FIXED : 0u);
             atomicAdd(&T.super_cnt[tile >> 6], cnt);
         }
         tile = ntile;
@@ -1935,7 +2108,7 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
             const uint32_t meta = T.tile_meta[tl];
             if (meta & DENSE_BIT) {
                 const uint32_t di = meta & ~DENSE_BIT;
-                c = di < T.dense_cap ? T.dense_cnt[di] : 0u;
+                c = di < T.dense_cap ? T.dense_cnt[di] & ~DENSE_FIXED : 0u;
             } else {
                 c = meta;
             }
@@ -1947,6 +2120,9 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
         if (!tc || tb + tc > T.cand_cap) continue;                // overflow: flagged by prefix, re-run
         const uint32_t *bm = T.dense_bits + (size_t)idx * nw;
         const uint64_t t0 = (uint64_t)tile * T.tile;
+        // fix-ups from the dense pass (DENSE_FIXED): rank r's is dense_fix[idx * FIXCAP + r]
+        const bool fixed = (T.dense_cnt[idx] & DENSE_FIXED) != 0u;
+        const uint8_t *fx = T.dense_fix + (size_t)idx * FIXCAP;
         uint64_t o = tb;
         for (uint32_t b0 = 0; b0 < nw; b0 += 64) {
             const uint32_t wi = b0 + (uint32_t)lane;
@@ -1955,7 +2131,9 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
             const uint32_t ic = wave_incl_scan(pc, lane);
             uint64_t q = o + (ic - pc);
             while (m) {
-                T.cand[q++] = t0 + wi * 32u + (uint32_t)__builtin_ctz(m);
+                const uint64_t pos = t0 + wi * 32u + (uint32_t)__builtin_ctz(m);
+                T.cand[q] = fixed ? pos | ((uint64_t)fx[q - tb] << 48) | CAND_KNOWN : pos;
+                ++q;
                 m &= m - 1;
             }
             o += (uint32_t)__builtin_amdgcn_readlane((int)ic, 63);
@@ -1994,7 +2172,7 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
         meta = T.tile_meta[tile];
         if (meta & DENSE_BIT) {
             const uint32_t idx = meta & ~DENSE_BIT;
-            c = (!T.dense_off && idx < T.dense_cap) ? T.dense_cnt[idx] : 0u;
+            c = (!T.dense_off && idx < T.dense_cap) ? T.dense_cnt[idx] & ~DENSE_FIXED : 0u;
         } else {
             c = meta;
         }
@@ -3524,8 +3702,12 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
     } else if (t.dense_off) {
         // no dense tile seen yet on this handle: no dense launch (fetch re-runs if needed)
     } else if (t.tile == (uint32_t)tile_bytes(DEFAULT_RUN)) {
-        hipLaunchKernelGGL(cdc_dense_packed_kernel<DEFAULT_RUN>, dim3(dblocks), dim3(64), buf_bytes(DEFAULT_RUN), s,
-                           d, p, t);
+        if (p.dense_fuse)
+            hipLaunchKernelGGL((cdc_dense_packed_kernel<DEFAULT_RUN, true>), dim3(dblocks), dim3(64),
+                               dense_buf_bytes(DEFAULT_RUN, true), s, d, p, t);
+        else
+            hipLaunchKernelGGL((cdc_dense_packed_kernel<DEFAULT_RUN, false>), dim3(dblocks), dim3(64),
+                               dense_buf_bytes(DEFAULT_RUN, false), s, d, p, t);
     } else {                                          // other scan geometries (development library)
 #ifdef SYNCR_CDC_DEV
         hipLaunchKernelGGL(cdc_dense_kernel, dim3(dblocks), dim3(64), HALO + t.tile, s, d, p, t);

@@ -13,7 +13,7 @@ of W+K back-to-back launches (and for the first launch after a host gap):
   resolve start    the resolve kernel's first stamp after the last scan wave's exit
                    (dense pass, compaction, fix-ups and the launch gaps between)
 
-    python tools/scan_timeline.py [--workload uniform1k|shard8|zipf10k] [--shard R]
+    python tools/scan_timeline.py [--workload uniform1k|shard8|zipf10k|dense1] [--shard R]
 """
 import argparse
 import ctypes
@@ -43,6 +43,8 @@ def table(name, shard):
     if name == "uniform1k":
         lens = np.full(1024, 1 << 20, np.uint64)
         return lens, np.arange(1024, dtype=np.uint64)
+    if name == "dense1":
+        return np.full(1, 128 << 20, np.uint64), np.arange(1, dtype=np.uint64)
     if name == "shard8":
         sh = WL.lpt_shard(sizes, 8)[shard]
         return sizes[sh], sh.astype(np.uint64)
@@ -109,7 +111,7 @@ def summarize(d, grid):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="uniform1k", choices=["uniform1k", "shard8", "zipf10k"])
+    ap.add_argument("--workload", default="uniform1k", choices=["uniform1k", "shard8", "zipf10k", "dense1"])
     ap.add_argument("--shard", type=int, default=0)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
@@ -124,7 +126,10 @@ def main():
     with syncr_amd.Chunker() as c:
         buf = syncr_amd.DeviceBuffer(c, span)
         try:
-            buf.gen_corpus(offs, lens, indices=idx)
+            if args.workload == "dense1":
+                buf.upload(np.resize(WL.periodic_pattern(), span))
+            else:
+                buf.gen_corpus(offs, lens, indices=idx)
             c.plan(offs, lens, span)
             info = c.info()
             grid = min(info["scan_grid"], (span + info["tile_bytes"] - 1) // info["tile_bytes"])
