@@ -519,6 +519,10 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     if constexpr (CUS) {
         if (threadIdx.x == 0) {
             *cu_next = (uint32_t)WPB;                                  // k < WPB: the waves' first tiles
+            // LDS is not cleared between workgroups: a slot left by an earlier
+            // launch on this CU can hold the very tag a wave waits for, so every
+            // slot starts with a tag no group has
+            for (uint32_t j = 2; j < CU_NSLOT; ++j) cu_grp[j] = ~0ull;
             cu_grp[0] = (uint64_t)blockIdx.x + 1;                     // group 0: the block's own
             const uint32_t g1 = gridDim.x + atomicAdd(&T.sched[SCHED_SCAN_GROUP * COARSE_STRIDE], 1u);
             cu_grp[1] = (1ull << 32) | ((uint64_t)g1 + 1);

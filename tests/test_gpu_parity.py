@@ -661,3 +661,43 @@ def test_launches_on_alternating_streams():
                 assert all(ends_of(g) == w for g, w in zip(ch.fetch(), want))
         finally:
             d.free()
+
+
+def test_small_batches_back_to_back_stable():
+    """Small batches run the CU scan schedule (a workgroup per CU, a ring of
+    group ids in LDS).  LDS survives between workgroups: a ring slot left by an
+    earlier launch on the same CU once carried the tag a wave was waiting for,
+    and the wave scanned a stale group (lost and doubled tiles: 2 of 10 000
+    files wrong in the bench's ingest leg).  Two handles with batches of
+    different sizes (last rows of their groups mostly past the batch end)
+    launch back to back, 12 times each; every launch equals the oracle."""
+    sizes = [(211, (1 << 20) + 4093), (97, (1 << 20) - 777)]
+    hs, bufs, refs, plans = [], [], [], []
+    try:
+        for nfiles, flen in sizes:
+            ch = syncr_amd.Chunker(chunk_bits=20, max_chunk=16 << 20, read_cap=2 << 20)
+            hs.append(ch)
+            lens = np.full(nfiles, flen, np.uint64)
+            offs = np.arange(nfiles, dtype=np.uint64) * np.uint64(flen)
+            span = int(lens.sum())
+            buf = syncr_amd.DeviceBuffer(ch, span)
+            bufs.append(buf)
+            buf.gen_corpus(offs, lens, indices=np.arange(nfiles, dtype=np.uint64) + 7 * nfiles)
+            ch.plan(offs, lens, span)
+            host = buf.download(span)
+            refs.append([r.tolist() for r in O.chunk_batch(host, offs, lens, read_cap=2 << 20,
+                                                           mode=O.MODE_PRODUCTION)])
+            plans.append(nfiles)
+            del host
+        for it in range(12):
+            for k, ch in enumerate(hs):
+                ch.launch(bufs[k].ptr)
+            for k, ch in enumerate(hs):
+                res = ch.fetch()
+                bad = [i for i in range(plans[k]) if ends_of(res[i]) != refs[k][i]]
+                assert not bad, (it, k, bad[:5])
+    finally:
+        for b in bufs:
+            b.free()
+        for ch in hs:
+            ch.close()

@@ -21,8 +21,11 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print("value", d["value"], "ms", d["ms_per_step"], "frac", d["roofline"]["frac"], "hashed", d["hashed"]["value"])
 print("parity", json.dumps(d["parity"].get("summary")))
-for k in ("uniform1k", "dedup", "dense", "ingest"):
+for k in ("uniform1k", "dedup", "dense", "ingest", "ingest_files", "h2d_probe"):
     v = d.get(k) or {}
-    print(k, {x: v.get(x) for x in ("value", "ms_per_step", "scan_frac", "error")})
+    print(k, {x: v.get(x) for x in ("value", "ms_per_step", "scan_frac", "frac_of_h2d", "host_stage_seconds", "error")})
+s8 = d.get("shard8") or {}
+print("shard8", {x: s8.get(x) for x in ("mean_step_frac", "mean_scan_frac", "max_step_ms", "projected_n8_value", "error")})
+print("sustained", (d.get("sustained") or {}).get("value"))
 print("legs_seconds", d.get("legs_seconds"))
 PY
