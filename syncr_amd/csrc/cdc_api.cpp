@@ -81,7 +81,7 @@ struct syncr_cdc {
     std::vector<uint64_t> h_foff, h_flen, h_cut_base;
     std::vector<uint32_t> h_cut_cap;
     DevBuf fstart, foff, flen, order, cut_base, cut_cap, tile_meta, slots, zeroed,
-        dense_list, dense_cnt, dense_bits, dense_fix, super_off, cand, linkw, cuts, counts;
+        dense_list, dense_cnt, dense_bits, dense_fix, dense_pos, super_off, cand, linkw, cuts, counts;
     // BLAKE3 of every chunk (launch_hashed)
     bool hash_on = false;
     uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 3, b3_nosplit = 0, b3_nouni = 0;     // dev A/B knobs; coop 3 = the product (LD_PAIR + quad merges)
@@ -230,6 +230,7 @@ Tables make_tables(syncr_cdc *h) {
     t.dense_cap = h->dense_cap;
     t.dense_bits = h->dense_bits.as<uint32_t>();
     t.dense_fix = h->dense_fix.as<uint8_t>();
+    t.dense_pos = h->dense_pos.as<uint16_t>();
     t.cand = h->cand.as<uint64_t>();
     // chain links only while the handle splits (periodic / low-entropy data):
     // random data never chains, and its fix-ups skip the link work
@@ -348,6 +349,7 @@ int32_t ensure_dense(syncr_cdc *h, uint32_t cap) {
     CHECK_HIP(h->dense_cnt.ensure(std::max<size_t>(cap, 1) * 4));
     CHECK_HIP(h->dense_bits.ensure(std::max<size_t>(cap, 1) * (size_t)(scan_tile_bytes(h->geom) / 32) * 4));
     CHECK_HIP(h->dense_fix.ensure(std::max<size_t>(cap, 1) * (size_t)FIXCAP));
+    CHECK_HIP(h->dense_pos.ensure(std::max<size_t>(cap, 1) * (size_t)FIXCAP * 2));
     return SYNCR_CDC_OK;
 }
 

@@ -16,8 +16,9 @@ constexpr int HALO = 64;                 // window warm-up bytes before the tile
 constexpr int LISTCAP = 64;              // candidate slots per tile
 constexpr uint32_t DENSE_BIT = 0x80000000u;
 // dense pass with fused head fix-ups (cdc_dense_packed_kernel<RUN, true>): up to
-// FIXCAP fix-ups per dense tile, by candidate rank, in Tables::dense_fix; a tile
-// whose fix-ups are there has DENSE_FIXED in its dense_cnt word.  The LDS
+// FIXCAP fix-ups per dense tile, by candidate rank, in Tables::dense_fix (and the
+// candidates' positions in Tables::dense_pos: no bitmap); a tile whose fix-ups are
+// there has DENSE_FIXED in its dense_cnt word.  The LDS
 // buffer holds DENSE_TAIL bytes past the tile (the last candidates' windows).
 constexpr uint32_t FIXCAP = 1024;
 constexpr uint32_t FIX_RMAX = 6;
@@ -205,6 +206,7 @@ struct Tables {
     uint32_t dense_cap;
     uint32_t *dense_bits;          // [dense_cap * tile/32] candidate bitmaps
     uint8_t *dense_fix;            // [dense_cap * FIXCAP] head fix-ups of dense tiles' candidates, by rank
+    uint16_t *dense_pos;           // [dense_cap * FIXCAP] their tile-relative positions (DENSE_FIXED tiles)
     uint64_t *cand;                // [cand_cap] compacted sorted candidates
     uint64_t *linkw;               // [cand_cap / 64 + 4] CAND_LINK bits, 64 candidates per word (cdc_fix_kernel)
     uint64_t cand_cap;

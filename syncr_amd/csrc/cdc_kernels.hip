@@ -1952,6 +1952,7 @@ __device__ __forceinline__ bool dense_fixups(const uint8_t *dbuf, const KParams 
         return -1;
     };
     uint8_t *fx = T.dense_fix + (size_t)idx * FIXCAP;
+    uint16_t *ps = T.dense_pos + (size_t)idx * FIXCAP;
     const int64_t span = (int64_t)T.span;
     auto window = [&](int run, int o, uint32_t &n, uint32_t (&w)[16]) {
         const uint32_t rel = (uint32_t)(run * RUN + o + 1);              // tile-relative chunk start
@@ -1972,8 +1973,14 @@ __device__ __forceinline__ bool dense_fixups(const uint8_t *dbuf, const KParams 
         window(lane, oA, nA, XA);
         window(lane + 64, oB, nB, XB);
         fix_pair(XA, XB, nA, nB, P, fA, fB);
-        if (oA >= 0) fx[preA + k] = (uint8_t)fA;
-        if (oB >= 0) fx[preB + k] = (uint8_t)fB;
+        if (oA >= 0) {
+            fx[preA + k] = (uint8_t)fA;
+            ps[preA + k] = (uint16_t)(lane * RUN + oA);
+        }
+        if (oB >= 0) {
+            fx[preB + k] = (uint8_t)fB;
+            ps[preB + k] = (uint16_t)((lane + 64) * RUN + oB);
+        }
     }
     return true;
 }
@@ -2038,16 +2045,27 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
         uint16_t *bm = (uint16_t *)(T.dense_bits + (size_t)idx * (TILE / 32));
         uint32_t rr[NG];
         uint32_t cnt = dense_roll<RUN>(A, B, P, lane, span - t0, [&](int g, uint32_t r) {
-            bm[lane * NG + g] = (uint16_t)(r >> 16);
-            bm[(lane + 64) * NG + g] = (uint16_t)r;
+            if constexpr (!FUSE) {
+                bm[lane * NG + g] = (uint16_t)(r >> 16);
+                bm[(lane + 64) * NG + g] = (uint16_t)r;
+            }
             rr[g] = r;
         });
         for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
         bool fixed = false;
         if constexpr (FUSE) {
+            // a tile whose fix-ups are stored gets its candidates as a position list
+            // (dense_pos, 2 B per candidate) instead of the bitmap (TILE / 8 bytes)
             fixed = dense_fixups<RUN>(dbuf, P, T, rr, cnt, idx, t0, lane);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // the fix-ups' LDS reads are done
             if (next < iend) issue_buf<BUFD, TILE, true>(data, T.span, ntile, lds0, lane);
+            if (!fixed) {
+#pragma unroll
+                for (int g = 0; g < NG; ++g) {
+                    bm[lane * NG + g] = (uint16_t)(rr[g] >> 16);
+                    bm[(lane + 64) * NG + g] = (uint16_t)rr[g];
+                }
+            }
         }
         if ((tile >> 12) != cur_c) {
             if (lane == 0 && acc_c) atomicAdd(&T.coarse[cur_c * COARSE_STRIDE], acc_c);
@@ -2124,9 +2142,14 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
         if (!tc || tb + tc > T.cand_cap) continue;                // overflow: flagged by prefix, re-run
         const uint32_t *bm = T.dense_bits + (size_t)idx * nw;
         const uint64_t t0 = (uint64_t)tile * T.tile;
-        // fix-ups from the dense pass (DENSE_FIXED): rank r's is dense_fix[idx * FIXCAP + r]
-        const bool fixed = (T.dense_cnt[idx] & DENSE_FIXED) != 0u;
-        const uint8_t *fx = T.dense_fix + (size_t)idx * FIXCAP;
+        if (T.dense_cnt[idx] & DENSE_FIXED) {
+            // the dense pass stored rank r's position and head fix-up (dense_pos / dense_fix)
+            const uint16_t *ps = T.dense_pos + (size_t)idx * FIXCAP;
+            const uint8_t *fx = T.dense_fix + (size_t)idx * FIXCAP;
+            for (uint32_t r = (uint32_t)lane; r < tc; r += 64)
+                T.cand[tb + r] = (t0 + ps[r]) | ((uint64_t)fx[r] << 48) | CAND_KNOWN;
+            continue;
+        }
         uint64_t o = tb;
         for (uint32_t b0 = 0; b0 < nw; b0 += 64) {
             const uint32_t wi = b0 + (uint32_t)lane;
@@ -2135,9 +2158,7 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
             const uint32_t ic = wave_incl_scan(pc, lane);
             uint64_t q = o + (ic - pc);
             while (m) {
-                const uint64_t pos = t0 + wi * 32u + (uint32_t)__builtin_ctz(m);
-                T.cand[q] = fixed ? pos | ((uint64_t)fx[q - tb] << 48) | CAND_KNOWN : pos;
-                ++q;
+                T.cand[q++] = t0 + wi * 32u + (uint32_t)__builtin_ctz(m);
                 m &= m - 1;
             }
             o += (uint32_t)__builtin_amdgcn_readlane((int)ic, 63);
