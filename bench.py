@@ -560,12 +560,13 @@ def main(argv=None):
 
     scan_ms = kms[0] / max(nl, 1)
     achieved = span / (scan_ms / 1e3) / 1e9 if scan_ms > 0 else 0.0
-    tr = load_traffic(args.workload, span, engine_info["run_bytes"])
+    scan_kernel = ch.scan_kernel_for(span)
+    tr = load_traffic(args.workload, span, engine_info["run_bytes"], kernel="cdc::" + scan_kernel)
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": (int(tr["hbm_bytes_per_launch"]) if tr else None),
-        "kernel": engine_info["scan_kernel"], "kernel_ms": round(scan_ms, 4),
+        "kernel": scan_kernel, "kernel_ms": round(scan_ms, 4),
         "algorithmic_bytes_per_launch": span,
         "dense_ms": round(pms[1] / max(pn, 1), 4), "resolve_ms": round(pms[2] / max(pn, 1), 4),
         "hash_ms": round(pms[3] / max(pn, 1), 4) if head_hashed else None,

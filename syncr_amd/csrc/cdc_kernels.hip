@@ -802,30 +802,13 @@ __device__ __forceinline__ uint32_t xpair32(const uint32_t (&XA)[ST_RUN / 4], co
 }
 
 // Publish one tile's list (n candidates, tile-relative positions) or mark it dense.
+template <class DS>
 __device__ __forceinline__ void publish_list(const Tables &T, uint32_t tile, const uint32_t *list, uint32_t n,
-                                             int lane, bool force_dense, DenseSlots &ds) {
+                                             int lane, bool force_dense, DS &ds) {
     if (n == 0u && !force_dense) return;
     if (lane == 0) atomicOr(&T.nonempty[tile >> 6], 1ull << (tile & 63));
     if (n > (uint32_t)ST_LISTCAP || force_dense) {
-        if (ds.lo == ds.hi) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&T.ctr[CTR_DENSE], DENSE_CHUNK);
-            base = (uint32_t)__builtin_amdgcn_readfirstlane(base);
-            ds.lo = base;
-            ds.hi = base + DENSE_CHUNK;
-            if ((uint32_t)lane < DENSE_CHUNK && base + (uint32_t)lane < T.dense_cap)
-                T.dense_list[base + (uint32_t)lane] = DENSE_HOLE;
-        }
-        const uint32_t idx = ds.lo++;
-        if (lane == 0) {
-            if (idx < T.dense_cap) {
-                T.dense_list[idx] = tile;
-                T.tile_meta[tile] = DENSE_BIT | idx;
-            } else {
-                T.tile_meta[tile] = DENSE_BIT | 0x7fffffffu;
-                atomicOr(&T.ctr[CTR_FLAGS], FLAG_DENSE_OVERFLOW);
-            }
-        }
+        dense_mark(T, tile, lane, ds);
         return;
     }
     const uint32_t e = (uint32_t)lane < n ? list[lane] : 0xffffffffu;
@@ -854,7 +837,6 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     DirtySlotST *dslots = (DirtySlotST *)(smem + RUNS * RUN);
     uint32_t *tlist = (uint32_t *)(smem + RUNS * RUN + ST_DIRTYCAP * sizeof(DirtySlotST));
     uint32_t *tcnt = tlist + ST_TILES * ST_LISTCAP;
-    uint32_t *dcount = tcnt + ST_TILES;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
     const uint32_t nst = (T.ntiles + ST_TILES - 1) / ST_TILES;
     const int64_t span = (int64_t)T.span;
@@ -904,12 +886,13 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     issue_seg(st, 0);
     load_halo(st);
     uint32_t pend = 0, nextst = 0;
-    DenseSlots dslots_alloc;
+    DensePend dslots_alloc;
     // (a ping-pong of two carried arrays, segments unrolled in pairs to drop the 64 moves
     // below, measured slower: 3 copies of the roll overflow the instruction cache)
     uint32_t Pd[64];                               // packed pairs the window drops at positions 0..63
     uint32_t Sc = 0;                               // carried state
     u16x2 Tc = as_u16x2(0u);
+    uint32_t dmark = 0;                            // tiles (bit t) holding a dirty group no slot took
     for (;;) {
 #pragma unroll 1
         for (uint32_t g = 0; g < (uint32_t)ST_SEGS; ++g) {
@@ -918,7 +901,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 if (lane < ST_TILES) tcnt[lane] = 0u;
                 if (lane == 0 && nst > gridDim.x) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);   // the next ST
             }
-            if (lane == 0) *dcount = 0u;
+            uint32_t have = 0;                                       // dirty slots taken (wave-uniform)
             wait_vmcnt<0>();                                         // segment g landed (and, at 0, the halo)
             if (first) {                                             // warm-up from the halo (closed form)
                 uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
@@ -961,7 +944,6 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             const uint32_t relA0 = (uint32_t)lane * L + g * RUN;
             uint32_t S = Sc;
             u16x2 Tv = Tc;
-            bool dirty = false;
             uint32_t xs[RUN];
 #pragma unroll
             for (int gg = 0; gg < NG; ++gg) {
@@ -980,29 +962,32 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 }
                 const uint32_t a = as_u32(acc);
                 const bool z = (a & 0xffffu) == 0u || (a >> 16) == 0u;
-                dirty = dirty || z;
                 const uint64_t bz = __ballot(z);
                 if (__builtin_expect(bz != 0ull, 0)) {
-                    const uint32_t have = __builtin_amdgcn_readfirstlane(
-                        __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)dcount, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WAVEFRONT));
-                    if (have + (uint32_t)__builtin_popcountll(bz) > (uint32_t)ST_DIRTYCAP) {
-                        if (lane == 0) *dcount = have | 0x10000u;          // overflow: dense (below)
-                    } else if (z) {
-                        const uint32_t idx = atomicAdd(dcount, 1u);
-                        DirtySlotST &ds = dslots[idx];
+                    const uint32_t nz = (uint32_t)__builtin_popcountll(bz);
+                    if (have + nz > (uint32_t)ST_DIRTYCAP) {
+                        // no room for this group's dirty streams: their tiles go to the dense
+                        // pass (lane l's streams l and l + 64 lie in tiles l / 16 and 4 + l / 16;
+                        // the marks are applied when the ST is published)
+                        dmark |= ((a & 0xffffu) == 0u ? 1u << (lane >> 4) : 0u) |
+                                 ((a >> 16) == 0u ? 16u << (lane >> 4) : 0u);
+                    } else {
+                        if (z) {                                           // slot: have + rank among z lanes
+                            const uint32_t idx = have + __builtin_amdgcn_mbcnt_hi(
+                                (uint32_t)(bz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bz, 0u));
+                            DirtySlotST &ds = dslots[idx];
 #pragma unroll
-                        for (int jj = 0; jj < 16; ++jj) {
-                            const int j = gg * 16 + jj;
-                            ds.dp[jj] = j < 64 ? Pd[j < 64 ? j : 0] : xs[j >= 64 ? j - 64 : 0];
-                            ds.xp[jj] = xs[j];
+                            for (int jj = 0; jj < 16; ++jj) {
+                                const int j = gg * 16 + jj;
+                                ds.dp[jj] = j < 64 ? Pd[j < 64 ? j : 0] : xs[j >= 64 ? j - 64 : 0];
+                                ds.xp[jj] = xs[j];
+                            }
+                            ds.S0 = S0;
+                            ds.T0 = as_u32(T0);
+                            ds.relA = relA0 + 16u * (uint32_t)gg;
                         }
-                        ds.S0 = S0;
-                        ds.T0 = as_u32(T0);
-                        ds.relA = relA0 + 16u * (uint32_t)gg;
+                        have += nz;
                     }
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
                 }
             }
             // carry the window: the pairs of positions RUN-64 .. RUN-1 are the next segment's dropped bytes
@@ -1010,24 +995,11 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             for (int j = 0; j < 64; ++j) Pd[j] = xs[RUN - 64 + j];
             Sc = S;
             Tc = Tv;
-            // ---- exact re-walk of the captured groups; an overflow marks the dirty streams' tiles dense
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            const uint32_t dc = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)dcount, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WAVEFRONT));
-            if (__builtin_expect(dc != 0u, 0)) {
-                if (dc & 0x10000u) {
-                    // more dirty groups than slots: every tile holding a dirty stream goes to the
-                    // dense pass (lane l's streams l and l + 64 lie in tiles l / 16 and 4 + l / 16)
-                    const uint64_t bal = __ballot(dirty);
-                    uint32_t m = 0;
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        if ((bal >> (16 * t)) & 0xffffull) m |= (1u << t) | (1u << (t + 4));
-                    if (lane < ST_TILES && ((m >> lane) & 1u)) tcnt[lane] |= 0x80000000u;   // dense mark
-                }
-                const uint32_t nd = dc & 0xffffu;
+            // ---- exact re-walk of the captured groups
+            if (__builtin_expect(have != 0u, 0)) {
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");     // the slots' LDS writes
+                const uint32_t nd = have;
                 if ((uint32_t)lane < nd) {
                     const DirtySlotST &ds = dslots[lane];
                     const u16x2 kk = as_u16x2(P.kk), km = as_u16x2(P.kmv);
@@ -1055,6 +1027,14 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 }
             }
             if (g + 1 == (uint32_t)ST_SEGS) {                        // the ST's tiles are complete: publish
+                if (__builtin_expect(__ballot(dmark != 0u) != 0ull, 0)) {   // tiles with unrecorded dirty groups
+                    uint32_t m = 0;
+#pragma unroll
+                    for (int t = 0; t < ST_TILES; ++t)
+                        if (__ballot((dmark >> t) & 1u)) m |= 1u << t;
+                    if (lane < ST_TILES && ((m >> lane) & 1u)) atomicOr(&tcnt[lane], 0x80000000u);
+                    dmark = 0u;
+                }
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll 1
@@ -1069,7 +1049,10 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 }
                 __builtin_amdgcn_wave_barrier();
             }
-            if (!more) return;
+            if (!more) {
+                dense_pend_flush(T, dslots_alloc, lane);
+                return;
+            }
         }
         st = nextst;
     }
@@ -3612,7 +3595,9 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
     else if (p.ablate == 7u)                                         // A/B: product + 3 waves per SIMD hint
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, d, p,
                            t);
-    else if (p.nt && scan_dynamic(t.ntiles, grid))                   // product: nt loads + dynamic groups + ROLL2
+    else if (p.nt && scan_dynamic(t.ntiles, grid) && RUN == DEFAULT_RUN)   // product, large batch: stream tiles
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
+    else if (p.nt && scan_dynamic(t.ntiles, grid))                   // other geometries: nt + dynamic groups + ROLL2
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.nt)                                                   // product, small batch: CU schedule
         launch_scan_cu<RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);
@@ -3702,9 +3687,8 @@ hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParam
     if (!t.ntiles) return hipSuccess;
     if (!scan_supported(g)) return hipErrorInvalidValue;
     grid = grid < t.ntiles ? grid : t.ntiles;
-    if (scan_dynamic(t.ntiles, grid))
-        hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
-                           lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
+    if (scan_dynamic(t.ntiles, grid))             // large batch: stream tiles (carried windows, §4.6)
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else                                          // small batch: the CU schedule (per-wave static shares end
         launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);   // with the slow waves alone)
     return hipGetLastError();

@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--idle", type=float, default=0.5)
-    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "shard8"])
+    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "shard8", "dense", "periodic"])
     args = ap.parse_args()
     sizes = WL.zipf_sizes()
     if args.workload == "uniform1k":
@@ -47,6 +47,15 @@ def main():
     base = syncr_amd.Chunker()
     buf = syncr_amd.DeviceBuffer(base, span)
     buf.gen_corpus(offs, lens, indices=idx)
+    if args.workload == "dense":                   # the adversarial table (benchlib.legs.fill_dense)
+        from benchlib import legs as LG
+        LG.fill_dense(buf, offs, lens, idx)
+    elif args.workload == "periodic":              # the zipf10k table, every byte of the 64-byte period
+        pat = WL.periodic_pattern()
+        chunk = 256 << 20
+        for o in range(0, span, chunk):
+            n = min(chunk, span - o)
+            buf.upload(np.resize(np.roll(pat, -(o % pat.size)), n), offset=o)
     handles = []
     for v in args.variants:
         saved = dict(os.environ)
