@@ -701,3 +701,49 @@ def test_small_batches_back_to_back_stable():
             b.free()
         for ch in hs:
             ch.close()
+
+
+@pytest.mark.parametrize("bits,cap", [(12, 64 << 10), (20, 2 << 20)])
+def test_large_batch_stream_tiles_vs_oracle(bits, cap):
+    """A batch big enough for the stream-tile scan (>= 96 tiles per scan wave:
+    the product's large-batch path) with random, periodic-64 and constant
+    files of ragged sizes, at a small mask (dirty groups in most segments: slot
+    overflow and dense marks) and at the production mask: every file's cuts vs
+    the oracle."""
+    from benchlib.workloads import periodic_pattern
+    rng = np.random.default_rng(bits * 7919 + cap)
+    ch = syncr_amd.Chunker(chunk_bits=bits, max_chunk=16 << 20, read_cap=cap)
+    try:
+        info = ch.info()
+        need = info["scan_grid"] * syncr_amd.SCAN_DYN_MIN_TILES_PER_WAVE * info["tile_bytes"] + (1 << 20)
+        lens = []
+        while sum(lens) < need:
+            lens.append(int(rng.integers(1, 96 << 20)))
+        lens = np.array(lens, np.uint64)
+        offs = np.zeros_like(lens)
+        offs[1:] = np.cumsum(lens)[:-1]
+        span = int(lens.sum())
+        assert ch.scan_kernel_for(span) == "cdc_scan_st_kernel"
+        buf = syncr_amd.DeviceBuffer(ch, span)
+        try:
+            buf.gen_corpus(offs, lens, indices=np.arange(lens.size, dtype=np.uint64) + 100003)
+            pat = periodic_pattern()
+            for i in range(lens.size):
+                if i % 8 == 3:                     # periodic-64 file
+                    buf.upload(np.resize(pat, int(lens[i])), offset=int(offs[i]))
+                elif i % 8 == 6:                   # one constant byte
+                    buf.upload(np.full(int(lens[i]), 0x5A, np.uint8), offset=int(offs[i]))
+            ch.plan(offs, lens, span)
+            ch.launch(buf.ptr)
+            res = ch.fetch()
+            host = buf.download(span)
+            print(f"stream-tile batch: {lens.size} files, {span / 2**30:.2f} GiB chunked; oracle next", flush=True)
+        finally:
+            buf.free()
+        # the windowed restatement of the production loop: the literal loop memmoves its
+        # 16 MiB buffer after every 64-byte chunk of a periodic file (quadratic)
+        ref = O.chunk_batch(host, offs, lens, bits=bits, read_cap=cap, mode=O.MODE_PRODUCTION_WINDOW)
+        bad = [i for i in range(lens.size) if ends_of(res[i]) != ref[i].tolist()]
+        assert not bad, bad[:10]
+    finally:
+        ch.close()
