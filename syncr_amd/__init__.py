@@ -220,9 +220,9 @@ def _u8(data) -> np.ndarray:
     return np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
 
 
-# cdc_kernels.hip SCAN_DYN_MIN_TILES_PER_WAVE: batches of at least this many tiles per scan wave
+# cdc_kernels.hip SCAN_ST_MIN_TILES_PER_WAVE: batches of at least this many tiles per scan wave
 # run the stream-tile scan, smaller ones the CU schedule
-SCAN_DYN_MIN_TILES_PER_WAVE = 96
+SCAN_ST_MIN_TILES_PER_WAVE = 32
 
 
 class Chunker:
@@ -379,13 +379,13 @@ class Chunker:
 
     def scan_kernel_for(self, span: int) -> str:
         """The scan kernel a launch over `span` bytes runs (cdc_kernels.hip
-        launch_scan): stream tiles from 96 tiles per wave, the CU schedule below."""
+        launch_scan): stream tiles from 32 tiles per wave, the CU schedule below."""
         d = self.info()
         if d["run_bytes"] >= 1000:
             return d["scan_kernel"]
         ntiles = -(-int(span) // d["tile_bytes"]) if span else 0
         grid = min(d["scan_grid"], ntiles) if ntiles else 0
-        if grid and ntiles >= grid * SCAN_DYN_MIN_TILES_PER_WAVE:
+        if grid and ntiles >= grid * SCAN_ST_MIN_TILES_PER_WAVE:
             return "cdc_scan_st_kernel"
         return "cdc_scan_kernel"
 

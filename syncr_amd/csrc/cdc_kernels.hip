@@ -484,6 +484,15 @@ constexpr uint32_t SCAN_DYN_MIN_TILES_PER_WAVE = 96;
 __host__ __device__ constexpr bool scan_dynamic(uint32_t ntiles, uint32_t grid) {
     return (uint64_t)ntiles >= (uint64_t)grid * SCAN_DYN_MIN_TILES_PER_WAVE;
 }
+// The product's choice (round 4): stream tiles (cdc_scan_st_kernel) from 32 tiles
+// (4 stream tiles) per wave, the CU schedule below.  Same-process A/B against the
+// CU schedule (profiles/r04_stream_tile_shards_ab.jsonl): config 4's shards at
+// N = 8 / 4 / 2 (35 / 69 / 138 tiles per wave) 0.259 vs 0.264, 0.486 vs 0.505,
+// 0.881 vs 0.913 ms; uniform1k (28 per wave) 0.224 vs 0.217 (stream tiles lose).
+constexpr uint32_t SCAN_ST_MIN_TILES_PER_WAVE = 32;
+__host__ __device__ constexpr bool scan_stream_tiles(uint32_t ntiles, uint32_t grid) {
+    return (uint64_t)ntiles >= (uint64_t)grid * SCAN_ST_MIN_TILES_PER_WAVE;
+}
 
 // MODE bit 5: ask for 3 waves per SIMD (VGPRs <= 168; development A/B only).
 // MODE bit 6: the round-2 roll with a branch per group (development A/B only)
@@ -3595,7 +3604,7 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
     else if (p.ablate == 7u)                                         // A/B: product + 3 waves per SIMD hint
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, d, p,
                            t);
-    else if (p.nt && scan_dynamic(t.ntiles, grid) && RUN == DEFAULT_RUN)   // product, large batch: stream tiles
+    else if (p.nt && scan_stream_tiles(t.ntiles, grid) && RUN == DEFAULT_RUN)   // product: stream tiles
         hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else if (p.nt && scan_dynamic(t.ntiles, grid))                   // other geometries: nt + dynamic groups + ROLL2
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
@@ -3687,7 +3696,7 @@ hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParam
     if (!t.ntiles) return hipSuccess;
     if (!scan_supported(g)) return hipErrorInvalidValue;
     grid = grid < t.ntiles ? grid : t.ntiles;
-    if (scan_dynamic(t.ntiles, grid))             // large batch: stream tiles (carried windows, §4.6)
+    if (scan_stream_tiles(t.ntiles, grid))        // >= 4 stream tiles per wave: carried windows (§4.6)
         hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else                                          // small batch: the CU schedule (per-wave static shares end
         launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);   // with the slow waves alone)

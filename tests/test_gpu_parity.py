@@ -715,7 +715,7 @@ def test_large_batch_stream_tiles_vs_oracle(bits, cap):
     ch = syncr_amd.Chunker(chunk_bits=bits, max_chunk=16 << 20, read_cap=cap)
     try:
         info = ch.info()
-        need = info["scan_grid"] * syncr_amd.SCAN_DYN_MIN_TILES_PER_WAVE * info["tile_bytes"] + (1 << 20)
+        need = info["scan_grid"] * 96 * info["tile_bytes"] + (1 << 20)      # well inside the stream-tile range
         lens = []
         while sum(lens) < need:
             lens.append(int(rng.integers(1, 96 << 20)))

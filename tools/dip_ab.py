@@ -32,13 +32,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--idle", type=float, default=0.5)
-    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "shard8", "dense", "periodic"])
+    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "shard8", "shard4", "shard2", "dense", "periodic"])
     args = ap.parse_args()
     sizes = WL.zipf_sizes()
     if args.workload == "uniform1k":
         lens, idx = np.full(1024, 1 << 20, np.uint64), np.arange(1024, dtype=np.uint64)
-    elif args.workload == "shard8":
-        sh = WL.lpt_shard(sizes, 8)[0]
+    elif args.workload in ("shard8", "shard4", "shard2"):
+        sh = WL.lpt_shard(sizes, int(args.workload[5:]))[0]
         lens, idx = sizes[sh], sh.astype(np.uint64)
     else:
         lens, idx = sizes, np.arange(sizes.size, dtype=np.uint64)
