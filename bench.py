@@ -560,7 +560,7 @@ def main(argv=None):
 
     scan_ms = kms[0] / max(nl, 1)
     achieved = span / (scan_ms / 1e3) / 1e9 if scan_ms > 0 else 0.0
-    scan_kernel = ch.scan_kernel_for(span)
+    scan_kernel = ch.scan_kernel_for(span, dense_tiles=int(stats.get("dense_tiles", 0) or 0))
     tr = load_traffic(args.workload, span, engine_info["run_bytes"], kernel="cdc::" + scan_kernel)
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

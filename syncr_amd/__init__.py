@@ -377,14 +377,18 @@ class Chunker:
             d["mfma_blocks"] = d["run_bytes"] - 1000
         return d
 
-    def scan_kernel_for(self, span: int) -> str:
+    def scan_kernel_for(self, span: int, dense_tiles: int = 0) -> str:
         """The scan kernel a launch over `span` bytes runs (cdc_kernels.hip
-        launch_scan): stream tiles from 32 tiles per wave, the CU schedule below."""
+        launch_scan): stream tiles from 32 tiles per wave, the CU schedule below;
+        after a fetched launch with >= 1 % dense tiles (`dense_tiles` of that
+        launch), tiles with dynamic groups from 96 tiles per wave."""
         d = self.info()
         if d["run_bytes"] >= 1000:
             return d["scan_kernel"]
         ntiles = -(-int(span) // d["tile_bytes"]) if span else 0
         grid = min(d["scan_grid"], ntiles) if ntiles else 0
+        if dense_tiles * 100 >= max(ntiles, 1):
+            return "cdc_scan_kernel"
         if grid and ntiles >= grid * SCAN_ST_MIN_TILES_PER_WAVE:
             return "cdc_scan_st_kernel"
         return "cdc_scan_kernel"

@@ -109,6 +109,8 @@ struct KParams {
                                //   SYNCR_CDC_FLAG_SPLIT_NOWAIT)
     uint32_t split_first;      // 1: split workers take the resolve grid's first blocks (dev A/B: SYNCR_CDC_SPLIT_FIRST)
     uint32_t no_skip;          // 1: no run skips in the resolve walk (dev A/B: SYNCR_CDC_NOSKIP)
+    uint32_t scan_tiles;       // 1: the last fetched launch of the handle was dense-heavy: scan by tiles
+                               //   (dynamic groups) instead of stream tiles (cdc_kernels.hip launch_scan)
     uint32_t dense_fuse;       // 1: the dense pass computes its candidates' head fix-ups (product; dev A/B:
                                //   SYNCR_CDC_DENSE_FUSE=0)
     uint32_t resolve_pf;       // development library only (SYNCR_CDC_RESOLVE_PF): candidate windows

@@ -3604,7 +3604,9 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
     else if (p.ablate == 7u)                                         // A/B: product + 3 waves per SIMD hint
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, d, p,
                            t);
-    else if (p.nt && scan_stream_tiles(t.ntiles, grid) && RUN == DEFAULT_RUN)   // product: stream tiles
+    else if (p.nt && p.scan_tiles && scan_dynamic(t.ntiles, grid))   // product, dense-heavy data: tiles
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
+    else if (p.nt && !p.scan_tiles && scan_stream_tiles(t.ntiles, grid) && RUN == DEFAULT_RUN)   // product: stream tiles
         hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else if (p.nt && scan_dynamic(t.ntiles, grid))                   // other geometries: nt + dynamic groups + ROLL2
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
@@ -3696,7 +3698,10 @@ hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParam
     if (!t.ntiles) return hipSuccess;
     if (!scan_supported(g)) return hipErrorInvalidValue;
     grid = grid < t.ntiles ? grid : t.ntiles;
-    if (scan_stream_tiles(t.ntiles, grid))        // >= 4 stream tiles per wave: carried windows (§4.6)
+    if (p.scan_tiles && scan_dynamic(t.ntiles, grid))   // the handle's last batch was dense-heavy:
+        hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),   // tiles
+                           lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
+    else if (!p.scan_tiles && scan_stream_tiles(t.ntiles, grid))   // >= 4 stream tiles per wave (§4.6)
         hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else                                          // small batch: the CU schedule (per-wave static shares end
         launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);   // with the slow waves alone)
