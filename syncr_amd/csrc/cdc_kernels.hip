@@ -661,7 +661,6 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             } else {
                 if (gj == 0) {                                       // group ends at its first tile (last round)
                     if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
-                    grabbed = true;
                 }
                 wait_vmcnt<0>();                                     // the grab
                 next = gbase(stride + (uint32_t)__builtin_amdgcn_readfirstlane(pend));
@@ -892,9 +891,15 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     };
     uint32_t st = blockIdx.x;
     if (st >= nst) return;
+    const bool stamp = blockIdx.x < (uint32_t)DBG_SCAN_N;              // timeline slot (dev)
+    if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x, wall_clock64());
+#ifdef SYNCR_CDC_DEV
+    uint32_t nst_done = 0;
+#endif
     issue_seg(st, 0);
     load_halo(st);
     uint32_t pend = 0, nextst = 0;
+    uint32_t nth = 0;                              // this wave's STs so far (wave-uniform)
     DensePend dslots_alloc;
     // (a ping-pong of two carried arrays, segments unrolled in pairs to drop the 64 moves
     // below, measured slower: 3 copies of the roll overflow the instruction cache)
@@ -906,12 +911,12 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 #pragma unroll 1
         for (uint32_t g = 0; g < (uint32_t)ST_SEGS; ++g) {
             const bool first = g == 0u;
-            if (first) {
-                if (lane < ST_TILES) tcnt[lane] = 0u;
-                if (lane == 0 && nst > gridDim.x) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);   // the next ST
-            }
+            if (first && lane < ST_TILES) tcnt[lane] = 0u;
             uint32_t have = 0;                                       // dirty slots taken (wave-uniform)
             wait_vmcnt<0>();                                         // segment g landed (and, at 0, the halo)
+#ifdef SYNCR_CDC_DEV
+            if (stamp && first && nst_done == 0) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 1, wall_clock64());
+#endif
             if (first) {                                             // warm-up from the halo (closed form)
                 uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
 #pragma unroll
@@ -940,6 +945,16 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             bool more = true;
             if (g + 1 < (uint32_t)ST_SEGS) {
                 issue_seg(st, g + 1);
+                // the next ST comes from a counter, grabbed behind the next segment's DMAs:
+                // in a wave's first ST at segment blockIdx.x % 8 (grabbing at segment 0 before
+                // its landing wait put every wave of the grid on one address at launch: the
+                // first segment landed 18.7 us after entry, median, tools/scan_timeline.py),
+                // later at segment 0
+                if (g == (nth == 0u ? (blockIdx.x & 7u) : 0u) && nst > gridDim.x) {
+                    // (the compiler waits for the result at once -- its copy into the
+                    // loop-carried register -- but segment 1's DMAs are in flight by then)
+                    if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
+                }
             } else {
                 nextst = nst > gridDim.x ? gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nst;
                 more = nextst < nst;
@@ -1060,10 +1075,24 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             }
             if (!more) {
                 dense_pend_flush(T, dslots_alloc, lane);
+#ifdef SYNCR_CDC_DEV
+                if (stamp) {
+                    uint32_t hwid, xcc;
+                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
+                                 : "=s"(hwid), "=s"(xcc));
+                    SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 2, wall_clock64());
+                    SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 3,
+                               (uint64_t)(8u * (nst_done + 1u)) | ((uint64_t)hwid << 32) | ((uint64_t)(xcc & 0xf) << 28));
+                }
+#endif
                 return;
             }
         }
         st = nextst;
+        ++nth;
+#ifdef SYNCR_CDC_DEV
+        ++nst_done;
+#endif
     }
 }
 
@@ -1214,7 +1243,6 @@ void cdc_scan3_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             } else {
                 if (gj == 0) {
                     if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
-                    grabbed = true;
                 }
                 wait_vmcnt<0>();                                     // the grab
                 next = gbase(stride + (uint32_t)__builtin_amdgcn_readfirstlane(pend));
