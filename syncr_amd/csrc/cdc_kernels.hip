@@ -945,12 +945,13 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             bool more = true;
             if (g + 1 < (uint32_t)ST_SEGS) {
                 issue_seg(st, g + 1);
-                // the next ST comes from a counter, grabbed behind the next segment's DMAs:
-                // in a wave's first ST at segment blockIdx.x % 8 (grabbing at segment 0 before
-                // its landing wait put every wave of the grid on one address at launch: the
-                // first segment landed 18.7 us after entry, median, tools/scan_timeline.py),
-                // later at segment 0
-                if (g == (nth == 0u ? (blockIdx.x & 7u) : 0u) && nst > gridDim.x) {
+                // the next ST comes from a counter, grabbed behind the next segment's DMAs and
+                // late in the ST (a wave that binds its next ST early can be a slow one holding
+                // the batch's last ST): at segment 7, in a wave's first ST at 4 + blockIdx.x % 4
+                // (grabbing at segment 0 before its landing wait put every wave of the grid on
+                // one address at launch: the first segment landed 18.7 us after entry, median,
+                // tools/scan_timeline.py)
+                if (g == (nth == 0u ? 4u + (blockIdx.x & 3u) : (uint32_t)ST_SEGS - 2u) && nst > gridDim.x) {
                     // (the compiler waits for the result at once -- its copy into the
                     // loop-carried register -- but segment 1's DMAs are in flight by then)
                     if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
