@@ -222,7 +222,7 @@ def _u8(data) -> np.ndarray:
 
 # cdc_kernels.hip SCAN_ST_MIN_TILES_PER_WAVE: batches of at least this many tiles per scan wave
 # run the stream-tile scan, smaller ones the CU schedule
-SCAN_ST_MIN_TILES_PER_WAVE = 32
+SCAN_ST_MIN_TILES_PER_WAVE = 24
 
 
 class Chunker:
@@ -379,7 +379,7 @@ class Chunker:
 
     def scan_kernel_for(self, span: int, dense_tiles: int = 0) -> str:
         """The scan kernel a launch over `span` bytes runs (cdc_kernels.hip
-        launch_scan): stream tiles from 32 tiles per wave, the CU schedule below;
+        launch_scan): stream tiles from 24 tiles per wave, the CU schedule below;
         after a fetched launch with >= 1 % dense tiles (`dense_tiles` of that
         launch), tiles with dynamic groups from 96 tiles per wave."""
         d = self.info()

@@ -484,12 +484,14 @@ constexpr uint32_t SCAN_DYN_MIN_TILES_PER_WAVE = 96;
 __host__ __device__ constexpr bool scan_dynamic(uint32_t ntiles, uint32_t grid) {
     return (uint64_t)ntiles >= (uint64_t)grid * SCAN_DYN_MIN_TILES_PER_WAVE;
 }
-// The product's choice (round 4): stream tiles (cdc_scan_st_kernel) from 32 tiles
-// (4 stream tiles) per wave, the CU schedule below.  Same-process A/B against the
+// The product's choice (round 4): stream tiles (cdc_scan_st_kernel) from 24 tiles
+// (3 stream tiles) per wave, the CU schedule below.  Same-process A/B against the
 // CU schedule (profiles/r04_stream_tile_shards_ab.jsonl): config 4's shards at
 // N = 8 / 4 / 2 (35 / 69 / 138 tiles per wave) 0.259 vs 0.264, 0.486 vs 0.505,
-// 0.881 vs 0.913 ms; uniform1k (28 per wave) 0.224 vs 0.217 (stream tiles lose).
-constexpr uint32_t SCAN_ST_MIN_TILES_PER_WAVE = 32;
+// 0.881 vs 0.913 ms; uniform1k (28 per wave) 0.207 vs 0.211 once the next-ST
+// grab moved off the launch contention (profiles/r04_stream_tile_uniform1k_ab.jsonl;
+// 0.224 vs 0.217 before it).
+constexpr uint32_t SCAN_ST_MIN_TILES_PER_WAVE = 24;
 __host__ __device__ constexpr bool scan_stream_tiles(uint32_t ntiles, uint32_t grid) {
     return (uint64_t)ntiles >= (uint64_t)grid * SCAN_ST_MIN_TILES_PER_WAVE;
 }
