@@ -697,8 +697,8 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         h->zpar = h->zlast = 0;
         CHECK_HIP(h->super_off.ensure(((size_t)h->nwords + 1) * 8));
         // dense tiles are rare (adversarial data); grow on demand in fetch()
-        // (scan waves take dense-list slots 8 at a time, so a list may hold up to
-        // ntiles + 8 x scan_grid slots, unused ones included: no clamp to ntiles)
+        // (scan waves take their dense-list slots in batches of up to 64 pending
+        // tiles, DensePend: the list has no holes, so ntiles slots always suffice)
         uint32_t dcap = std::max<uint32_t>(64u, h->ntiles / 256u);
         int32_t rc = ensure_dense(h, dcap);
         if (rc) return rc;
@@ -817,7 +817,7 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
                 rerun = true;
             }
             if (ctr[CTR_FLAGS] & FLAG_DENSE_OVERFLOW) {
-                // the counter includes the slots of every wave's last chunk: enough
+                // the counter holds every dense tile of the launch: enough
                 const uint64_t need = (uint64_t)ctr[CTR_DENSE] + ctr[CTR_DENSE] / 4 + 16;
                 const uint64_t lim = (uint64_t)h->ntiles + 8ull * h->scan_grid + 64;
                 const uint32_t want = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(need, 2ull * h->dense_cap), lim);

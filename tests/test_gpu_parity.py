@@ -703,10 +703,62 @@ def test_small_batches_back_to_back_stable():
             ch.close()
 
 
+@pytest.mark.parametrize("below", [False, True])
+def test_stream_tile_threshold_edge_vs_oracle(below):
+    """The two scans either side of SCAN_ST_MIN_TILES_PER_WAVE (cdc_kernels.hip
+    launch_scan): a batch of exactly grid x 24 tiles whose last tile holds one
+    byte (stream tiles; the batch's last stream tile is mostly past the span:
+    the clamped DMA path) and one tile less (the CU schedule), random files with
+    periodic-64 and constant ones at chunk_bits 13: every file's cuts vs the
+    oracle."""
+    from benchlib.workloads import periodic_pattern
+    bits, cap = 13, 256 << 10
+    rng = np.random.default_rng(24 + below)
+    ch = syncr_amd.Chunker(chunk_bits=bits, max_chunk=16 << 20, read_cap=cap)
+    try:
+        info = ch.info()
+        tb = info["tile_bytes"]
+        ntiles = info["scan_grid"] * syncr_amd.SCAN_ST_MIN_TILES_PER_WAVE
+        span = (ntiles - 1) * tb + (0 if below else 1)
+        lens = []
+        while sum(lens) < span:
+            lens.append(int(rng.integers(1, 24 << 20)))
+        lens[-1] -= sum(lens) - span
+        if lens[-1] == 0:
+            lens.pop()
+        lens = np.array(lens, np.uint64)
+        offs = np.zeros_like(lens)
+        offs[1:] = np.cumsum(lens)[:-1]
+        assert int(lens.sum()) == span
+        want = "cdc_scan_kernel" if below else "cdc_scan_st_kernel"
+        assert ch.scan_kernel_for(span) == want
+        buf = syncr_amd.DeviceBuffer(ch, span)
+        try:
+            buf.gen_corpus(offs, lens, indices=np.arange(lens.size, dtype=np.uint64) + 7001)
+            pat = periodic_pattern()
+            for i in range(lens.size):
+                if i % 5 == 2:
+                    buf.upload(np.resize(pat, int(lens[i])), offset=int(offs[i]))
+                elif i % 5 == 4:
+                    buf.upload(np.full(int(lens[i]), 0xA5, np.uint8), offset=int(offs[i]))
+            ch.plan(offs, lens, span)
+            ch.launch(buf.ptr)
+            res = ch.fetch()
+            host = buf.download(span)
+            print(f"{want} edge batch: {lens.size} files, {span} bytes; oracle next", flush=True)
+        finally:
+            buf.free()
+        ref = O.chunk_batch(host, offs, lens, bits=bits, read_cap=cap, mode=O.MODE_PRODUCTION_WINDOW)
+        bad = [i for i in range(lens.size) if ends_of(res[i]) != ref[i].tolist()]
+        assert not bad, bad[:10]
+    finally:
+        ch.close()
+
+
 @pytest.mark.parametrize("bits,cap", [(12, 64 << 10), (20, 2 << 20)])
 def test_large_batch_stream_tiles_vs_oracle(bits, cap):
-    """A batch big enough for the stream-tile scan (>= 96 tiles per scan wave:
-    the product's large-batch path) with random, periodic-64 and constant
+    """A batch well inside the stream-tile scan's range (96 tiles per scan wave;
+    the product's scan from 24) with random, periodic-64 and constant
     files of ragged sizes, at a small mask (dirty groups in most segments: slot
     overflow and dense marks) and at the production mask: every file's cuts vs
     the oracle."""
