@@ -3305,7 +3305,10 @@ __device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P,
 }
 
 // After the resolve launch (so after every walker): copy the cuts of every
-// segment walk a file walker adopted into that file's output.
+// segment walk a file walker adopted into that file's output.  PARTS waves per
+// record / run, U 16-byte loads in flight per lane (dev A/B: SYNCR_CDC_ABLATE=18
+// runs <16, 16>).
+template <uint32_t COPY_PARTS, int U1>
 __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
     const int lane = threadIdx.x & 63;
     const uint32_t wid = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
@@ -3314,10 +3317,8 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
     if (nsplit == 0u && nruns == 0u) return;                  // nothing split or deferred
     if (blockIdx.x == 0 && threadIdx.x < 64) DBG_STAMP(T, DBG_COPY_START);
     const uint32_t nrec = nsplit ? min(T.split[SPL_RESERVED], T.seg_cap) : 0u;
-    // COPY_PARTS waves per record / run (up to 3 x 4096 cuts: one wave each left
-    // most of the grid idle and each wave latency-bound), four 16-byte loads in
-    // flight per lane
-    constexpr uint32_t COPY_PARTS = 8;
+    // several waves per record / run (up to 3 x 4096 cuts: one wave each left
+    // most of the grid idle and each wave latency-bound)
     // 1. scratch cuts of every adopted segment walk (its deferred run, if any,
     //    leaves a gap of run_len slots after its first run_pre cuts)
     for (uint32_t w = wid; w < nrec * COPY_PARTS; w += nw) {
@@ -3331,13 +3332,13 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
         const uint64_t a = (uint64_t)part * per, e = min(n, a + per);
         const DevCut *src = T.seg_cuts + (uint64_t)q * T.seg_scap;
         DevCut *dst = T.cuts + T.cut_base[i];
-        for (uint64_t t = a + (uint64_t)lane; t < e; t += 256) {
-            DevCut v[4];
+        for (uint64_t t = a + (uint64_t)lane; t < e; t += 64u * U1) {
+            DevCut v[U1];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < U1; ++u)
                 if (t + 64u * u < e) v[u] = src[t + 64u * u];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U1; ++u) {
                 const uint64_t tt = t + 64u * u, d = o + tt + (tt < rp ? 0u : rl);
                 if (tt < e && d < cap) dst[d] = v[u];
             }
@@ -3805,7 +3806,10 @@ hipError_t launch_resolve(const uint8_t *d, const KParams &p, const Tables &t, h
             hipLaunchKernelGGL((cdc_resolve_wave_kernel<RESOLVE_PF, true>), grid, dim3(256), 0, s, d, p, t);
         else
             hipLaunchKernelGGL((cdc_resolve_wave_kernel<RESOLVE_PF, false>), grid, dim3(256), 0, s, d, p, t);
-        if (split) hipLaunchKernelGGL(cdc_split_copy_kernel, dim3(1024), dim3(256), 0, s, t);
+        if (split && p.ablate == 18u)
+            hipLaunchKernelGGL((cdc_split_copy_kernel<16, 16>), dim3(1024), dim3(256), 0, s, t);
+        else if (split)
+            hipLaunchKernelGGL((cdc_split_copy_kernel<8, 4>), dim3(1024), dim3(256), 0, s, t);
     }
     return hipGetLastError();
 }

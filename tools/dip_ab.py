@@ -32,11 +32,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--idle", type=float, default=0.5)
-    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "shard8", "shard4", "shard2", "dense", "periodic"])
+    ap.add_argument("--workload", default="zipf10k", choices=["zipf10k", "uniform1k", "shard8", "shard4", "shard2", "dense", "periodic", "dense1"])
     args = ap.parse_args()
     sizes = WL.zipf_sizes()
     if args.workload == "uniform1k":
         lens, idx = np.full(1024, 1 << 20, np.uint64), np.arange(1024, dtype=np.uint64)
+    elif args.workload == "dense1":                # one 128 MiB periodic-64 file
+        lens, idx = np.full(1, 128 << 20, np.uint64), np.arange(1, dtype=np.uint64)
     elif args.workload in ("shard8", "shard4", "shard2"):
         sh = WL.lpt_shard(sizes, int(args.workload[5:]))[0]
         lens, idx = sizes[sh], sh.astype(np.uint64)
@@ -50,7 +52,7 @@ def main():
     if args.workload == "dense":                   # the adversarial table (benchlib.legs.fill_dense)
         from benchlib import legs as LG
         LG.fill_dense(buf, offs, lens, idx)
-    elif args.workload == "periodic":              # the zipf10k table, every byte of the 64-byte period
+    elif args.workload in ("periodic", "dense1"):              # the zipf10k table, every byte of the 64-byte period
         pat = WL.periodic_pattern()
         chunk = 256 << 20
         for o in range(0, span, chunk):
