@@ -475,7 +475,7 @@ def main(argv=None):
         d.barrier()
         kms, nl = ch.kernel_times()
         ch.set_timing(False)
-        return dt, kms, nl
+        return dt, kms, nl, ch.last_scan()      # the library's own report of the scan it ran
 
     # The host-side fetch (D2H + list building) is a gap of the device's load,
     # and on MI355X the shader clock dips whenever the scan load resumes after a
@@ -485,13 +485,13 @@ def main(argv=None):
     # with grown capacities, the timed launches ran with the smaller ones, so the
     # region is timed again (now with settled capacities, fetch after step 1).
     fetch_mode = args.fetch_at
-    dt, kms, nl = warm_and_time(fetch_mode)
+    dt, kms, nl, scan_info = warm_and_time(fetch_mode)
     retimed = False
     if fetch_mode == "after":
         ch.fetch(hashed=head_hashed)
         if d.reduce(float(ch.fetch_reruns()), "max") > 0:
             fetch_mode, retimed = "first", True
-            dt, kms, nl = warm_and_time(fetch_mode)
+            dt, kms, nl, scan_info = warm_and_time(fetch_mode)
     # diagnostics outside the timed region: every phase bracketed by events
     ch.set_timing(True)
     run_steps(1, min(args.steps, 5))
@@ -560,13 +560,13 @@ def main(argv=None):
 
     scan_ms = kms[0] / max(nl, 1)
     achieved = span / (scan_ms / 1e3) / 1e9 if scan_ms > 0 else 0.0
-    scan_kernel = ch.scan_kernel_for(span, dense_tiles=int(stats.get("dense_tiles", 0) or 0))
+    scan_kernel = scan_info["kernel"]           # syncr_cdc_last_scan of the last timed launch
     tr = load_traffic(args.workload, span, engine_info["run_bytes"], kernel="cdc::" + scan_kernel)
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": (int(tr["hbm_bytes_per_launch"]) if tr else None),
-        "kernel": scan_kernel, "kernel_ms": round(scan_ms, 4),
+        "kernel": scan_kernel, "kernel_ms": round(scan_ms, 4), "scan_schedule": scan_info,
         "algorithmic_bytes_per_launch": span,
         "dense_ms": round(pms[1] / max(pn, 1), 4), "resolve_ms": round(pms[2] / max(pn, 1), 4),
         "hash_ms": round(pms[3] / max(pn, 1), 4) if head_hashed else None,

@@ -44,6 +44,7 @@ def time_steps(ch, ptr: int, span: int, steps: int, warmup: int, hashed: bool = 
     dt = (time.perf_counter() - t0) / max(steps, 1)
     kms, nl = ch.kernel_times()
     ch.set_timing(False)
+    scan = ch.last_scan()                     # the library's report of the scan the timed steps ran
     ch.set_timing(True)
     for _ in range(min(steps, 5)):
         ch.launch(ptr, hashed=hashed)
@@ -54,7 +55,8 @@ def time_steps(ch, ptr: int, span: int, steps: int, warmup: int, hashed: bool = 
     out = {"value": round(span / dt / 2**30, 3), "unit": "GiB/s", "ms_per_step": round(dt * 1e3, 4),
            "scan_ms": round(scan_ms, 4),
            "scan_frac": round(span / (scan_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if scan_ms > 0 else None,
-           "dense_ms": round(pms[1] / max(pn, 1), 4), "resolve_ms": round(pms[2] / max(pn, 1), 4)}
+           "dense_ms": round(pms[1] / max(pn, 1), 4), "resolve_ms": round(pms[2] / max(pn, 1), 4),
+           "scan_kernel": scan["kernel"], "scan_schedule": scan["kind"]}
     if hashed:
         out["hash_ms"] = round(pms[3] / max(pn, 1), 4)
     return out
@@ -232,7 +234,7 @@ def shard_leg(device: int, steps: int, warmup: int, nshards: int = 8) -> dict:
                             "scan_ms": t["scan_ms"], "scan_frac": t["scan_frac"],
                             "step_frac": round(span / (t["ms_per_step"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                             "dense_ms": t["dense_ms"], "resolve_ms": t["resolve_ms"],
-                            "parity_mismatches": p["mismatches"]})
+                            "scan_schedule": t["scan_schedule"], "parity_mismatches": p["mismatches"]})
         finally:
             b.free()
     total = int(sizes.sum())

@@ -319,6 +319,18 @@ int32_t syncr_cdc_split_stats(syncr_cdc *h, uint64_t *stats6);
  * timing launches it has not yet fetched checks this: launches before a re-run
  * ran with the smaller capacities. */
 int32_t syncr_cdc_fetch_reruns(syncr_cdc *h, uint64_t *reruns);
+/* Which scan kernel the last launch ran (the library's own choice, made per
+ * launch from the batch size and the handle's history; a capacity re-run inside
+ * fetch counts as a launch).  kind: one of SYNCR_CDC_SCAN_*; info4 (may be NULL) =
+ * [kind, tiles, scan waves launched, tiles per wave x 1000]; *name (may be NULL)
+ * = the kernel's symbol name as a profiler shows it. */
+#define SYNCR_CDC_SCAN_NONE 0         /* no launch yet, or an empty batch             */
+#define SYNCR_CDC_SCAN_STREAM_TILES 1 /* cdc_scan_st_kernel: batches >= 24 tiles/wave */
+#define SYNCR_CDC_SCAN_CU 2           /* cdc_scan_kernel, CU schedule: small batches  */
+#define SYNCR_CDC_SCAN_TILES 3        /* cdc_scan_kernel, dynamic tile groups: large
+                                         batches after a >= 1 % dense-tile batch      */
+#define SYNCR_CDC_SCAN_DEV 255        /* development library variant                  */
+int32_t syncr_cdc_last_scan(const syncr_cdc *h, uint64_t *info4, const char **name);
 /* Engine geometry: [run_bytes, tile_bytes, scan_grid, compute_units,
  * scan_blocks_per_cu, lds_bytes_per_scan_block, device, abi_version]. */
 int32_t syncr_cdc_get_info(const syncr_cdc *h, uint64_t *info8);

@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "syncr_cache_close", "syncr_ingest_set_cache", "syncr_ingest_cache_hits",
     "syncr_ingest_open_multi", "syncr_ingest_device_stats", "syncr_cache_get_params",
     "syncr_ingest_set_read_fault", "syncr_cdc_fetch_reruns", "syncr_ingest_timing",
+    "syncr_cdc_last_scan",
 )
 
 ABI_VERSION = 3
@@ -151,6 +152,7 @@ def library():
             "syncr_cdc_split_stats": ([_vp, _pu64], _i32),
             "syncr_cdc_fetch_reruns": ([_vp, _pu64], _i32),
             "syncr_cdc_get_info": ([_vp, _pu64], _i32),
+            "syncr_cdc_last_scan": ([_vp, _pu64, ctypes.POINTER(ctypes.c_char_p)], _i32),
             "syncr_cdc_chunk_host_hashed": ([_vp, _vp, _u64, _vp, _u64, _pu64], _i32),
             "syncr_cdc_chunk_batch_host_hashed": ([_vp, _vp, _u64, _vp, _vp, _u32, _vp, _u64, _vp, _pu64], _i32),
             "syncr_cdc_launch_hashed": ([_vp, _vp, _vp], _i32),
@@ -220,9 +222,8 @@ def _u8(data) -> np.ndarray:
     return np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
 
 
-# cdc_kernels.hip SCAN_ST_MIN_TILES_PER_WAVE: batches of at least this many tiles per scan wave
-# run the stream-tile scan, smaller ones the CU schedule
-SCAN_ST_MIN_TILES_PER_WAVE = 24
+# syncr_cdc_last_scan kinds (include/syncr_cdc.h SYNCR_CDC_SCAN_*)
+SCAN_KINDS = {0: "none", 1: "stream_tiles", 2: "cu_schedule", 3: "tiles_dynamic", 255: "dev"}
 
 
 class Chunker:
@@ -370,28 +371,16 @@ class Chunker:
         _check(library().syncr_cdc_get_info(self._h, v), "syncr_cdc_get_info")
         keys = ("run_bytes", "tile_bytes", "scan_grid", "compute_units", "scan_blocks_per_cu",
                 "lds_bytes_per_scan_block", "device", "abi_version")
-        d = {k: int(x) for k, x in zip(keys, v)}
-        # info8[0] = kind * 1000 + param (cdc_api.cpp syncr_cdc_get_info)
-        d["scan_kernel"] = "cdc_scan_mfma_kernel" if d["run_bytes"] >= 1000 else "cdc_scan_kernel"
-        if d["run_bytes"] >= 1000:
-            d["mfma_blocks"] = d["run_bytes"] - 1000
-        return d
+        return {k: int(x) for k, x in zip(keys, v)}
 
-    def scan_kernel_for(self, span: int, dense_tiles: int = 0) -> str:
-        """The scan kernel a launch over `span` bytes runs (cdc_kernels.hip
-        launch_scan): stream tiles from 24 tiles per wave, the CU schedule below;
-        after a fetched launch with >= 1 % dense tiles (`dense_tiles` of that
-        launch), tiles with dynamic groups from 96 tiles per wave."""
-        d = self.info()
-        if d["run_bytes"] >= 1000:
-            return d["scan_kernel"]
-        ntiles = -(-int(span) // d["tile_bytes"]) if span else 0
-        grid = min(d["scan_grid"], ntiles) if ntiles else 0
-        if dense_tiles * 100 >= max(ntiles, 1):
-            return "cdc_scan_kernel"
-        if grid and ntiles >= grid * SCAN_ST_MIN_TILES_PER_WAVE:
-            return "cdc_scan_st_kernel"
-        return "cdc_scan_kernel"
+    def last_scan(self) -> dict:
+        """The scan kernel the library ran for the last launch (syncr_cdc_last_scan):
+        its own choice, never restated on this side."""
+        v = (ctypes.c_uint64 * 4)()
+        name = ctypes.c_char_p()
+        _check(library().syncr_cdc_last_scan(self._h, v, ctypes.byref(name)), "syncr_cdc_last_scan")
+        return {"kind": SCAN_KINDS.get(int(v[0]), str(int(v[0]))), "kernel": (name.value or b"").decode(),
+                "tiles": int(v[1]), "waves": int(v[2]), "tiles_per_wave": int(v[3]) / 1000.0}
 
     def synchronize(self) -> None:
         _check(library().syncr_cdc_synchronize(self._h), "syncr_cdc_synchronize")

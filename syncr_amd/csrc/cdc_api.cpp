@@ -120,6 +120,7 @@ struct syncr_cdc {
     hipStream_t last_stream = nullptr;  // stream of the last launch (nullptr: none since open)
     hipEvent_t xstream_ev = nullptr;    // orders a launch after the previous one on another stream
     uint64_t stats[4] = {0, 0, 0, 0};
+    uint64_t scan_info[4] = {SYNCR_CDC_SCAN_NONE, 0, 0, 0};   // syncr_cdc_last_scan
     uint64_t reruns = 0;                // capacity re-runs of the last fetch
     bool split_launched = false;        // the last launch started split workers
     uint64_t split_stats[6] = {0, 0, 0, 0, 0, 0};
@@ -454,6 +455,14 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     if (t.dbg) CHECK_HIP(hipMemsetAsync(t.dbg, 0, DBG_WORDS * sizeof(uint64_t), s));
 #endif
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[0], s));
+    {
+        const int kind = scan_kind(h->geom, h->scan_grid, kp, t);
+        const uint64_t waves = std::min<uint64_t>(h->scan_grid, t.ntiles);
+        h->scan_info[0] = (uint64_t)kind;
+        h->scan_info[1] = t.ntiles;
+        h->scan_info[2] = kind == SYNCR_CDC_SCAN_NONE ? 0u : waves;
+        h->scan_info[3] = waves ? (uint64_t)t.ntiles * 1000u / waves : 0u;
+    }
     CHECK_HIP(launch_scan(h->geom, h->scan_grid, d_bytes, kp, t, s));
     if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[1], s));
     if (order) {
@@ -781,7 +790,7 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
     try {
         CHECK_HIP(hipSetDevice(h->device));
         for (int attempt = 0; attempt < 8; attempt++) {
-            CHECK_HIP(hipStreamSynchronize(h->last_stream));
+            if (h->last_stream) CHECK_HIP(hipStreamSynchronize(h->last_stream));
             uint32_t ctr[4];
             CHECK_HIP(hipMemcpy(ctr, zblock(h, h->zlast), 16, hipMemcpyDeviceToHost));
             const uint64_t ncand = (uint64_t)ctr[CTR_CANDS_LO] | ((uint64_t)ctr[CTR_CANDS_HI] << 32);
@@ -841,11 +850,15 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
                 rerun = true;
             }
             if (rerun) {
-                int32_t rc = do_launch(h, h->last_bytes, h->last_stream);
+                int32_t rc = do_launch(h, h->last_bytes, h->last_stream ? h->last_stream : h->stream);
                 if (rc) return rc;
                 h->reruns++;
                 continue;
             }
+            // the launch is complete (synchronised above, nothing enqueued since): the
+            // caller's stream is not touched again (the header lets the caller destroy it
+            // after this fetch), so later plans / launches / fetches never use it
+            h->last_stream = nullptr;
             h->stats[0] = ncand;
             h->stats[2] = h->ntiles;
             h->stats[3] = ctr[CTR_FLAGS];
@@ -853,8 +866,8 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
                 uint32_t sp[SPL_WORDS];
                 CHECK_HIP(hipMemcpy(sp, zblock(h, h->zlast) + split_ctr_offset(h), sizeof sp,
                                     hipMemcpyDeviceToHost));
-                // dense tiles the dense pass rolled (the list counter also counts the
-                // unused slots of the scan waves' 8-slot chunks)
+                // dense tiles the dense pass rolled (in the development library's
+                // DenseSlots scans the list counter also counts unused 8-slot padding)
                 h->stats[1] = ctr[CTR_DENSE] ? sp[SPL_DENSE_TILES] : 0u;
                 // a batch with >= 1 % dense tiles: the next launch scans by tiles (stream tiles
                 // branch on every dirty 16-byte group: 6 % slower on the dense workload)
@@ -1168,6 +1181,21 @@ int32_t syncr_cdc_split_stats(syncr_cdc *h, uint64_t *stats6) {
 int32_t syncr_cdc_fetch_reruns(syncr_cdc *h, uint64_t *reruns) {
     if (!h || !reruns) return SYNCR_CDC_EINVAL;
     *reruns = h->reruns;
+    return SYNCR_CDC_OK;
+}
+
+int32_t syncr_cdc_last_scan(const syncr_cdc *h, uint64_t *info4, const char **name) {
+    if (!h) return SYNCR_CDC_EINVAL;
+    if (info4) for (int k = 0; k < 4; k++) info4[k] = h->scan_info[k];
+    if (name) {
+        switch ((int)h->scan_info[0]) {
+            case SYNCR_CDC_SCAN_STREAM_TILES: *name = "cdc_scan_st_kernel"; break;
+            case SYNCR_CDC_SCAN_CU:
+            case SYNCR_CDC_SCAN_TILES: *name = "cdc_scan_kernel"; break;
+            case SYNCR_CDC_SCAN_DEV: *name = "dev"; break;
+            default: *name = ""; break;
+        }
+    }
     return SYNCR_CDC_OK;
 }
 

@@ -314,6 +314,9 @@ int scan_blocks_per_cu(ScanGeom g);
 hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d_bytes, const KParams &p, const Tables &t,
                        hipStream_t s);
 bool scan_dense_inline(ScanGeom g, const KParams &p);      // the scan passes dense tiles itself
+// Which scan kernel launch_scan runs for this launch (SYNCR_CDC_SCAN_* of include/syncr_cdc.h):
+// the one decision, reported through syncr_cdc_last_scan so callers never restate it.
+int scan_kind(ScanGeom g, uint32_t grid, const KParams &p, const Tables &t);
 hipError_t launch_post(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s, bool dense_inline);
 hipError_t launch_resolve(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s);
 bool resolve_splits(const KParams &p, const Tables &t);   // launch_resolve starts split workers

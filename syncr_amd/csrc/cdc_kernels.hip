@@ -14,6 +14,10 @@
 //   Candidates are compacted into one sorted array (dense -> prefix ->
 //   gather), then cdc_resolve_kernel walks compute_file_chunks' loop for each
 //   file (one lane per file) applying MAX_CHUNK_SIZE and the tokio read cap.
+#include <mutex>
+#include <set>
+
+#include "../../include/syncr_cdc.h"
 #include "cdc_internal.h"
 #include "lds_dma.h"
 
@@ -663,6 +667,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             } else {
                 if (gj == 0) {                                       // group ends at its first tile (last round)
                     if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
+                    grabbed = true;                                  // (no second grab below: it would drop a group)
                 }
                 wait_vmcnt<0>();                                     // the grab
                 next = gbase(stride + (uint32_t)__builtin_amdgcn_readfirstlane(pend));
@@ -1246,6 +1251,7 @@ void cdc_scan3_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             } else {
                 if (gj == 0) {
                     if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
+                    grabbed = true;
                 }
                 wait_vmcnt<0>();                                     // the grab
                 next = gbase(stride + (uint32_t)__builtin_amdgcn_readfirstlane(pend));
@@ -3540,18 +3546,30 @@ hipError_t launch_read_probe(const uint8_t *d, uint64_t bytes, bool nt, uint32_t
 // The CU schedule: one workgroup of SCAN_CU_WAVES waves per CU (grid = the
 // per-wave grid / SCAN_CU_WAVES), plus the LDS tile counter.
 constexpr int SCAN_CU_WAVES = 8;
+// The > 64 KB dynamic-LDS attribute is set once per (kernel instance, device), under
+// a lock: multi-device ingest opens and launches handles from several threads.
 template <int RUN, int MODE>
-static void launch_scan_cu(uint32_t wave_grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
+static hipError_t launch_scan_cu(uint32_t wave_grid, const uint8_t *d, const KParams &p, const Tables &t,
+                                 hipStream_t s) {
     const size_t lds = (size_t)SCAN_CU_WAVES * lds_wave_bytes(RUN) + 16 + 8 * CU_NSLOT;
     const void *f = (const void *)&cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>;
-    static bool attr = false;
-    if (!attr) {                                   // > 64 KB of dynamic LDS per workgroup
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
+    {
+        static std::mutex mu;
+        static std::set<int> done;                 // devices whose attribute is set
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        std::lock_guard<std::mutex> g(mu);
+        if (!done.count(dev)) {
+            e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            done.insert(dev);
+        }
     }
     uint32_t grid = (wave_grid + SCAN_CU_WAVES - 1) / SCAN_CU_WAVES;
     hipLaunchKernelGGL((cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>), dim3(grid), dim3(64 * SCAN_CU_WAVES), lds, s,
                        d, p, t);
+    return hipGetLastError();
 }
 
 #ifdef SYNCR_CDC_DEV
@@ -3624,9 +3642,9 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
     else if (p.ablate == 17u)                                        // A/B: stream-tile scan (exact)
         hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else if (p.ablate == 15u) {                                      // A/B: CU schedule (exact)
-        launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s);
+        (void)launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s);
     } else if (p.ablate == 16u) {                                    // timing only: CU schedule, no warm-up/halo
-        launch_scan_cu<RUN, 4 | 16 | 256 | 512>(grid, d, p, t, s);
+        (void)launch_scan_cu<RUN, 4 | 16 | 256 | 512>(grid, d, p, t, s);
     }
     else if (p.ablate == 12u)                                        // timing only: no closed-form warm-up
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256>), dim3(grid), dim3(64), lds, s, d, p, t);
@@ -3643,7 +3661,7 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
     else if (p.nt && scan_dynamic(t.ntiles, grid))                   // other geometries: nt + dynamic groups + ROLL2
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.nt)                                                   // product, small batch: CU schedule
-        launch_scan_cu<RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);
+        (void)launch_scan_cu<RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);
     else
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE & ~4>), dim3(grid), dim3(64), lds, s, d, p, t);
 }
@@ -3729,17 +3747,29 @@ hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParam
                        hipStream_t s) {
     if (!t.ntiles) return hipSuccess;
     if (!scan_supported(g)) return hipErrorInvalidValue;
+    const int kind = scan_kind(g, grid, p, t);
     grid = grid < t.ntiles ? grid : t.ntiles;
-    if (p.scan_tiles && scan_dynamic(t.ntiles, grid))   // the handle's last batch was dense-heavy:
-        hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),   // tiles
+    if (kind == SYNCR_CDC_SCAN_TILES)             // the handle's last batch was dense-heavy: tiles
+        hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
                            lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
-    else if (!p.scan_tiles && scan_stream_tiles(t.ntiles, grid))   // >= 4 stream tiles per wave (§4.6)
+    else if (kind == SYNCR_CDC_SCAN_STREAM_TILES) // >= 3 stream tiles per wave (§4.6)
         hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else                                          // small batch: the CU schedule (per-wave static shares end
-        launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);   // with the slow waves alone)
+        return launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);   // with the slow waves alone)
     return hipGetLastError();
 }
 #endif
+
+// The product's choice between its three exact scans (the dev library's
+// variants, other geometries and ablations report SYNCR_CDC_SCAN_DEV).
+int scan_kind(ScanGeom g, uint32_t grid, const KParams &p, const Tables &t) {
+    if (!t.ntiles) return SYNCR_CDC_SCAN_NONE;
+    if (g.kind != SCAN_VALU || g.param != DEFAULT_RUN || p.ablate != 0u || !p.nt) return SYNCR_CDC_SCAN_DEV;
+    grid = grid < t.ntiles ? grid : t.ntiles;
+    if (p.scan_tiles && scan_dynamic(t.ntiles, grid)) return SYNCR_CDC_SCAN_TILES;
+    if (!p.scan_tiles && scan_stream_tiles(t.ntiles, grid)) return SYNCR_CDC_SCAN_STREAM_TILES;
+    return SYNCR_CDC_SCAN_CU;
+}
 
 int scan_blocks_per_cu(ScanGeom g) {
     int n = 0;

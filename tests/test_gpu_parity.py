@@ -370,7 +370,7 @@ def test_product_ignores_environment(kat_cases, monkeypatch):
         monkeypatch.setenv(k, v)
     with syncr_amd.Chunker() as ch:
         info = ch.info()
-        assert info["run_bytes"] == 144 and info["scan_kernel"] == "cdc_scan_kernel" and info["scan_grid"] > 3
+        assert info["run_bytes"] == 144 and info["scan_grid"] > 3
         data = O.xorshift_bytes(4242, 12 * M + 77)
         got = ch.chunk_bytes(data, hashed=True)
         ends = [c.offset + c.size for c in got]
@@ -703,6 +703,11 @@ def test_small_batches_back_to_back_stable():
             ch.close()
 
 
+# cdc_kernels.hip SCAN_ST_MIN_TILES_PER_WAVE / SCAN_DYN_MIN_TILES_PER_WAVE: the tests pin the
+# library's choice at these thresholds through syncr_cdc_last_scan (the host never restates it)
+SCAN_ST_MIN_TILES_PER_WAVE = 24
+SCAN_DYN_MIN_TILES_PER_WAVE = 96
+
 @pytest.mark.parametrize("below", [False, True])
 def test_stream_tile_threshold_edge_vs_oracle(below):
     """The two scans either side of SCAN_ST_MIN_TILES_PER_WAVE (cdc_kernels.hip
@@ -718,7 +723,7 @@ def test_stream_tile_threshold_edge_vs_oracle(below):
     try:
         info = ch.info()
         tb = info["tile_bytes"]
-        ntiles = info["scan_grid"] * syncr_amd.SCAN_ST_MIN_TILES_PER_WAVE
+        ntiles = info["scan_grid"] * SCAN_ST_MIN_TILES_PER_WAVE
         span = (ntiles - 1) * tb + (0 if below else 1)
         lens = []
         while sum(lens) < span:
@@ -731,7 +736,6 @@ def test_stream_tile_threshold_edge_vs_oracle(below):
         offs[1:] = np.cumsum(lens)[:-1]
         assert int(lens.sum()) == span
         want = "cdc_scan_kernel" if below else "cdc_scan_st_kernel"
-        assert ch.scan_kernel_for(span) == want
         buf = syncr_amd.DeviceBuffer(ch, span)
         try:
             buf.gen_corpus(offs, lens, indices=np.arange(lens.size, dtype=np.uint64) + 7001)
@@ -744,6 +748,9 @@ def test_stream_tile_threshold_edge_vs_oracle(below):
             ch.plan(offs, lens, span)
             ch.launch(buf.ptr)
             res = ch.fetch()
+            rep = ch.last_scan()                   # the library's own report (syncr_cdc_last_scan)
+            assert rep["kernel"] == want and rep["kind"] == ("cu_schedule" if below else "stream_tiles"), rep
+            assert rep["tiles"] == ntiles - below and rep["waves"] == info["scan_grid"], rep
             host = buf.download(span)
             print(f"{want} edge batch: {lens.size} files, {span} bytes; oracle next", flush=True)
         finally:
@@ -775,7 +782,6 @@ def test_large_batch_stream_tiles_vs_oracle(bits, cap):
         offs = np.zeros_like(lens)
         offs[1:] = np.cumsum(lens)[:-1]
         span = int(lens.sum())
-        assert ch.scan_kernel_for(span) == "cdc_scan_st_kernel"
         buf = syncr_amd.DeviceBuffer(ch, span)
         try:
             buf.gen_corpus(offs, lens, indices=np.arange(lens.size, dtype=np.uint64) + 100003)
@@ -788,6 +794,7 @@ def test_large_batch_stream_tiles_vs_oracle(bits, cap):
             ch.plan(offs, lens, span)
             ch.launch(buf.ptr)
             res = ch.fetch()
+            assert ch.last_scan()["kind"] == "stream_tiles", ch.last_scan()
             host = buf.download(span)
             print(f"stream-tile batch: {lens.size} files, {span / 2**30:.2f} GiB chunked; oracle next", flush=True)
         finally:
@@ -799,3 +806,89 @@ def test_large_batch_stream_tiles_vs_oracle(bits, cap):
         assert not bad, bad[:10]
     finally:
         ch.close()
+
+
+def test_dense_heavy_handle_large_batch_dynamic_tiles_vs_oracle():
+    """after a batch with >= 1 % dense tiles a handle scans its
+    next large batches (>= 96 tiles per wave) by tiles with dynamic groups.  A
+    batch whose tile count leaves a partial last round (ntiles % (8 x grid) in
+    [1, 2 x grid)) makes groups that end at their first tile; a lost grab there
+    used to drop a group (its candidates vanished without an error).  One
+    handle: a dense-heavy batch first, then such a batch of random, periodic-64
+    and constant files; the library must report the tile scan, and every file's
+    cuts must equal the oracle's."""
+    from benchlib.workloads import periodic_pattern
+    bits, cap = 20, 2 << 20
+    rng = np.random.default_rng(96)
+    ch = syncr_amd.Chunker(chunk_bits=bits, max_chunk=16 << 20, read_cap=cap)
+    try:
+        info = ch.info()
+        tb, grid = info["tile_bytes"], info["scan_grid"]
+        pat = periodic_pattern()
+        # 1: a dense-heavy batch (periodic data: every tile dense)
+        dense = np.resize(pat, 64 << 20)
+        first = ch.batch_arrays(dense, [0], [dense.size])[0]
+        assert ends_of(first) == O.chunk_production_window(dense).tolist()
+        assert ch.last_stats()["dense_tiles"] * 100 >= -(-dense.size // tb)
+        # 2: the large batch, a partial last round of single-tile groups
+        rounds = -(-grid * SCAN_DYN_MIN_TILES_PER_WAVE // (8 * grid))
+        ntiles = rounds * 8 * grid + grid // 2 + 3
+        span = (ntiles - 1) * tb + 777
+        lens = []
+        while sum(lens) < span:
+            lens.append(int(rng.integers(1, 64 << 20)))
+        lens[-1] -= sum(lens) - span
+        if lens[-1] == 0:
+            lens.pop()
+        lens = np.array(lens, np.uint64)
+        offs = np.zeros_like(lens)
+        offs[1:] = np.cumsum(lens)[:-1]
+        buf = syncr_amd.DeviceBuffer(ch, span)
+        try:
+            buf.gen_corpus(offs, lens, indices=np.arange(lens.size, dtype=np.uint64) + 960001)
+            for i in range(lens.size):
+                if i % 16 == 5:
+                    buf.upload(np.resize(pat, int(lens[i])), offset=int(offs[i]))
+                elif i % 16 == 11:
+                    buf.upload(np.full(int(lens[i]), 0x3C, np.uint8), offset=int(offs[i]))
+            ch.plan(offs, lens, span)
+            ch.launch(buf.ptr)
+            rep = ch.last_scan()
+            assert rep["kind"] == "tiles_dynamic" and rep["kernel"] == "cdc_scan_kernel", rep
+            assert rep["tiles"] == ntiles and ntiles % (8 * grid) in range(1, 2 * grid), rep
+            res = ch.fetch()
+            host = buf.download(span)
+            print(f"dynamic-tile batch: {lens.size} files, {span / 2**30:.2f} GiB; oracle next", flush=True)
+        finally:
+            buf.free()
+        ref = O.chunk_batch(host, offs, lens, bits=bits, read_cap=cap, mode=O.MODE_PRODUCTION_WINDOW)
+        bad = [i for i in range(lens.size) if ends_of(res[i]) != ref[i].tolist()]
+        assert not bad, bad[:10]
+    finally:
+        ch.close()
+
+
+def test_stream_destroyed_after_fetch():
+    """the header lets a caller destroy its stream once the launch on
+    it has been fetched.  Launch on a caller stream (another handle's, destroyed
+    with that handle), fetch, destroy it, then plan, launch on the handle's own
+    stream and fetch again: nothing may touch the destroyed stream, and the cuts
+    stay exact."""
+    data = O.xorshift_bytes(515, 9 * M + 3)
+    want = O.chunk_production(data).tolist()
+    with syncr_amd.Chunker() as ch:
+        buf = syncr_amd.DeviceBuffer(ch, data.size)
+        try:
+            buf.upload(data)
+            for rep in range(3):
+                other = syncr_amd.Chunker()
+                ch.plan([0], [data.size], data.size)
+                ch.launch(buf.ptr, stream=other.stream)
+                assert ends_of(ch.fetch()[0]) == want
+                other.close()                           # destroys the stream the launch ran on
+                ch.plan([0], [data.size], data.size)
+                ch.launch(buf.ptr)
+                assert ends_of(ch.fetch()[0]) == want
+                ch.synchronize()
+        finally:
+            buf.free()
