@@ -793,9 +793,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 // right after it is rolled, from the packed pairs it added and dropped (still
 // in registers then) and its entry state.
 // ---------------------------------------------------------------------------
-constexpr int ST_RUN = 128;                   // bytes per segment and stream
-constexpr int ST_SEGS = 9;                    // segments per stream: 1152-byte streams
-constexpr int ST_TILES = 8;                   // batch tiles per ST
+constexpr int ST_RUN = 128;                   // bytes per segment and stream (ST_SEGS of them: 1152-byte streams)
 constexpr int ST_LISTCAP = 32;                // candidate slots per tile (more: dense)
 constexpr int ST_DIRTYCAP = 6;                // side slots per segment
 constexpr uint32_t ST_L = ST_SEGS * ST_RUN;   // stream bytes
@@ -837,6 +835,53 @@ __device__ __forceinline__ void publish_list(const Tables &T, uint32_t tile, con
     }
 }
 
+// Publish part `part` (of T.st_parts) of a split ST's tile: its sorted list into
+// the part's slot range and its count into T.tail_meta, or request the dense
+// pass for the tile (ST_TILES comment in cdc_internal.h).
+template <class DS>
+__device__ __forceinline__ void publish_part(const Tables &T, uint32_t tile, const uint32_t *list, uint32_t n,
+                                             int lane, bool force_dense, uint32_t part, DS &ds) {
+    const uint32_t ss = (uint32_t)LISTCAP / T.st_parts;        // slots per part
+    const bool dense = force_dense || n > ss || n > (uint32_t)ST_LISTCAP;
+    if (n == 0u && !dense) return;
+    uint32_t old = 0;
+    if (lane == 0)
+        old = atomicOr(&T.tail_meta[tile - T.tail_tile0], dense ? TAIL_DENSE : n << (TAIL_PART_BITS * part));
+    old = (uint32_t)__builtin_amdgcn_readfirstlane(old);
+    if (old & TAIL_DENSE) return;                              // another part sent the tile to the dense pass
+    if (lane == 0) atomicOr(&T.nonempty[tile >> 6], 1ull << (tile & 63));
+    if (dense) {
+        // the first part to find the tile dense takes back what the parts before it added
+        uint32_t prior = 0;
+        for (uint32_t q = 0; q < T.st_parts; ++q) prior += tail_part_count(old, q);
+        if (lane == 0 && prior) {
+            atomicSub(&T.super_cnt[tile >> 6], prior);
+            atomicSub(&T.coarse[(tile >> 12) * COARSE_STRIDE], prior);
+        }
+        dense_mark(T, tile, lane, ds);
+        return;
+    }
+    const uint32_t e = (uint32_t)lane < n ? list[lane] : 0xffffffffu;
+    uint32_t rank = 0;
+    for (uint32_t m = 0; m < n; ++m) rank += list[m] < e;
+    if ((uint32_t)lane < n) T.slots[(size_t)tile * LISTCAP + part * ss + rank] = make_uint2(e, 0u);
+    if (lane == 0) {
+        atomicAdd(&T.super_cnt[tile >> 6], n);
+        atomicAdd(&T.coarse[(tile >> 12) * COARSE_STRIDE], n);
+    }
+}
+
+// Work unit u of the stream-tile scan: ST `st`, segments [g0, g1); part ~0u: a whole ST
+struct StUnit {
+    uint32_t st, g0, g1, part;
+};
+__device__ __forceinline__ StUnit st_unit(const Tables &T, uint32_t u) {
+    if (u < T.st_full) return {u, 0u, (uint32_t)ST_SEGS, ~0u};
+    const uint32_t v = u - T.st_full, part = v / T.st_tail;
+    return {T.st_full + v % T.st_tail, part * (uint32_t)ST_SEGS / T.st_parts,
+            (part + 1u) * (uint32_t)ST_SEGS / T.st_parts, part};
+}
+
 template <int MODE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
@@ -853,7 +898,8 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     uint32_t *tlist = (uint32_t *)(smem + RUNS * RUN + ST_DIRTYCAP * sizeof(DirtySlotST));
     uint32_t *tcnt = tlist + ST_TILES * ST_LISTCAP;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
-    const uint32_t nst = (T.ntiles + ST_TILES - 1) / ST_TILES;
+    // work units: st_full whole STs, then st_tail STs in st_parts parts each
+    const uint32_t nunits = T.st_full + T.st_tail * T.st_parts;
     const int64_t span = (int64_t)T.span;
     // DMA instruction i, lane l fills slot 64 i + l = stream 8 i + l / 8, physical piece l % 8,
     // which holds logical piece (l % 8) ^ ((l / 8) & 7): a per-lane offset fixed for the kernel
@@ -882,10 +928,10 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             }
         }
     };
-    // the 64 bytes before each of this lane's two streams (segment 0's warm-up)
+    // the 64 bytes before segment g0 of each of this lane's two streams (the unit's warm-up)
     uint32_t HA[16], HB[16];
-    auto load_halo = [&](uint32_t st) {
-        const int64_t sa = (int64_t)st * STB + (int64_t)lane * L - 64, sbb = sa + 64 * (int64_t)L;
+    auto load_halo = [&](uint32_t st, uint32_t g0) {
+        const int64_t sa = (int64_t)st * STB + (int64_t)lane * L + (int64_t)g0 * RUN - 64, sbb = sa + 64 * (int64_t)L;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             uint4 va, vb;
@@ -896,16 +942,18 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             HB[4 * m] = vb.x; HB[4 * m + 1] = vb.y; HB[4 * m + 2] = vb.z; HB[4 * m + 3] = vb.w;
         }
     };
-    uint32_t st = blockIdx.x;
-    if (st >= nst) return;
+    if (blockIdx.x >= nunits) return;
+    StUnit un = st_unit(T, blockIdx.x);
+    uint32_t st = un.st;
     const bool stamp = blockIdx.x < (uint32_t)DBG_SCAN_N;              // timeline slot (dev)
     if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x, wall_clock64());
 #ifdef SYNCR_CDC_DEV
     uint32_t nst_done = 0;
 #endif
-    issue_seg(st, 0);
-    load_halo(st);
-    uint32_t pend = 0, nextst = 0;
+    issue_seg(st, un.g0);
+    load_halo(st, un.g0);
+    uint32_t pend = 0, nextu = 0;
+    StUnit nun = un;
     uint32_t nth = 0;                              // this wave's STs so far (wave-uniform)
     DensePend dslots_alloc;
     // (a ping-pong of two carried arrays, segments unrolled in pairs to drop the 64 moves
@@ -916,8 +964,8 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     uint32_t dmark = 0;                            // tiles (bit t) holding a dirty group no slot took
     for (;;) {
 #pragma unroll 1
-        for (uint32_t g = 0; g < (uint32_t)ST_SEGS; ++g) {
-            const bool first = g == 0u;
+        for (uint32_t g = un.g0; g < un.g1; ++g) {
+            const bool first = g == un.g0;
             if (first && lane < ST_TILES) tcnt[lane] = 0u;
             uint32_t have = 0;                                       // dirty slots taken (wave-uniform)
             wait_vmcnt<0>();                                         // segment g landed (and, at 0, the halo)
@@ -950,7 +998,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // segment in registers: buffer free
             bool more = true;
-            if (g + 1 < (uint32_t)ST_SEGS) {
+            if (g + 1 < un.g1) {
                 issue_seg(st, g + 1);
                 // the next ST comes from a counter, grabbed behind the next segment's DMAs and
                 // late in the ST (a wave that binds its next ST early can be a slow one holding
@@ -958,17 +1006,19 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 // (grabbing at segment 0 before its landing wait put every wave of the grid on
                 // one address at launch: the first segment landed 18.7 us after entry, median,
                 // tools/scan_timeline.py)
-                if (g == (nth == 0u ? 4u + (blockIdx.x & 3u) : (uint32_t)ST_SEGS - 2u) && nst > gridDim.x) {
+                // (a part of a split ST grabs at its second-to-last segment too: parts have >= 2)
+                if (g == (nth == 0u ? 4u + (blockIdx.x & 3u) : un.g1 - 2u) && nunits > gridDim.x) {
                     // (the compiler waits for the result at once -- its copy into the
                     // loop-carried register -- but segment 1's DMAs are in flight by then)
                     if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
                 }
             } else {
-                nextst = nst > gridDim.x ? gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nst;
-                more = nextst < nst;
+                nextu = nunits > gridDim.x ? gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nunits;
+                more = nextu < nunits;
                 if (more) {
-                    issue_seg(nextst, 0);
-                    load_halo(nextst);
+                    nun = st_unit(T, nextu);
+                    issue_seg(nun.st, nun.g0);
+                    load_halo(nun.st, nun.g0);
                 }
             }
             // ---- roll segment g: positions 0..63 drop Pd, later ones this segment's own pairs
@@ -1058,7 +1108,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                     }
                 }
             }
-            if (g + 1 == (uint32_t)ST_SEGS) {                        // the ST's tiles are complete: publish
+            if (g + 1 == un.g1) {                                    // the unit's tiles are complete: publish
                 if (__builtin_expect(__ballot(dmark != 0u) != 0ull, 0)) {   // tiles with unrecorded dirty groups
                     uint32_t m = 0;
 #pragma unroll
@@ -1076,8 +1126,12 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                     const uint32_t c = __builtin_amdgcn_readfirstlane(
                         __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)&tcnt[t], __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WAVEFRONT));
-                    publish_list(T, tile, tlist + t * ST_LISTCAP, c & 0x7fffffffu, lane, (c >> 31) != 0u,
-                                 dslots_alloc);
+                    if (un.part == ~0u)
+                        publish_list(T, tile, tlist + t * ST_LISTCAP, c & 0x7fffffffu, lane, (c >> 31) != 0u,
+                                     dslots_alloc);
+                    else
+                        publish_part(T, tile, tlist + t * ST_LISTCAP, c & 0x7fffffffu, lane, (c >> 31) != 0u,
+                                     un.part, dslots_alloc);
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -1096,7 +1150,8 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 return;
             }
         }
-        st = nextst;
+        un = nun;
+        st = un.st;
         ++nth;
 #ifdef SYNCR_CDC_DEV
         ++nst_done;
@@ -2140,6 +2195,50 @@ __device__ __forceinline__ uint64_t word_prefix(const Tables &T, uint32_t w, int
     return readlane64(wave_sum64(a), 0);
 }
 
+// A nonempty tile's candidate count for the compaction, its tile_meta (DENSE_BIT |
+// dense index, else 0 or the count) and, for a tile of the stream-tile scan's split
+// last round (not sent to the dense pass), its tail_meta word (else 0).
+__device__ __forceinline__ uint32_t tile_cands(const Tables &T, uint32_t tile, uint32_t &meta, uint32_t &tm) {
+    tm = 0u;
+    if (tile >= T.tail_tile0) {
+        const uint32_t w = T.tail_meta[tile - T.tail_tile0];
+        if (!(w & TAIL_DENSE)) {
+            uint32_t c = 0;
+            for (uint32_t q = 0; q < T.st_parts; ++q) c += tail_part_count(w, q);
+            meta = 0u;
+            tm = w;
+            return c;
+        }
+    }
+    meta = T.tile_meta[tile];
+    if (meta & DENSE_BIT) {
+        const uint32_t idx = meta & ~DENSE_BIT;
+        return (!T.dense_off && idx < T.dense_cap) ? T.dense_cnt[idx] & ~DENSE_FIXED : 0u;
+    }
+    return meta;
+}
+
+// The candidates of a split tile in position order: each part's list is sorted,
+// so an element's rank is its index plus the elements of the other parts below it.
+__device__ __forceinline__ void copy_split_tile(const Tables &T, uint32_t tile, uint32_t tm, uint64_t base) {
+    const uint32_t ss = (uint32_t)LISTCAP / T.st_parts;
+    const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
+    const uint64_t t0 = (uint64_t)tile * T.tile;
+    for (uint32_t p = 0; p < T.st_parts; ++p) {
+        const uint32_t np = tail_part_count(tm, p);
+        for (uint32_t i = 0; i < np; ++i) {
+            const uint32_t e = sl[p * ss + i].x;
+            uint32_t rank = i;
+            for (uint32_t q = 0; q < T.st_parts; ++q) {
+                if (q == p) continue;
+                const uint32_t nq = tail_part_count(tm, q);
+                for (uint32_t j = 0; j < nq; ++j) rank += sl[q * ss + j].x < e;
+            }
+            T.cand[base + rank] = t0 + e;
+        }
+    }
+}
+
 // Dense tiles are expanded by the blocks past the word blocks, one wave per
 // dense tile (grid-stride over the dense list): a word of 64 dense tiles on
 // one wave was 64 dependent bitmap passes (dense1: 330 us for 2.1 M candidates).
@@ -2156,13 +2255,8 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
         const uint32_t tl = w * 64 + (uint32_t)lane;
         uint32_t c = 0;
         if ((bits >> lane) & 1ull) {
-            const uint32_t meta = T.tile_meta[tl];
-            if (meta & DENSE_BIT) {
-                const uint32_t di = meta & ~DENSE_BIT;
-                c = di < T.dense_cap ? T.dense_cnt[di] & ~DENSE_FIXED : 0u;
-            } else {
-                c = meta;
-            }
+            uint32_t meta, tm;
+            c = tile_cands(T, tl, meta, tm);
         }
         const uint32_t incl = wave_incl_scan(c, lane);
         const uint32_t j = tile & 63u;
@@ -2221,23 +2315,19 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
     if (!bits) return;
     const uint32_t tile = w * 64 + lane;
     const bool has = (bits >> lane) & 1ull;
-    uint32_t meta = 0, c = 0;
-    if (has) {
-        meta = T.tile_meta[tile];
-        if (meta & DENSE_BIT) {
-            const uint32_t idx = meta & ~DENSE_BIT;
-            c = (!T.dense_off && idx < T.dense_cap) ? T.dense_cnt[idx] & ~DENSE_FIXED : 0u;
-        } else {
-            c = meta;
-        }
-    }
+    uint32_t meta = 0, c = 0, tm = 0;
+    if (has) c = tile_cands(T, tile, meta, tm);
     const uint32_t incl = wave_incl_scan(c, lane);
     const uint64_t base = pre + (incl - c);
     const bool dense = has && (meta & DENSE_BIT) && c;
     if (has && c && !dense && base + c <= T.cand_cap) {   // overflow is flagged by prefix; host re-runs
-        const uint64_t t0 = (uint64_t)tile * T.tile;
-        const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
-        for (uint32_t j = 0; j < c; ++j) T.cand[base + j] = t0 + sl[j].x;    // fix-up: cdc_fix_kernel
+        if (__builtin_expect(tm != 0u, 0)) {
+            copy_split_tile(T, tile, tm, base);               // parts of a split ST: merge
+        } else {
+            const uint64_t t0 = (uint64_t)tile * T.tile;
+            const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
+            for (uint32_t j = 0; j < c; ++j) T.cand[base + j] = t0 + sl[j].x;    // fix-up: cdc_fix_kernel
+        }
     }
     (void)dense;                                               // dense tiles: gather_dense
 }

@@ -1,0 +1,91 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the per-run gpu_r04*.sh scripts).
+# Each STEP runs under its own time limit; the first failure ends the call.
+# Outputs go to gpurun_out/<TAG>_<step>*.
+#
+#   bash tools/gpu.sh TAG STEP [STEP ...]
+#
+# STEP (arguments separated by '|'):
+#   tests[|<pytest -k expr>]            product library, pytest -m gpu
+#   devtests|<ENV=V,...>[|<-k expr>]    the GPU suite on libsyncr_cdc_dev.so with a variant forced
+#   smoke                               __graft_entry__.smoke()
+#   bench[|<extra bench.py flags>]      the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
+#   ab|<workload>|<rounds>|<V1>|<V2>... tools/dip_ab.py variants (dev library) in the driver's condition
+#   trace|<workload>[|<shard>]          kernel trace of one small-batch leg (tools/legs_trace.py, product)
+#   sttrace|<workload>|<ENV=V,...>      per-wave stream-tile scan timeline (tools/scan_timeline.py, dev)
+#   prof|<PROFTAG>[|<extra flags>]      tools/prof.sh: trace + traffic + SQ passes of the driver's command
+#   build                               python -m syncr_amd.build (+ --dev) on the box (normally built here)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+O=$R/gpurun_out
+mkdir -p "$O"
+TAG=$1
+shift
+export TMPDIR=/tmp
+
+envrun() {   # envrun "A=1,B=2" cmd...: run cmd with the comma-separated variables set
+    local kv=$1; shift
+    ( IFS=','; for x in $kv; do [ -n "$x" ] && export "$x"; done; "$@" )
+}
+
+n=0
+for step in "$@"; do
+    n=$((n + 1))
+    IFS='|' read -r -a a <<< "$step"
+    kind=${a[0]}
+    out="$O/${TAG}_${n}_${kind}"
+    echo "== step $n: $step"
+    case "$kind" in
+    tests)
+        K=(); [ -n "${a[1]}" ] && K=(-k "${a[1]}")
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" > "$out.log" 2>&1 \
+            || { echo "tests failed rc=$?"; tail -40 "$out.log"; exit 11; }
+        tail -2 "$out.log" ;;
+    devtests)
+        K=(); [ -n "${a[2]}" ] && K=(-k "${a[2]}")
+        envrun "SYNCR_TEST_DEV_LIBRARY=1,${a[1]}" timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 \
+            --timeout-method thread "${K[@]}" > "$out.log" 2>&1 || { echo "devtests failed rc=$?"; tail -40 "$out.log"; exit 12; }
+        tail -2 "$out.log" ;;
+    smoke)
+        timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out.log" 2>&1 \
+            || { echo "smoke failed rc=$?"; tail -20 "$out.log"; exit 13; }
+        tail -c 300 "$out.log"; echo ;;
+    bench)
+        timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 ${a[1]} > "$out.json" 2> "$out.err" \
+            || { echo "bench failed rc=$?"; tail -30 "$out.err"; exit 14; }
+        python tools/bench_summary.py "$out.json" ;;
+    ab)
+        timeout -k 10 600 python -u tools/dip_ab.py "${a[@]:3}" --workload "${a[1]}" --rounds "${a[2]}" > "$out.jsonl" 2> "$out.err" \
+            || { echo "ab failed rc=$?"; tail -30 "$out.err"; exit 15; }
+        python - "$out.jsonl" <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    d = json.loads(l)
+    print(d["workload"], {v: (x["scan_ms_med"], x["step_ms_med"]) for v, x in d["variants"].items()})
+PY
+        ;;
+    trace)
+        P=$O/${TAG}_${n}_trace_${a[1]}
+        mkdir -p "$P"
+        SH=${a[2]:-0}
+        ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$P" -o run -- \
+            python3 "$R/tools/legs_trace.py" --workload "${a[1]}" --shard "$SH" > "$P/leg.json" 2> "$P/leg.err" ) \
+            || { echo "trace failed rc=$?"; tail -20 "$P/leg.err"; exit 16; }
+        f=$(find "$P" -name '*kernel_trace.csv' | head -1)
+        nb=$(python3 -c "import json;print(json.loads(open('$P/leg.json').read().strip().splitlines()[-1])['bytes'])")
+        python3 tools/legs_trace_show.py "$f" 20 5 "$nb" > "$P/steps.json" && cat "$P/steps.json" | head -30 ;;
+    sttrace)
+        envrun "${a[2]}" timeout -k 10 300 python -u tools/scan_timeline.py --workload "${a[1]}" > "$out.json" 2> "$out.err" \
+            || { echo "sttrace failed rc=$?"; tail -20 "$out.err"; exit 17; }
+        head -c 1500 "$out.json"; echo ;;
+    prof)
+        bash tools/prof.sh "${a[1]}" ${a[2]} || { echo "prof failed rc=$?"; exit 18; } ;;
+    build)
+        timeout -k 10 900 python -m syncr_amd.build --force > "$out.log" 2>&1 && \
+        timeout -k 10 900 python -m syncr_amd.build --force --dev >> "$out.log" 2>&1 || { echo "build failed"; exit 19; } ;;
+    *)
+        echo "unknown step $kind"; exit 2 ;;
+    esac
+done
+echo "gpu.sh $TAG: all steps done"

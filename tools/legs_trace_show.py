@@ -23,7 +23,9 @@ def main():
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     rows = [(short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
     rows = [r for r in rows if r[0].startswith(("cdc_", "b3_"))]
-    starts = [k for k, r in enumerate(rows) if r[0] == "cdc_scan_kernel"]
+    SCANS = ("cdc_scan_kernel", "cdc_scan_st_kernel")           # the scan a step starts with (any schedule)
+    rows = [("scan" if r[0] in SCANS else r[0], r[1], r[2]) for r in rows]
+    starts = [k for k, r in enumerate(rows) if r[0] == "scan"]
     steps = []
     for j, k in enumerate(starts):
         end = starts[j + 1] if j + 1 < len(starts) else len(rows)
@@ -46,9 +48,9 @@ def main():
     mean = lambda v: round(sum(v) / len(v), 2) if v else None   # noqa: E731
     out = {"steps_in_window": len(window), "kernel_us": {k: mean(v) for k, v in dur.items()},
            "gap_us": {k: mean(v) for k, v in gap.items()}, "period_us": mean(period),
-           "scan_us_each": [round(v, 1) for v in dur["cdc_scan_kernel"]]}
+           "scan_us_each": [round(v, 1) for v in dur["scan"]]}
     if nbytes:
-        out["scan_frac_8tbs"] = round(nbytes / (out["kernel_us"]["cdc_scan_kernel"] / 1e6) / 8e12, 4)
+        out["scan_frac_8tbs"] = round(nbytes / (out["kernel_us"]["scan"] / 1e6) / 8e12, 4)
         if out["period_us"]:
             out["period_frac_8tbs"] = round(nbytes / (out["period_us"] / 1e6) / 8e12, 4)
     print(json.dumps(out, indent=1))
