@@ -2332,6 +2332,128 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
     (void)dense;                                               // dense tiles: gather_dense
 }
 
+// Compaction and head fix-ups in one launch, for launches with no dense pass and
+// no chain links (random data, the common case: cdc_gather_kernel followed by
+// cdc_fix_kernel otherwise).  A word wave computes its 64 tiles' output offsets as
+// the gather does, stages the word's candidates (word-relative positions, in
+// order) in LDS 128 at a time, and rolls their head fix-ups two per lane as
+// cdc_fix_kernel does: every candidate is written once, complete (CAND_KNOWN).
+// The blocks past the word blocks compute the read-boundary grid points' fix-ups.
+// One dependent launch fewer per step: on small batches (BASELINE config 4's
+// per-rank shards, 1 GiB) the chain of short post-scan launches is ~10 % of a step.
+__global__ __launch_bounds__(256) void cdc_gather_fix_kernel(const uint8_t *__restrict__ data, KParams P,
+                                                             Tables T) {
+    __shared__ uint32_t lpos[4][128];
+    const uint32_t wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wblocks = (T.nwords + 3) / 4;
+    if (blockIdx.x >= wblocks) {                              // grid points, two per lane
+        const uint32_t nthr = (gridDim.x - wblocks) * 256;
+        for (uint64_t q = (uint64_t)(blockIdx.x - wblocks) * 256 + threadIdx.x; 2 * q < T.ngrid; q += nthr) {
+            uint64_t a[2] = {0, 0};
+            uint32_t n[2] = {0, 0};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint64_t i = 2 * q + (uint64_t)h;
+                if (i < T.ngrid) {
+                    a[h] = T.gpos[i];
+                    const uint64_t end = T.gend[i];
+                    n[h] = (uint32_t)min<uint64_t>(63ull, end > a[h] ? end - a[h] : 0ull);
+                }
+            }
+            uint32_t A[16], B[16], fA = 0u, fB = 0u;
+            fix_load(data, T.span, a[0], n[0], A);
+            fix_load(data, T.span, a[1], n[1], B);
+            fix_pair(A, B, n[0], n[1], P, fA, fB);
+            T.gfix[2 * q] = (uint8_t)fA;
+            if (2 * q + 1 < T.ngrid) T.gfix[2 * q + 1] = (uint8_t)fB;
+        }
+        return;
+    }
+    const uint32_t w = blockIdx.x * 4 + wv;
+    if (w >= T.nwords) return;
+    if (w == 0) {                                             // the total (resolve, fetch)
+        uint64_t a = 0;
+        for (uint32_t k = (uint32_t)lane; k < T.ncoarse; k += 64) a += T.coarse[k * COARSE_STRIDE];
+        const uint64_t total = readlane64(wave_sum64(a), 0);
+        if (lane == 0) {
+            T.super_off[T.nwords] = total;
+            T.ctr[CTR_CANDS_LO] = (uint32_t)total;
+            T.ctr[CTR_CANDS_HI] = (uint32_t)(total >> 32);
+            if (total > T.cand_cap) T.ctr[CTR_FLAGS] |= FLAG_CAND_OVERFLOW;
+        }
+    }
+    const uint64_t pre = word_prefix(T, w, lane);
+    if (lane == 0) T.super_off[w] = pre;
+    const unsigned long long bits = T.nonempty[w];
+    if (!bits) return;
+    const uint32_t tile = w * 64 + (uint32_t)lane;
+    const bool has = (bits >> lane) & 1ull;
+    uint32_t meta = 0, c = 0, tm = 0;
+    if (has) c = tile_cands(T, tile, meta, tm);              // (dense_off: a dense tile counts 0; fetch re-runs)
+    if (meta & DENSE_BIT) c = 0u;
+    const uint32_t incl = wave_incl_scan(c, lane);
+    const uint32_t ctot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t b0 = incl - c;                             // this tile's first word-relative index
+    const uint64_t wbase = (uint64_t)w * 64u * T.tile;
+    const uint32_t trel = (uint32_t)lane * T.tile;           // this tile's offset in the word
+    const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
+    const uint32_t ss = (uint32_t)LISTCAP / T.st_parts;
+    for (uint32_t k0 = 0; k0 < ctot; k0 += 128) {
+        // stage positions k0 .. k0 + 127 of the word's ordered candidates
+        if (c && b0 < k0 + 128 && b0 + c > k0) {
+            if (!tm) {
+                for (uint32_t j = 0; j < c; ++j) {
+                    const uint32_t i = b0 + j;
+                    if (i >= k0 && i < k0 + 128) lpos[wv][i - k0] = trel + sl[j].x;
+                }
+            } else {                                          // a split ST's tile: merge its parts
+                for (uint32_t p = 0; p < T.st_parts; ++p) {
+                    const uint32_t np = tail_part_count(tm, p);
+                    for (uint32_t j = 0; j < np; ++j) {
+                        const uint32_t e = sl[p * ss + j].x;
+                        uint32_t rank = j;
+                        for (uint32_t q = 0; q < T.st_parts; ++q) {
+                            if (q == p) continue;
+                            const uint32_t nq = tail_part_count(tm, q);
+                            for (uint32_t m = 0; m < nq; ++m) rank += sl[q * ss + m].x < e;
+                        }
+                        const uint32_t i = b0 + rank;
+                        if (i >= k0 && i < k0 + 128) lpos[wv][i - k0] = trel + e;
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        uint64_t a[2] = {0, 0};
+        uint32_t n[2] = {0, 0};
+        bool in[2] = {false, false};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t i = k0 + 2u * (uint32_t)lane + (uint32_t)h;
+            if (i < ctot) {
+                in[h] = true;
+                a[h] = wbase + lpos[wv][2 * lane + h] + 1;      // a candidate e: the chunk starts at e + 1
+                n[h] = (uint32_t)min<uint64_t>(63ull, T.span > a[h] ? T.span - a[h] : 0ull);
+            }
+        }
+        uint32_t fA = 0u, fB = 0u;
+        if (__ballot(in[0])) {
+            uint32_t A[16], B[16];
+            fix_load(data, T.span, a[0], n[0], A);
+            fix_load(data, T.span, a[1], n[1], B);
+            fix_pair(A, B, n[0], n[1], P, fA, fB);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint64_t o = pre + k0 + 2u * (uint32_t)lane + (uint32_t)h;
+            if (in[h] && o < T.cand_cap) T.cand[o] = (a[h] - 1) | ((uint64_t)(h ? fB : fA) << 48) | CAND_KNOWN;
+        }
+        __builtin_amdgcn_wave_barrier();                       // (the staging is reused)
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Resolve: one lane per file walks compute_file_chunks' loop over the sorted
 // candidate array.
@@ -3891,6 +4013,12 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
     // + up to 2048 blocks (one wave per dense tile) that expand dense tiles; they
     // exit at once when there are none.  (256 blocks left ~33 serial tile
     // expansions per wave on the dense workload: 0.2 ms.)
+    if (t.dense_off && !t.linkw && !dense_inline) {
+        // no dense pass, no chain links: compaction and fix-ups in one launch
+        const uint32_t gblocks = std::min<uint32_t>((t.ngrid + 511) / 512, 1024u);
+        hipLaunchKernelGGL(cdc_gather_fix_kernel, dim3((t.nwords + 3) / 4 + gblocks), dim3(256), 0, s, d, p, t);
+        return hipGetLastError();
+    }
     const uint32_t dgb = t.dense_off ? 0u : std::min<uint32_t>((t.dense_cap + 3) / 4, 2048u);
     hipLaunchKernelGGL(cdc_gather_kernel, dim3((t.nwords + 3) / 4 + dgb), dim3(256), 0, s, t);
     const uint64_t want = (t.cand_cap + t.ngrid + 511) / 512;       // two items per thread

@@ -11,7 +11,7 @@
 #   smoke                               __graft_entry__.smoke()
 #   bench[|<extra bench.py flags>]      the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 #   ab|<workload>|<rounds>|<V1>|<V2>... tools/dip_ab.py variants (dev library) in the driver's condition
-#   trace|<workload>[|<shard>]          kernel trace of one small-batch leg (tools/legs_trace.py, product)
+#   trace|<workload>[|<shard>[|--no-events]]  kernel trace of one small-batch leg (tools/legs_trace.py, product)
 #   sttrace|<workload>|<ENV=V,...>      per-wave stream-tile scan timeline (tools/scan_timeline.py, dev)
 #   prof|<PROFTAG>[|<extra flags>]      tools/prof.sh: trace + traffic + SQ passes of the driver's command
 #   build                               python -m syncr_amd.build (+ --dev) on the box (normally built here)
@@ -70,7 +70,7 @@ PY
         mkdir -p "$P"
         SH=${a[2]:-0}
         ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$P" -o run -- \
-            python3 "$R/tools/legs_trace.py" --workload "${a[1]}" --shard "$SH" > "$P/leg.json" 2> "$P/leg.err" ) \
+            python3 "$R/tools/legs_trace.py" --workload "${a[1]}" --shard "$SH" ${a[3]} > "$P/leg.json" 2> "$P/leg.err" ) \
             || { echo "trace failed rc=$?"; tail -20 "$P/leg.err"; exit 16; }
         f=$(find "$P" -name '*kernel_trace.csv' | head -1)
         nb=$(python3 -c "import json;print(json.loads(open('$P/leg.json').read().strip().splitlines()[-1])['bytes'])")

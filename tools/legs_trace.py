@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--shard", type=int, default=0)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-events", action="store_true",
+                    help="time the K steps with no HIP events at all (what the events cost a small step)")
     args = ap.parse_args()
     sizes = WL.zipf_sizes()
     if args.workload == "uniform1k":
@@ -44,7 +46,21 @@ def main():
         try:
             b.gen_corpus(offs, lens, indices=idx)
             ch.plan(offs, lens, span)
-            r = L.time_steps(ch, b.ptr, span, args.steps, args.warmup)
+            if args.no_events:
+                import time
+                ch.launch(b.ptr)
+                ch.fetch()
+                for _ in range(args.warmup - 1):
+                    ch.launch(b.ptr)
+                ch.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    ch.launch(b.ptr)
+                ch.synchronize()
+                dt = (time.perf_counter() - t0) / args.steps
+                r = {"ms_per_step": round(dt * 1e3, 4), "value": round(span / dt / 2**30, 3), "events": False}
+            else:
+                r = L.time_steps(ch, b.ptr, span, args.steps, args.warmup)
         finally:
             b.free()
     r.update({"workload": args.workload, "shard": args.shard, "bytes": span, "files": int(lens.size),
