@@ -464,7 +464,11 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
 #ifdef SYNCR_CDC_DEV
     if (t.dbg) CHECK_HIP(hipMemsetAsync(t.dbg, 0, DBG_WORDS * sizeof(uint64_t), s));
 #endif
-    if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[0], s));
+    // the scan's two events are bound to its own dispatch (hipExtLaunchKernel): they
+    // time the kernel itself and add no marker packets to the queue (two markers cost
+    // a small batch's step ~18 us of idle GPU: profiles/r05c_*_trace_shard8)
+    const bool bound = h->timing && t.ntiles;
+    if (h->timing && !bound) CHECK_HIP(hipEventRecord(pt.ev[0], s));
     {
         const int kind = scan_kind(h->geom, h->scan_grid, kp, t);
         const uint64_t waves = std::min<uint64_t>(h->scan_grid, t.ntiles);
@@ -481,16 +485,17 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
             t.tail_tile0 = t.st_full * ST_TILES;
         }
     }
-    CHECK_HIP(launch_scan(h->geom, h->scan_grid, d_bytes, kp, t, s));
-    if (h->timing) CHECK_HIP(hipEventRecord(pt.ev[1], s));
+    CHECK_HIP(launch_scan(h->geom, h->scan_grid, d_bytes, kp, t, s, bound ? pt.ev[0] : nullptr,
+                          bound ? pt.ev[1] : nullptr));
+    if (h->timing && !bound) CHECK_HIP(hipEventRecord(pt.ev[1], s));
     if (order) {
         std::lock_guard<std::mutex> g(so.mu);
         CHECK_HIP(hipEventRecord(h->scan_done, s));
         so.owner = h;
         so.ev = h->scan_done;
     }
-    // an event record costs ~6 us of queue idle: the scan-only mode records
-    // just the two around the scan
+    // an event record costs ~6 us of queue idle: the scan-only mode has only the
+    // two bound to the scan dispatch (no markers); the phase mode adds markers
     const bool phases = h->timing && !h->timing_scan_only;
     CHECK_HIP(launch_post(d_bytes, kp, t, s, scan_dense_inline(h->geom, kp)));
     h->last_dense_off = t.dense_off != 0u;

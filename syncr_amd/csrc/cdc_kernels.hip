@@ -17,6 +17,8 @@
 #include <mutex>
 #include <set>
 
+#include <hip/hip_ext.h>
+
 #include "../../include/syncr_cdc.h"
 #include "cdc_internal.h"
 #include "lds_dma.h"
@@ -3762,7 +3764,7 @@ constexpr int SCAN_CU_WAVES = 8;
 // a lock: multi-device ingest opens and launches handles from several threads.
 template <int RUN, int MODE>
 static hipError_t launch_scan_cu(uint32_t wave_grid, const uint8_t *d, const KParams &p, const Tables &t,
-                                 hipStream_t s) {
+                                 hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const size_t lds = (size_t)SCAN_CU_WAVES * lds_wave_bytes(RUN) + 16 + 8 * CU_NSLOT;
     const void *f = (const void *)&cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>;
     {
@@ -3779,7 +3781,7 @@ static hipError_t launch_scan_cu(uint32_t wave_grid, const uint8_t *d, const KPa
         }
     }
     uint32_t grid = (wave_grid + SCAN_CU_WAVES - 1) / SCAN_CU_WAVES;
-    hipLaunchKernelGGL((cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>), dim3(grid), dim3(64 * SCAN_CU_WAVES), lds, s,
+    hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>), dim3(grid), dim3(64 * SCAN_CU_WAVES), lds, s, e0, e1, 0u,
                        d, p, t);
     return hipGetLastError();
 }
@@ -3831,90 +3833,90 @@ static const void *scan_kernel_ptr(ScanGeom g) {
 }
 
 template <int RUN>
-static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
+static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const size_t lds = lds_wave_bytes(RUN);
     if (p.ablate == 1u)                                              // timing only: staging, no roll
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 1>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, 1>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 2u)                                         // timing only: roll, no DMA
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, 2>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 3u)                                         // timing only: staging, nt
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 5>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, 5>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 4u)                                         // A/B: static stride always (exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 8u)                                         // A/B: dynamic groups always (exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 5u)                                         // A/B: round-1 roll (two dependent mads, exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 11u)                                        // A/B: dense tiles passed by the scan wave
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 128>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 128>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 6u)                                         // timing only: roll, no DMA
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 17u)                                        // A/B: stream-tile scan (exact)
-        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 15u) {                                      // A/B: CU schedule (exact)
-        (void)launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s);
+        (void)launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s, e0, e1);
     } else if (p.ablate == 16u) {                                    // timing only: CU schedule, no warm-up/halo
-        (void)launch_scan_cu<RUN, 4 | 16 | 256 | 512>(grid, d, p, t, s);
+        (void)launch_scan_cu<RUN, 4 | 16 | 256 | 512>(grid, d, p, t, s, e0, e1);
     }
     else if (p.ablate == 12u)                                        // timing only: no closed-form warm-up
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 13u)                                        // timing only: no warm-up, no halo bytes
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256 | 512>), dim3(grid), dim3(64), lds, s, d,
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256 | 512>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d,
                            p, t);
     else if (p.ablate == 7u)                                         // A/B: product + 3 waves per SIMD hint
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, d, p,
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p,
                            t);
     else if (p.nt && p.scan_tiles && scan_dynamic(t.ntiles, grid))   // product, dense-heavy data: tiles
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.nt && !p.scan_tiles && scan_stream_tiles(t.ntiles, grid) && RUN == DEFAULT_RUN)   // product: stream tiles
-        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, e0, e1, 0u, d, p, t);
     else if (p.nt && scan_dynamic(t.ntiles, grid))                   // other geometries: nt + dynamic groups + ROLL2
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.nt)                                                   // product, small batch: CU schedule
-        (void)launch_scan_cu<RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);
+        (void)launch_scan_cu<RUN, SCAN_STATIC_MODE>(grid, d, p, t, s, e0, e1);
     else
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE & ~4>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE & ~4>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
 }
 
-static void launch_scan3(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
+static void launch_scan3(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const size_t lds = lds3_wave_bytes(W3_RUN);
     if (p.ablate == 6u)                                              // timing only: roll, no DMA
-        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8 | 2>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8 | 2>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (scan_dynamic(t.ntiles, grid))
-        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else
-        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
 }
 
 template <int NB, int V>
-static void launch_mfma_v(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
+static void launch_mfma_v(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     constexpr int VM = ((V & MFV_SINGLE) ? 8 : 0) | ((V & MFV_NOPIPE) ? 16 : 0);
     const size_t lds = mf_lds_bytes(NB, (V & MFV_SINGLE) ? 1 : 2);
     const bool low16 = p.bits >= 16;
     if (p.ablate == 1u || p.ablate == 3u)
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 5, true>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 5, true>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.ablate == 2u)
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 2, true>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 2, true>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (low16 && p.nt)
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, true>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, true>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (low16)
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, true>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, true>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else if (p.nt)
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, false>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, false>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
     else
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, false>), dim3(grid), dim3(64), lds, s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, false>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
 }
 
 template <int NB>
 static void launch_mfma_t(int var, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
-                          hipStream_t s) {
+                          hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     switch (var & 3) {
-        case 0: launch_mfma_v<NB, 0>(grid, d, p, t, s); break;
-        case 1: launch_mfma_v<NB, 1>(grid, d, p, t, s); break;
-        case 2: launch_mfma_v<NB, 2>(grid, d, p, t, s); break;
-        default: launch_mfma_v<NB, 3>(grid, d, p, t, s); break;
+        case 0: launch_mfma_v<NB, 0>(grid, d, p, t, s, e0, e1); break;
+        case 1: launch_mfma_v<NB, 1>(grid, d, p, t, s, e0, e1); break;
+        case 2: launch_mfma_v<NB, 2>(grid, d, p, t, s, e0, e1); break;
+        default: launch_mfma_v<NB, 3>(grid, d, p, t, s, e0, e1); break;
     }
 }
 
@@ -3923,27 +3925,27 @@ bool scan_dense_inline(ScanGeom g, const KParams &p) {
 }
 
 hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
-                       hipStream_t s) {
+                       hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (!t.ntiles) return hipSuccess;
     grid = grid < t.ntiles ? grid : t.ntiles;
     if (g.kind == SCAN_MFMA) {
         switch (g.param) {
-            case 4: launch_mfma_t<4>(g.var, grid, d, p, t, s); break;
-            case 6: launch_mfma_t<6>(g.var, grid, d, p, t, s); break;
-            case 8: launch_mfma_t<8>(g.var, grid, d, p, t, s); break;
-            case 10: launch_mfma_t<10>(g.var, grid, d, p, t, s); break;
-            case 12: launch_mfma_t<12>(g.var, grid, d, p, t, s); break;
+            case 4: launch_mfma_t<4>(g.var, grid, d, p, t, s, e0, e1); break;
+            case 6: launch_mfma_t<6>(g.var, grid, d, p, t, s, e0, e1); break;
+            case 8: launch_mfma_t<8>(g.var, grid, d, p, t, s, e0, e1); break;
+            case 10: launch_mfma_t<10>(g.var, grid, d, p, t, s, e0, e1); break;
+            case 12: launch_mfma_t<12>(g.var, grid, d, p, t, s, e0, e1); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
     }
     switch (g.param) {
-        case 48: launch_scan_t<48>(grid, d, p, t, s); break;
-        case 80: launch_scan_t<80>(grid, d, p, t, s); break;
-        case W3_RUN: launch_scan3(grid, d, p, t, s); break;
-        case 112: launch_scan_t<112>(grid, d, p, t, s); break;
-        case 144: launch_scan_t<144>(grid, d, p, t, s); break;
-        case 176: launch_scan_t<176>(grid, d, p, t, s); break;
+        case 48: launch_scan_t<48>(grid, d, p, t, s, e0, e1); break;
+        case 80: launch_scan_t<80>(grid, d, p, t, s, e0, e1); break;
+        case W3_RUN: launch_scan3(grid, d, p, t, s, e0, e1); break;
+        case 112: launch_scan_t<112>(grid, d, p, t, s, e0, e1); break;
+        case 144: launch_scan_t<144>(grid, d, p, t, s, e0, e1); break;
+        case 176: launch_scan_t<176>(grid, d, p, t, s, e0, e1); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -3956,18 +3958,18 @@ static const void *scan_kernel_ptr(ScanGeom) { return (const void *)&cdc_scan_ke
 bool scan_dense_inline(ScanGeom, const KParams &) { return false; }
 
 hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
-                       hipStream_t s) {
+                       hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (!t.ntiles) return hipSuccess;
     if (!scan_supported(g)) return hipErrorInvalidValue;
     const int kind = scan_kind(g, grid, p, t);
     grid = grid < t.ntiles ? grid : t.ntiles;
     if (kind == SYNCR_CDC_SCAN_TILES)             // the handle's last batch was dense-heavy: tiles
-        hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
-                           lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
+                           lds_wave_bytes(DEFAULT_RUN), s, e0, e1, 0u, d, p, t);
     else if (kind == SYNCR_CDC_SCAN_STREAM_TILES) // >= 3 stream tiles per wave (§4.6)
-        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
+        hipExtLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, e0, e1, 0u, d, p, t);
     else                                          // small batch: the CU schedule (per-wave static shares end
-        return launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);   // with the slow waves alone)
+        return launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s, e0, e1);   // with the slow waves alone)
     return hipGetLastError();
 }
 #endif
