@@ -323,6 +323,8 @@ def run_legs(args, dev_id: int, dbuf, offs, lens, idx, rank_span: int, out: dict
         out["dedup"] = timed("dedup", L.dedup_leg, dev_id, k, w)
     if args.workload != "dense":
         out["dense"] = timed("dense", L.dense_leg, dev_id, k, w)
+    if args.workload != "dense1":
+        out["dense1"] = timed("dense1", L.dense1_leg, dev_id, k, w)
     out["h2d_probe"] = timed("h2d_probe", L.h2d_probe, dev_id)
     if host is not None:
         out["ingest"] = timed("ingest", L.ingest_leg, host, offs, lens, idx, dev_id)
@@ -337,8 +339,10 @@ def run_legs(args, dev_id: int, dbuf, offs, lens, idx, rank_span: int, out: dict
     # one summary: every parity check of the line
     checks = []
     for name, p in list(parity.items()) + [(f"{s}.parity", out.get(s, {}).get("parity")) for s in
-                                            ("shard8", "uniform1k", "dedup", "dense", "ingest", "ingest_files")] + \
-            [(f"{s}.parity_hashed", out.get(s, {}).get("parity_hashed")) for s in ("dedup", "dense")]:
+                                            ("shard8", "uniform1k", "dedup", "dense", "dense1", "ingest",
+                                             "ingest_files", "ingest_zero_copy")] + \
+            [(f"{s}.parity_hashed", out.get(s, {}).get("parity_hashed")) for s in ("dedup", "dense", "dense1")] + \
+            [("dense1.parity_ideal", out.get("dense1", {}).get("parity_ideal"))]:
         if isinstance(p, dict) and "mismatches" in p:
             checks.append((name, p.get("files", p.get("cases", 0)), p["mismatches"] + p.get("hash_mismatches", 0)))
         elif isinstance(p, dict):

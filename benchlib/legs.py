@@ -402,6 +402,44 @@ def dense_leg(device: int, steps: int, warmup: int) -> dict:
     return out
 
 
+def dense1_leg(device: int, steps: int, warmup: int) -> dict:
+    """The adversarial single file: one DENSE1_BYTES (128 MiB) file of the
+    64-byte period that hits every 64 bytes (the shape of the reference's
+    constant-data tests, tests/chunking_test.rs:95-108 and
+    tests/protocol_list_test.rs:360-378, with an edge in every period): 2 M
+    chained cuts, dense tiles everywhere, split resolve walks.  Timed like the
+    other legs (boundaries; then with BLAKE3); parity of its cuts (both
+    semantics) and hashes against tests/golden/dense1_digests.npz."""
+    import syncr_amd
+    span = WL.DENSE1_BYTES
+    lens, offs, idx = np.array([span], np.uint64), np.zeros(1, np.uint64), np.zeros(1, np.uint64)
+    data = np.resize(WL.periodic_pattern(), span)
+    with syncr_amd.Chunker(device=device) as ch, syncr_amd.Chunker(read_cap=0, device=device) as chi:
+        b = syncr_amd.DeviceBuffer(ch, span)
+        try:
+            b.upload(data)
+            ch.plan(offs, lens, span)
+            out = time_steps(ch, b.ptr, span, steps, warmup)
+            cuts = ch.fetch()
+            out["split"] = ch.split_stats()
+            out["dense_tiles"] = int(ch.last_stats()["dense_tiles"])
+            hashed = time_steps(ch, b.ptr, span, max(steps // 2, 3), 2, hashed=True)
+            hcuts = ch.fetch(hashed=True)
+            chi.plan(offs, lens, span)
+            chi.launch(b.ptr)
+            icuts = chi.fetch()
+        finally:
+            b.free()
+    out.update({"config": f"adversarial single file: {span} bytes of the periodic-64 pattern",
+                "chunks": int(cuts[0].size),
+                "step_frac": round(span / (out["ms_per_step"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "hashed": {k: hashed[k] for k in ("value", "ms_per_step", "hash_ms")},
+                "parity": G.check_files("dense1", cuts, idx),
+                "parity_ideal": G.check_files("dense1", icuts, idx, semantics="ideal"),
+                "parity_hashed": G.check_files("dense1", hcuts, idx, hashed=True)})
+    return out
+
+
 def ideal_leg(dbuf, offs, lens, idx, device: int) -> dict:
     """Ideal semantics (chunk_data, tests/chunking_test.rs:170-192: read_cap 0)
     on the headline corpus already in HBM, every file against the golden ideal

@@ -127,6 +127,7 @@ def dedup_shift(entry) -> int:
     return ln if kind == "insert" else (-min(ln, DEDUP_BASE - pos) if kind == "delete" else 0)
 
 
+DENSE1_BYTES = 128 * M                 # the adversarial single file (bench --workload dense1, the dense1 leg)
 WORKLOADS = ("zipf10k", "uniform1k", "uniform2k", "uniform4k", "dense", "big1", "dense1", "dedup")
 
 
@@ -147,7 +148,7 @@ def workload(name: str, world: int, scaling: str = "strong"):
         one = np.full(1, 128 * M, np.uint64)
         desc = "diagnostic: one 128 MiB file (the longest resolve walk of zipf10k)"
     elif name == "dense1":
-        one = np.full(1, 128 * M, np.uint64)
+        one = np.full(1, DENSE1_BYTES, np.uint64)
         desc = "diagnostic: one 128 MiB periodic-64 file (2 M chained cuts: the dense workload's longest walk)"
     elif name == "dedup":
         one = np.array([p[4] for p in dedup_plan()], np.uint64)

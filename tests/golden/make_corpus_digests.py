@@ -17,7 +17,7 @@ running the oracle over 10-32 GiB there.  Fixture contents (npz, no pickles):
   ends_fnv = FNV-1a-64 over the cut END offsets (SURVEY App. A);
   hash_fnv = FNV-1a-64 over the chunk hashes read as 4 little-endian u64 each.
 
-    python tests/golden/make_corpus_digests.py [zipf10k] [dense] [dedup]
+    python tests/golden/make_corpus_digests.py [zipf10k] [dense] [dense1] [dedup]
 """
 from __future__ import annotations
 
@@ -111,6 +111,16 @@ def make_dense():
          "literal loop (orc_chunk_production_window, checked against the literal loop in tests/test_oracle.py)")
 
 
+def make_dense1():
+    n = WL.DENSE1_BYTES
+    buf = np.resize(WL.periodic_pattern(), n)
+    lens = np.array([n], np.uint64)
+    save("dense1", digests(buf, np.zeros(1, np.uint64), lens, linear_prod=np.ones(1, bool)),
+         "dense1 (adversarial single file, tests/chunking_test.rs:95-108 / tests/protocol_list_test.rs:360-378 "
+         "shape): one DENSE1_BYTES file of periodic_pattern() repeated (an edge every 64 bytes: dense tiles, "
+         "millions of chained cuts, split walks); production cuts by orc_chunk_production_window")
+
+
 def make_dedup():
     plan = WL.dedup_plan()
     base, _ = O.corpus_fill_threads(np.array([WL.DEDUP_BASE], np.uint64), np.array([WL.DEDUP_BASE_INDEX], np.uint64))
@@ -131,6 +141,6 @@ def make_dedup():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["zipf10k", "dense", "dedup"]
+    which = sys.argv[1:] or ["zipf10k", "dense", "dense1", "dedup"]
     for w in which:
-        {"zipf10k": make_zipf10k, "dense": make_dense, "dedup": make_dedup}[w]()
+        {"zipf10k": make_zipf10k, "dense": make_dense, "dense1": make_dense1, "dedup": make_dedup}[w]()
