@@ -330,8 +330,9 @@ def run_legs(args, dev_id: int, dbuf, offs, lens, idx, rank_span: int, out: dict
         out["ingest"] = timed("ingest", L.ingest_leg, host, offs, lens, idx, dev_id)
         parity["ingest_multi_device"] = out["ingest"].get("multi_device", {}).get("parity")
         out["ingest_files"] = timed("ingest_files", L.ingest_files_leg, host, offs, lens, idx, dev_id)
+        out["ingest_zero_copy"] = timed("ingest_zero_copy", L.ingest_zero_copy_leg, host, offs, lens, idx, dev_id)
         h2d = out["h2d_probe"].get("h2d", {}).get("best_gbs")
-        for key in ("ingest", "ingest_files"):
+        for key in ("ingest", "ingest_files", "ingest_zero_copy"):
             v = out[key].get("value")
             if h2d and v:          # the end-to-end rate on its link ceiling (GiB/s -> GB/s)
                 out[key]["frac_of_h2d"] = round(v * 2**30 / 1e9 / h2d, 4)

@@ -210,7 +210,9 @@ int32_t syncr_ingest_open_multi(const int32_t *devices, uint32_t ndevices, const
                                 syncr_ingest_cb cb, void *ctx, syncr_ingest **out);
 /* bytes already in memory (copied into the staging batch before returning) */
 int32_t syncr_ingest_submit(syncr_ingest *g, const uint8_t *data, uint64_t len, uint64_t tag);
-/* a file read with pread straight into pinned staging */
+/* a file read with pread straight into pinned staging: opened and sized on the
+ * calling thread, read by the copy_threads pool while the caller goes on (the
+ * batch waits for its reads when it is sealed) */
 int32_t syncr_ingest_submit_file(syncr_ingest *g, const char *path, uint64_t tag);
 /* zero-copy: reserve `len` bytes of pinned staging, fill them, then commit */
 int32_t syncr_ingest_reserve(syncr_ingest *g, uint64_t len, uint8_t **dst);
@@ -223,7 +225,9 @@ int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4);
  * SYNCR_CDC_ERANGE if n < 4 * ndevices */
 int32_t syncr_ingest_device_stats(const syncr_ingest *g, uint64_t *stats, uint32_t n);
 /* Host seconds spent so far, summed over sub-pipelines, per stage: sec[0] copying
- * submitted bytes into pinned staging, [1] reading files into it (submit_file),
+ * submitted bytes into pinned staging, [1] waiting for (and helping with) the
+ * reads of a batch's files before its H2D (submit_file queues each file's preads
+ * on the copy_threads pool, 2 MiB per task, and returns),
  * [2] sealing batches (plan + H2D and kernel enqueue), [3] waiting for a batch's
  * results (fetch: the device side -- H2D, kernels, D2H -- not yet done), [4]
  * per-file delivery (callbacks).  Diagnostics of where an end-to-end run is

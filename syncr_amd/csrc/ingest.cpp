@@ -62,6 +62,32 @@ class Pool {
         cv_.notify_all();
         for (auto &t : th_) t.join();
     }
+    // Queue fn to run on a pool thread (inline when the pool has none).  Posted
+    // tasks must not wait on anything the caller holds.
+    void post(std::function<void()> fn) {
+        if (th_.empty()) {
+            fn();
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            tasks_.push_back(std::move(fn));
+        }
+        cv_.notify_one();
+    }
+    // Run one posted task on the calling thread, if any is queued (a caller that
+    // waits for its tasks helps instead of idling).
+    bool run_one() {
+        std::function<void()> f;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (tasks_.empty()) return false;
+            f = std::move(tasks_.front());
+            tasks_.pop_front();
+        }
+        f();
+        return true;
+    }
     // run fn(0..n-1) on the pool plus the calling thread; returns when all done.
     // Callers on several threads (sub-pipelines sharing the pool) take turns.
     void parallel(unsigned n, const std::function<void(unsigned)> &fn) {
@@ -103,13 +129,22 @@ class Pool {
     void run() {
         uint64_t seen = 0;
         for (;;) {
+            std::function<void()> task;
             {
                 std::unique_lock<std::mutex> g(mu_);
-                cv_.wait(g, [&] { return stop_ || (gen_ != seen && fn_ && next_ < total_); });
-                if (stop_) return;
-                seen = gen_;
+                cv_.wait(g, [&] { return stop_ || (gen_ != seen && fn_ && next_ < total_) || !tasks_.empty(); });
+                if (stop_ && tasks_.empty()) return;
+                if (gen_ != seen && fn_ && next_ < total_) {
+                    seen = gen_;
+                } else if (!tasks_.empty()) {
+                    task = std::move(tasks_.front());
+                    tasks_.pop_front();
+                } else {
+                    continue;
+                }
             }
-            work();
+            if (task) task();
+            else work();
         }
     }
     std::vector<std::thread> th_;
@@ -117,9 +152,28 @@ class Pool {
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     const std::function<void(unsigned)> *fn_ = nullptr;
+    std::deque<std::function<void()>> tasks_;  // posted (asynchronous) tasks
     unsigned next_ = 0, total_ = 0, done_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
+};
+
+// One file read by the pool into a slot's staging, PIECE bytes per task.  Per
+// piece: bytes read from its start and the errno that stopped it (0 = EOF: the
+// file shrank under us).  In a deque: its address is stable while later files
+// are queued.
+struct PendingRead {
+    int fd = -1;
+    uint8_t *dst = nullptr;
+    uint64_t len = 0;
+    size_t entry = 0;                 // the file's index in the slot
+    std::string path;                 // chunk cache key (when a cache is attached)
+    uint32_t mtime = 0;
+    uint64_t fault_off = UINT64_MAX;  // syncr_ingest_set_read_fault
+    int fault_err = 0;
+    std::vector<uint64_t> got;
+    std::vector<int> perr;
+    uint32_t left = 0;                // pieces of this file not yet read (guarded by Pipe::rmu)
 };
 
 struct Slot {
@@ -141,6 +195,11 @@ struct Slot {
     bool inflight = false;
     std::vector<syncr_chunk_info> out;
     std::vector<uint64_t> counts;
+    // files whose bytes the pool is reading into this slot (submit_file): their
+    // entries above are provisional until seal() has waited for the reads
+    std::deque<PendingRead> reads;
+    uint32_t pending = 0;             // pieces not yet read (guarded by Pipe::rmu)
+    uint32_t small_uses = 0;          // batch-sized batches since the slot was grown (shrink_slot)
 };
 
 constexpr uint64_t PAR_COPY = 4ull << 20;   // copies above this are split over the pool
@@ -173,6 +232,9 @@ struct Pipe {
     // pinned staging, file reads into it, seal (plan + H2D and kernel enqueue),
     // waiting for a batch's results (fetch), per-file delivery
     std::atomic<uint64_t> tns[5] = {{0}, {0}, {0}, {0}, {0}};
+    // completion of the pool's file reads (Slot::pending)
+    std::mutex rmu;
+    std::condition_variable rcv;
 };
 
 enum { T_COPY = 0, T_READ = 1, T_SEAL = 2, T_WAIT = 3, T_DELIVER = 4 };
@@ -251,11 +313,17 @@ int32_t ensure_slot(Pipe *g, Slot &s, uint64_t bytes) {
     return SYNCR_CDC_OK;
 }
 
-// A slot grown for one oversized file goes back to batch size once that
-// file's batch is delivered, so the pipeline's pinned and device memory stays
-// depth x batch_bytes between oversized files.
-void shrink_slot(Pipe *g, Slot &s) {
+// A slot grown for an oversized file goes back to batch size after SHRINK_AFTER
+// batch-sized batches have been delivered from it, so the pipeline's pinned and
+// device memory returns to depth x batch_bytes between runs of oversized files.
+// (Shrinking right after each oversized file made a stream of them pay a
+// device-synchronising free and a fresh pin per file: ADVICE r4.)
+constexpr uint32_t SHRINK_AFTER = 4;
+void shrink_slot(Pipe *g, Slot &s, bool oversized) {
     if (s.cap <= std::max<uint64_t>(g->batch, 64) || s.inflight || s.used) return;
+    s.small_uses = oversized ? 0u : s.small_uses + 1u;
+    if (s.small_uses < SHRINK_AFTER) return;
+    s.small_uses = 0;
     uint8_t *dev = nullptr, *host = nullptr;
     free_slot_buffers(g, s);
     if (alloc_slot(g, std::max<uint64_t>(g->batch, 64), &dev, &host) == SYNCR_CDC_OK) {
@@ -340,12 +408,55 @@ int32_t complete(Pipe *g, Slot &s) {
     s.cstart.clear();
     s.ccount.clear();
     s.cbuf.clear();
+    const bool oversized = s.used > g->batch;
     s.used = 0;
-    shrink_slot(g, s);
+    shrink_slot(g, s, oversized);
     return SYNCR_CDC_OK;
 }
 
+// Wait for the pool's reads into slot s, then turn each file's provisional
+// entry into its final one: the prefix read without a gap (the reference reads
+// sequentially and stops at the first failure or EOF), its status, and its
+// chunk-cache key when it was read whole.
+void finish_reads(Pipe *g, Slot &s) {
+    if (s.reads.empty()) return;
+    {
+        StageTimer tr(g->tns[T_READ]);
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> l(g->rmu);
+                if (!s.pending) break;
+            }
+            if (g->pool && g->pool->run_one()) continue;          // help with queued reads
+            std::unique_lock<std::mutex> l(g->rmu);
+            g->rcv.wait_for(l, std::chrono::microseconds(200), [&] { return s.pending == 0; });
+        }
+    }
+    for (PendingRead &pr : s.reads) {
+        uint64_t P = 0;
+        int err = 0;
+        for (size_t i = 0; i < pr.got.size(); i++) {
+            P += pr.got[i];
+            const uint64_t want = std::min<uint64_t>(pr.len, (uint64_t)(i + 1) * PIECE) - (uint64_t)i * PIECE;
+            if (pr.got[i] < want) { err = pr.perr[i]; break; }
+        }
+        const size_t e = pr.entry;
+        s.len[e] = P;
+        if (err) {                                   // file_operations.rs:738-743 (P = 0) / :776-782
+            s.status[e] = -err;
+            s.trunc[e] = P > 0 ? 1 : 0;
+        } else if (g->cache && P == pr.len) {        // complete (or shrank to P bytes: EOF, not cached)
+            s.key[e] = pr.path;
+            s.mtime[e] = pr.mtime;
+            s.fsize[e] = pr.len;
+        }
+        g->stats[1] += P;
+    }
+    s.reads.clear();
+}
+
 int32_t seal(Pipe *g, Slot &s) {
+    finish_reads(g, s);
     if (s.off.empty()) return SYNCR_CDC_OK;
     StageTimer ts(g->tns[T_SEAL]);
     int32_t rc = syncr_cdc_plan(s.h, s.off.data(), s.len.data(), (uint32_t)s.off.size(), s.used);
@@ -396,6 +507,7 @@ void record(Slot &s, uint64_t len, uint64_t tag, int32_t status, bool trunc = fa
 
 void pipe_close(Pipe *g) {
     if (!g) return;
+    for (Slot &s : g->slots) finish_reads(g, s);     // no read may outlive the buffers
     for (Slot &s : g->slots) {
         if (s.h) {
             (void)syncr_cdc_synchronize(s.h);
@@ -472,6 +584,26 @@ int32_t pipe_submit(Pipe *g, const uint8_t *data, uint64_t len, uint64_t tag) {
     return pipe_commit(g, tag);
 }
 
+// Piece i of a file (bytes [i * PIECE, +PIECE) of it): pread until done, EOF
+// (the file shrank) or an error; with an injected fault (the test hook), bytes
+// at and past the fault offset are never read and the read that would cross it
+// fails with fault_err (0: EOF there).
+void read_piece(PendingRead &pr, unsigned i) {
+    const uint64_t a = (uint64_t)i * PIECE, b = std::min<uint64_t>(pr.len, a + PIECE);
+    const uint64_t e = std::min(b, std::max(a, pr.fault_off));
+    uint64_t pos = a;
+    const uint64_t stop = e < b ? e : b;
+    while (pos < stop) {
+        const ssize_t r = pread(pr.fd, pr.dst + pos, (size_t)(stop - pos), (off_t)pos);
+        if (r < 0 && errno == EINTR) continue;
+        if (r < 0) { pr.perr[i] = errno ? errno : EIO; break; }    // a real error (before any fault)
+        if (r == 0) break;                                         // EOF before st_size / the fault
+        pos += (uint64_t)r;
+    }
+    if (e < b && pos == e) pr.perr[i] = pr.fault_err;
+    pr.got[i] = pos - a;
+}
+
 int32_t pipe_submit_file(Pipe *g, const char *path, uint64_t tag) {
     if (g->reserved) return SYNCR_CDC_ESTATE;
     if (g->error) return g->error;
@@ -519,63 +651,44 @@ int32_t pipe_submit_file(Pipe *g, const char *path, uint64_t tag) {
         close(fd);
         return rc;
     }
-    // pread straight into pinned memory, split over the pool for big files.
-    // Per piece: bytes read from its start, and the errno that stopped it (0 =
-    // EOF: the file shrank under us).
-    const unsigned pieces = len ? (unsigned)((len + PIECE - 1) / PIECE) : 0u;
-    std::vector<uint64_t> got(pieces, 0);
-    std::vector<int> perr(pieces, 0);
-    const uint64_t fault_off = g->fault_off.load();
-    const int fault_err = g->fault_err.load();
-    auto read_piece = [&](unsigned i) {
-        const uint64_t a = (uint64_t)i * PIECE, b = std::min<uint64_t>(len, a + PIECE);
-        const uint64_t e = std::min(b, std::max(a, fault_off));    // injected fault (test hook)
-        uint64_t pos = a;
-        if (e < b) {
-            // bytes at and after the fault offset are never read
-            while (pos < e) {
-                const ssize_t r = pread(fd, dst + pos, (size_t)(e - pos), (off_t)pos);
-                if (r < 0 && errno == EINTR) continue;
-                if (r < 0) { perr[i] = errno ? errno : EIO; break; }   // a real error before the fault
-                if (r == 0) break;                                     // EOF before the fault
-                pos += (uint64_t)r;
-            }
-            if (pos == e) perr[i] = fault_err;
-            got[i] = pos - a;
-            return;
-        }
-        while (pos < b) {
-            const ssize_t r = pread(fd, dst + pos, (size_t)(b - pos), (off_t)pos);
-            if (r < 0 && errno == EINTR) continue;
-            if (r < 0) { perr[i] = errno ? errno : EIO; break; }
-            if (r == 0) break;                                   // EOF before st_size
-            pos += (uint64_t)r;
-        }
-        got[i] = pos - a;
-    };
-    {
-        StageTimer tr(g->tns[T_READ]);
-        if (len > PAR_COPY && g->pool) g->pool->parallel(pieces, read_piece);
-        else for (unsigned i = 0; i < pieces; i++) read_piece(i);
-    }
-    close(fd);
-    // the prefix read without a gap: the reference reads sequentially and
-    // stops at the first failure or EOF
-    uint64_t P = 0;
-    int err = 0;
-    for (unsigned i = 0; i < pieces; i++) {
-        P += got[i];
-        const uint64_t want = std::min<uint64_t>(len, (uint64_t)(i + 1) * PIECE) - (uint64_t)i * PIECE;
-        if (got[i] < want) { err = perr[i]; break; }
-    }
     g->reserved = false;
-    if (err) {                                       // file_operations.rs:738-743 (P = 0) / :776-782
-        record(g->slots[g->cur], P, tag, -err, P > 0);
-    } else {                                         // complete, or shrank to P bytes (EOF)
-        record(g->slots[g->cur], P, tag, 0, false, g->cache && P == len ? path : nullptr, mt, len);
-    }
-    g->stats[1] += P;
+    Slot &s = g->slots[g->cur];
+    record(s, len, tag, 0);                          // provisional: finish_reads() sets length and status
     g->stats[0]++;
+    if (!len) {
+        close(fd);
+        return SYNCR_CDC_OK;
+    }
+    // pread straight into pinned memory on the pool, PIECE bytes per task: the
+    // caller goes on to the next file (many small files are read in parallel),
+    // and seal() waits for the slot's reads before the batch's H2D
+    PendingRead &pr = s.reads.emplace_back();
+    pr.fd = fd;
+    pr.dst = dst;
+    pr.len = len;
+    pr.entry = s.off.size() - 1;
+    if (g->cache) pr.path = path;
+    pr.mtime = mt;
+    pr.fault_off = g->fault_off.load();
+    pr.fault_err = g->fault_err.load();
+    const unsigned pieces = (unsigned)((len + PIECE - 1) / PIECE);
+    pr.got.assign(pieces, 0);
+    pr.perr.assign(pieces, 0);
+    {
+        std::lock_guard<std::mutex> l(g->rmu);
+        pr.left = pieces;
+        s.pending += pieces;
+    }
+    for (unsigned i = 0; i < pieces; i++) {
+        auto task = [g, &s, &pr, i] {
+            read_piece(pr, i);
+            std::lock_guard<std::mutex> l(g->rmu);            // (pr may be gone once pending drops)
+            if (--pr.left == 0) close(pr.fd);
+            if (--s.pending == 0) g->rcv.notify_all();
+        };
+        if (g->pool) g->pool->post(task);
+        else task();
+    }
     return SYNCR_CDC_OK;
 }
 
