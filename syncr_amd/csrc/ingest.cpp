@@ -653,12 +653,13 @@ int32_t pipe_submit_file(Pipe *g, const char *path, uint64_t tag) {
     }
     g->reserved = false;
     Slot &s = g->slots[g->cur];
-    record(s, len, tag, 0);                          // provisional: finish_reads() sets length and status
     g->stats[0]++;
-    if (!len) {
+    if (!len) {                                      // nothing to read: final now (and cacheable)
         close(fd);
+        record(s, 0, tag, 0, false, g->cache ? path : nullptr, mt, 0);
         return SYNCR_CDC_OK;
     }
+    record(s, len, tag, 0);                          // provisional: finish_reads() sets length and status
     // pread straight into pinned memory on the pool, PIECE bytes per task: the
     // caller goes on to the next file (many small files are read in parallel),
     // and seal() waits for the slot's reads before the batch's H2D
