@@ -473,7 +473,9 @@ def main(argv=None):
             ch.fetch(hashed=head_hashed)
         d.barrier()
         ch.synchronize()
-        ch.set_timing(True, scan_only=True)       # HIP events around the scan kernel, on its stream
+        # the scan kernel timed by the device clock inside the kernel (no event packets in the
+        # queue: the timed steps run exactly as untimed ones); HIP events cross-check below
+        ch.set_timing(True, scan_only=True)
         t0 = time.perf_counter()
         run_steps(1, args.steps)                  # the timed region: one batch in flight
         dt = time.perf_counter() - t0
@@ -501,6 +503,12 @@ def main(argv=None):
     ch.set_timing(True)
     run_steps(1, min(args.steps, 5))
     pms, pn = ch.kernel_times()
+    ch.set_timing(False)
+    # cross-check of the device-clock scan time: the same K steps with HIP events bound to the
+    # scan's dispatch on its launch stream (each event pair adds queue idle to a step)
+    ch.set_timing(True, scan_only=True, events=True)
+    run_steps(1, args.steps)
+    ems, en = ch.kernel_times()
     ch.set_timing(False)
 
     dt_max = d.reduce(dt, "max")
@@ -572,6 +580,11 @@ def main(argv=None):
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": (int(tr["hbm_bytes_per_launch"]) if tr else None),
         "kernel": scan_kernel, "kernel_ms": round(scan_ms, 4), "scan_schedule": scan_info,
+        "kernel_timing": "mean over the K timed launches by the device clock (the scan's waves stamp "
+                         "wall_clock64 at entry / exit, syncr_cdc_set_timing mode 2: no queue packets); "
+                         "kernel_ms_hip_events: the same K steps right after, HIP events bound to the scan "
+                         "dispatch on its stream",
+        "kernel_ms_hip_events": round(ems[0] / max(en, 1), 4) if en else None,
         "algorithmic_bytes_per_launch": span,
         "dense_ms": round(pms[1] / max(pn, 1), 4), "resolve_ms": round(pms[2] / max(pn, 1), 4),
         "hash_ms": round(pms[3] / max(pn, 1), 4) if head_hashed else None,

@@ -29,8 +29,8 @@ def _tests_path():
 def time_steps(ch, ptr: int, span: int, steps: int, warmup: int, hashed: bool = False) -> dict:
     """K one-in-flight steps after W warm-up steps (results fetched after the
     first), wall clock bracketed by device synchronisation; the scan kernel's
-    mean time from HIP events on its stream; then a few steps with every phase
-    bracketed by events (outside the timed steps)."""
+    mean time by the device clock (no queue packets in the timed steps); then a
+    few steps with every phase bracketed by events (outside the timed steps)."""
     ch.launch(ptr, hashed=hashed)
     ch.fetch(hashed=hashed)
     for _ in range(max(warmup - 1, 0)):

@@ -301,11 +301,17 @@ int32_t syncr_cdc_gen_corpus(syncr_cdc *h, uint8_t *d_bytes, const uint64_t *fil
  * the handle's stream after one warm-up.  ms2 = [best, mean] ms per pass. */
 int32_t syncr_cdc_read_probe(syncr_cdc *h, const uint8_t *d_bytes, uint64_t bytes, uint32_t reps,
                              int32_t nt, double *ms2);
-/* Per-kernel timing: enable = 1 brackets every phase of each launch with HIP
- * events on the launch stream (kernel_times: summed ms of [scan, dense +
- * compaction, resolve] since the last reset, and the number of launches);
- * enable = 2 records only the two events around the scan kernel (each event
- * costs a few microseconds of queue idle); 0 disables. */
+/* Per-kernel timing (kernel_times: summed ms of [scan, dense + compaction,
+ * resolve] since the last set_timing, and the number of launches):
+ *   enable = 1  every phase of each launch bracketed by HIP events on the launch stream;
+ *   enable = 2  the scan kernel only, by the device's own clock: its first waves
+ *               stamp their entry, every wave its exit (wall_clock64, the constant
+ *               clock HIP events read), the launch's resolve adds last exit - first
+ *               entry to device-side sums -- no packets in the queue, so the timed
+ *               launches run exactly as untimed ones (an event pair costs a 1 GiB
+ *               batch ~6 % of its step in queue idle);
+ *   enable = 3  the scan kernel only, by HIP events bound to its dispatch;
+ *   enable = 0  off. */
 int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable);
 int32_t syncr_cdc_kernel_times(syncr_cdc *h, double *ms3, uint64_t *launches);
 /* The same for up to 4 phases: [scan, dense+compaction, resolve, hash]. */

@@ -329,9 +329,11 @@ class Chunker:
         _check(fn(self._h, out.ctypes.data, out.size, counts.ctypes.data, ctypes.byref(n)), "syncr_cdc_fetch")
         return _split(out[: int(n.value)], counts[:nf])
 
-    def set_timing(self, on: bool, scan_only: bool = False) -> None:
-        """HIP events around each launch's kernels; scan_only: only around the scan."""
-        mode = (2 if scan_only else 1) if on else 0
+    def set_timing(self, on: bool, scan_only: bool = False, events: bool = False) -> None:
+        """Per-kernel timing (syncr_cdc_set_timing): HIP events around each launch's
+        phases; scan_only: the scan kernel alone, by the device clock (no queue
+        packets), or with events=True by HIP events bound to its dispatch."""
+        mode = ((3 if events else 2) if scan_only else 1) if on else 0
         _check(library().syncr_cdc_set_timing(self._h, mode), "syncr_cdc_set_timing")
 
     def kernel_times(self) -> tuple[list[float], int]:

@@ -130,7 +130,10 @@ struct syncr_cdc {
 
     // timing
     bool timing = false;
-    bool timing_scan_only = false;            // set_timing(h, 2): events around the scan only
+    bool timing_scan_only = false;            // set_timing(h, 2 or 3): the scan only
+    bool timing_clock = false;                // set_timing(h, 2): by the device clock (no events)
+    DevBuf tacc;                              // [sum of scan ticks, launches] (timing_clock)
+    uint64_t wall_khz = 100000;               // the device clock's rate
     std::vector<PendingTiming> pending;
     double ms[NPHASE] = {0, 0, 0, 0};
     uint64_t timed_launches = 0;
@@ -205,7 +208,8 @@ size_t sched_offset(const syncr_cdc *h) { return (split_ctr_offset(h) + SPL_WORD
 uint32_t nst_of(const syncr_cdc *h) { return (h->ntiles + ST_TILES - 1) / ST_TILES; }
 size_t tail_offset(const syncr_cdc *h) { return sched_offset(h) + (size_t)SCHED_REGIONS * COARSE_STRIDE * 4; }
 size_t tail_tiles_cap(const syncr_cdc *h) { return (size_t)std::min<uint32_t>(h->scan_grid, nst_of(h)) * ST_TILES; }
-size_t zeroed_bytes(const syncr_cdc *h) { return tail_offset(h) + tail_tiles_cap(h) * 4; }
+size_t tscan_offset(const syncr_cdc *h) { return (tail_offset(h) + tail_tiles_cap(h) * 4 + 127) & ~size_t(127); }
+size_t zeroed_bytes(const syncr_cdc *h) { return tscan_offset(h) + 128; }
 size_t zstride(const syncr_cdc *h) { return (zeroed_bytes(h) + 255) & ~size_t(255); }
 uint8_t *zblock(const syncr_cdc *h, uint32_t par) { return h->zeroed.as<uint8_t>() + par * zstride(h); }
 
@@ -266,6 +270,8 @@ Tables make_tables(syncr_cdc *h) {
     t.st_tail = 0;
     t.st_parts = 1;
     t.tail_tile0 = h->ntiles;
+    t.tscan = reinterpret_cast<uint64_t *>(zb + tscan_offset(h));
+    t.tacc = (h->timing && h->timing_clock) ? h->tacc.as<uint64_t>() : nullptr;
     t.znext = reinterpret_cast<uint4 *>(zblock(h, h->zpar ^ 1u));
     t.znext_vec = (uint32_t)(zstride(h) / 16);
     t.hzero = nullptr;
@@ -433,7 +439,7 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     Tables t = make_tables(h);
     PendingTiming pt{};
     pt.nev = h->timing_scan_only ? 2 : h->hash_on ? 5 : 4;
-    if (h->timing) {
+    if (h->timing && !h->timing_clock) {
         if (h->pending.size() >= 256) drain_timing(h);
         // timing only: no system-scope release (a cache writeback + invalidate per
         // event would stall the queue and perturb the kernels being timed)
@@ -467,8 +473,9 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     // the scan's two events are bound to its own dispatch (hipExtLaunchKernel): they
     // time the kernel itself and add no marker packets to the queue (two markers cost
     // a small batch's step ~18 us of idle GPU: profiles/r05c_*_trace_shard8)
-    const bool bound = h->timing && t.ntiles;
-    if (h->timing && !bound) CHECK_HIP(hipEventRecord(pt.ev[0], s));
+    const bool events = h->timing && !h->timing_clock;
+    const bool bound = events && t.ntiles;
+    if (events && !bound) CHECK_HIP(hipEventRecord(pt.ev[0], s));
     {
         const int kind = scan_kind(h->geom, h->scan_grid, kp, t);
         const uint64_t waves = std::min<uint64_t>(h->scan_grid, t.ntiles);
@@ -487,7 +494,7 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     }
     CHECK_HIP(launch_scan(h->geom, h->scan_grid, d_bytes, kp, t, s, bound ? pt.ev[0] : nullptr,
                           bound ? pt.ev[1] : nullptr));
-    if (h->timing && !bound) CHECK_HIP(hipEventRecord(pt.ev[1], s));
+    if (events && !bound) CHECK_HIP(hipEventRecord(pt.ev[1], s));
     if (order) {
         std::lock_guard<std::mutex> g(so.mu);
         CHECK_HIP(hipEventRecord(h->scan_done, s));
@@ -496,7 +503,7 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     }
     // an event record costs ~6 us of queue idle: the scan-only mode has only the
     // two bound to the scan dispatch (no markers); the phase mode adds markers
-    const bool phases = h->timing && !h->timing_scan_only;
+    const bool phases = events && !h->timing_scan_only;
     CHECK_HIP(launch_post(d_bytes, kp, t, s, scan_dense_inline(h->geom, kp)));
     h->last_dense_off = t.dense_off != 0u;
     if (phases) CHECK_HIP(hipEventRecord(pt.ev[2], s));
@@ -510,7 +517,7 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
         CHECK_HIP(launch_hash(h->device, d_bytes, t, make_hash_tables(h), s));
         if (phases) CHECK_HIP(hipEventRecord(pt.ev[4], s));
     }
-    if (h->timing) h->pending.push_back(pt);
+    if (events) h->pending.push_back(pt);
     h->launched = true;
     h->last_bytes = d_bytes;
     h->last_stream = s;
@@ -576,6 +583,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
             khz = 100000;
         h->kp.split_patience = (prm.flags & SYNCR_CDC_FLAG_SPLIT_NOWAIT) ? 0ull : 100ull * (uint64_t)khz;
+        h->wall_khz = (uint64_t)khz;
     }
     h->kp.dense_fuse = 1u;                      // dense pass computes its candidates' head fix-ups
 #ifdef SYNCR_CDC_DEV
@@ -1169,20 +1177,41 @@ int32_t syncr_cdc_read_probe(syncr_cdc *h, const uint8_t *d_bytes, uint64_t byte
 }
 
 int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable) {
-    if (!h) return SYNCR_CDC_EINVAL;
-    (void)hipSetDevice(h->device);
+    if (!h || enable < 0 || enable > 3) return SYNCR_CDC_EINVAL;
+    CHECK_HIP(hipSetDevice(h->device));
     drain_timing(h);
+    if (enable == 2) {
+        CHECK_HIP(h->tacc.ensure(16));
+        CHECK_HIP(hipDeviceSynchronize());            // no earlier launch may still add to the sums
+        CHECK_HIP(hipMemset(h->tacc.p, 0, 16));
+    }
     h->timing = enable != 0;
-    h->timing_scan_only = enable == 2;
+    h->timing_scan_only = enable == 2 || enable == 3;
+    h->timing_clock = enable == 2;
     for (double &m : h->ms) m = 0;
     h->timed_launches = 0;
     return SYNCR_CDC_OK;
 }
 
+namespace {
+// the device-clock sums into ms[0] / timed_launches (timing mode 2)
+int32_t read_clock_times(syncr_cdc *h) {
+    if (!h->timing_clock || !h->tacc.p) return SYNCR_CDC_OK;
+    CHECK_HIP(hipDeviceSynchronize());
+    uint64_t v[2] = {0, 0};
+    CHECK_HIP(hipMemcpy(v, h->tacc.p, 16, hipMemcpyDeviceToHost));
+    h->ms[0] = (double)v[0] / (double)h->wall_khz;
+    h->timed_launches = v[1];
+    return SYNCR_CDC_OK;
+}
+}  // namespace
+
 int32_t syncr_cdc_kernel_times(syncr_cdc *h, double *ms3, uint64_t *launches) {
     if (!h) return SYNCR_CDC_EINVAL;
     (void)hipSetDevice(h->device);
     drain_timing(h);
+    int32_t rc = read_clock_times(h);
+    if (rc) return rc;
     if (ms3) for (int k = 0; k < 3; k++) ms3[k] = h->ms[k];
     if (launches) *launches = h->timed_launches;
     return SYNCR_CDC_OK;
@@ -1192,6 +1221,8 @@ int32_t syncr_cdc_kernel_times_ex(syncr_cdc *h, double *ms, uint32_t n, uint64_t
     if (!h || (n && !ms)) return SYNCR_CDC_EINVAL;
     (void)hipSetDevice(h->device);
     drain_timing(h);
+    int32_t rc = read_clock_times(h);
+    if (rc) return rc;
     for (uint32_t k = 0; k < n; k++) ms[k] = k < (uint32_t)NPHASE ? h->ms[k] : 0.0;
     if (launches) *launches = h->timed_launches;
     return SYNCR_CDC_OK;

@@ -278,6 +278,12 @@ struct Tables {
     uint32_t st_parts;
     uint32_t tail_tile0;           // first tile of the split STs (st_full * ST_TILES)
     uint32_t *tail_meta;           // [st_tail * ST_TILES] per-part counts | TAIL_DENSE (zeroed per launch)
+    // scan timing by the device clock (syncr_cdc_set_timing mode 2; null: off): the scan's
+    // waves stamp wall_clock64 -- tscan[0] = ~0 - the earliest entry, tscan[1] = the
+    // latest exit (atomic max, zeroed per launch) -- and the resolve adds exit - entry
+    // to tacc[0] and 1 to tacc[1] (the handle's running sums).  No queue packets.
+    uint64_t *tscan;
+    uint64_t *tacc;
 };
 // dev timeline slots: resolve entry (min over waves), end (max); the largest
 // split file's walker: entry, after split setup, adoption blocks (start, end),

@@ -108,6 +108,31 @@ __device__ __forceinline__ uint64_t sload_u64(const void *p) {
 #define SCAN_STAMP(T, slot, v) do { } while (0)
 #endif
 
+// Device-clock scan timing (Tables::tscan / tacc): the first blocks dispatched stamp
+// the entry (a launch's blocks start within ~1 us of each other), every wave
+// that worked stamps its exit; non-returning atomics, nothing waits on them.
+__device__ __forceinline__ void scan_time_entry(const Tables &T) {
+    if (T.tacc && blockIdx.x < 8u && threadIdx.x == 0)
+        __hip_atomic_fetch_max(&T.tscan[0], ~0ull - wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void scan_time_exit(const Tables &T, int lane) {
+    if (T.tacc && lane == 0)
+        __hip_atomic_fetch_max(&T.tscan[1], (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// (the resolve, after the scan on the same stream) the launch's scan time into the sums
+__device__ __forceinline__ void scan_time_account(const Tables &T) {
+    if (T.tacc && blockIdx.x == 0 && threadIdx.x == 0) {
+        const uint64_t t0 = __hip_atomic_load(&T.tscan[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t e = __hip_atomic_load(&T.tscan[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t b = ~0ull - t0;
+        if (t0 && e > b) {
+            T.tacc[0] += e - b;
+            T.tacc[1] += 1;
+        }
+    }
+}
+
 __device__ __forceinline__ void record(uint32_t *wcount, uint32_t *wlist, uint32_t rel) {
     const uint32_t idx = atomicAdd(wcount, 1u);
     if (idx < (uint32_t)LISTCAP) wlist[idx] = rel;
@@ -527,6 +552,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     const int lane = threadIdx.x & 63;
     const uint32_t wid = CUS ? (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
     uint8_t *wl = smem + wid * (uint32_t)lds_wave_bytes(RUN);
+    scan_time_entry(T);
     // CU schedule state after the waves' regions: the local tile counter, then
     // the group ring (u64: local group index << 32 | global group id + 1)
     typedef __attribute__((address_space(3))) uint32_t lds_u32;
@@ -756,6 +782,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             pf_store();
         }
     }
+    scan_time_exit(T, lane);
 #ifdef SYNCR_CDC_DEV
     if (stamp) {
         // where the wave ran: HW_ID (wave, SIMD, CU, SH, SE) and the XCC id
@@ -944,6 +971,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             HB[4 * m] = vb.x; HB[4 * m + 1] = vb.y; HB[4 * m + 2] = vb.z; HB[4 * m + 3] = vb.w;
         }
     };
+    scan_time_entry(T);
     if (blockIdx.x >= nunits) return;
     StUnit un = st_unit(T, blockIdx.x);
     uint32_t st = un.st;
@@ -1139,6 +1167,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             }
             if (!more) {
                 dense_pend_flush(T, dslots_alloc, lane);
+                scan_time_exit(T, lane);
 #ifdef SYNCR_CDC_DEV
                 if (stamp) {
                     uint32_t hwid, xcc;
@@ -2489,6 +2518,7 @@ __device__ __forceinline__ void zero_next(const Tables &T) {
 
 __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restrict__ data, KParams P,
                                                          Tables T) {
+    scan_time_account(T);
     zero_next(T);
     const uint32_t kf = blockIdx.x * 64 + threadIdx.x;
     if (kf >= T.nfiles) return;
@@ -3618,6 +3648,7 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
     __shared__ uint64_t rings[4 * PF * 64];                     // each wave's candidate-window ring
     const uint64_t *ring = rings + (threadIdx.x >> 6) * (PF * 64);
     if (blockIdx.x == 0 && threadIdx.x < 64) DBG_STAMP(T, DBG_RES_START);   // (one wave: no contention)
+    scan_time_account(T);
     zero_next(T);
     if (blockIdx.x == 0 && threadIdx.x < 64) DBG_STAMP(T, 6);
     const uint32_t nmain = (T.nfiles + 3u) / 4u, nwork = gridDim.x - nmain;

@@ -328,12 +328,21 @@ def test_kernel_timing_api(chunkers):
         ms, n = ch.kernel_times()
         ch.set_timing(False)
         assert n == 3 and ms[0] > 0 and ms[2] > 0
-        ch.set_timing(True, scan_only=True)          # two events per launch, around the scan
+        ch.set_timing(True, scan_only=True)          # the scan by the device clock (no events)
         for _ in range(2):
             ch.launch(buf.ptr)
         ms2, n2 = ch.kernel_times()
         ch.set_timing(False)
         assert n2 == 2 and ms2[0] > 0 and ms2[1] == ms2[2] == ms2[3] == 0
+        ch.set_timing(True, scan_only=True, events=True)   # the scan by HIP events on its dispatch
+        for _ in range(2):
+            ch.launch(buf.ptr)
+        ms3, n3 = ch.kernel_times()
+        ch.set_timing(False)
+        assert n3 == 2 and ms3[0] > 0 and ms3[1] == ms3[2] == ms3[3] == 0
+        # the two clocks agree on the same kernel (the events include the dispatch's own
+        # start-up and end-of-kernel flush: a few microseconds of a ~10 us+ scan)
+        assert 0.5 * ms3[0] <= ms2[0] <= 1.2 * ms3[0], (ms2[0], ms3[0])
         ch.fetch()
         st = ch.last_stats()
         assert st["tiles"] >= data_len // (144 * 128) and st["flags"] == 0
