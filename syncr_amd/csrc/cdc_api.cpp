@@ -603,6 +603,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_CDC_SPLIT_FIRST")) h->kp.split_first = (uint32_t)atoi(a) != 0; // A/B only
     if (const char *a = getenv("SYNCR_CDC_NOSKIP")) h->kp.no_skip = atoi(a) != 0;                    // A/B only
     if (const char *a = getenv("SYNCR_CDC_DENSE_FUSE")) h->kp.dense_fuse = atoi(a) != 0;           // A/B only
+    if (const char *a = getenv("SYNCR_CDC_ST_PRIO")) h->kp.st_prio = atoi(a) != 0;               // A/B only
     if (const char *a = getenv("SYNCR_CDC_ST_PARTS"))                                         // A/B only
         h->kp.st_parts = (uint32_t)std::min(std::max(atoi(a), 1), (int)ST_MAX_PARTS);
     if (const char *a = getenv("SYNCR_CDC_TRACE"))                                              // timeline

@@ -138,6 +138,8 @@ struct KParams {
                                //   SYNCR_CDC_DENSE_FUSE=0)
     uint32_t resolve_pf;       // development library only (SYNCR_CDC_RESOLVE_PF): candidate windows
                                //   the resolve walk loads ahead (0: RESOLVE_PF)
+    uint32_t st_prio;          // (dev A/B: SYNCR_CDC_ST_PRIO) a wave in the batch's last round of stream-tile
+                               //   units raises its issue priority the later it took its unit
     uint32_t st_parts;         // stream-tile scan: the batch's last round of STs is handed out in this many
                                //   parts each (segment ranges; 1 = whole STs; ST_MAX_PARTS at most)
 };

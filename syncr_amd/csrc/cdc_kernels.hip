@@ -1184,6 +1184,14 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         un = nun;
         st = un.st;
         ++nth;
+        if (P.st_prio && nextu + gridDim.x >= nunits) {
+            // the last round: the later a wave took its unit, the more of it is left when
+            // the others finish -- it gets the SIMD's issue slots first (dev A/B)
+            const uint32_t r = (nextu + gridDim.x - nunits) * 3u / gridDim.x;   // 0 .. 2
+            if (r >= 2u) __builtin_amdgcn_s_setprio(3);
+            else if (r == 1u) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(1);
+        }
 #ifdef SYNCR_CDC_DEV
         ++nst_done;
 #endif
