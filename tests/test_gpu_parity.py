@@ -340,9 +340,9 @@ def test_kernel_timing_api(chunkers):
         ms3, n3 = ch.kernel_times()
         ch.set_timing(False)
         assert n3 == 2 and ms3[0] > 0 and ms3[1] == ms3[2] == ms3[3] == 0
-        # the two clocks agree on the same kernel (the events include the dispatch's own
-        # start-up and end-of-kernel flush: a few microseconds of a ~10 us+ scan)
-        assert 0.5 * ms3[0] <= ms2[0] <= 1.2 * ms3[0], (ms2[0], ms3[0])
+        # the two measure the same kernel: the same order of magnitude (on a 64 MiB batch the
+        # scan is ~20-40 us and its dispatch start-up is part of both)
+        assert 0.5 * ms3[0] <= ms2[0] <= 2.0 * ms3[0], (ms2[0], ms3[0])
         ch.fetch()
         st = ch.last_stats()
         assert st["tiles"] >= data_len // (144 * 128) and st["flags"] == 0
