@@ -470,11 +470,11 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
 #ifdef SYNCR_CDC_DEV
     if (t.dbg) CHECK_HIP(hipMemsetAsync(t.dbg, 0, DBG_WORDS * sizeof(uint64_t), s));
 #endif
-    // the scan's two events are bound to its own dispatch (hipExtLaunchKernel): they
-    // time the kernel itself and add no marker packets to the queue (two markers cost
-    // a small batch's step ~18 us of idle GPU: profiles/r05c_*_trace_shard8)
+    // HIP events (timing modes 1 and 3) are marker packets around the kernels: each
+    // costs queue idle (an event pair ~18 us of a 1 GiB batch's ~0.3 ms step,
+    // profiles/r05c_*_trace_shard8); mode 2 times the scan by the device clock instead
     const bool events = h->timing && !h->timing_clock;
-    const bool bound = events && t.ntiles;
+    const bool bound = events && t.ntiles;           // the pair around the scan: launch_scan records it
     if (events && !bound) CHECK_HIP(hipEventRecord(pt.ev[0], s));
     {
         const int kind = scan_kind(h->geom, h->scan_grid, kp, t);

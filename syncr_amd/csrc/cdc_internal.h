@@ -350,8 +350,7 @@ bool scan_supported(ScanGeom g);
 int scan_tile_bytes(ScanGeom g);
 int scan_lds_bytes(ScanGeom g);
 int scan_blocks_per_cu(ScanGeom g);
-// e0 / e1 (may be null): HIP events bound to the scan kernel's own dispatch (hipExtLaunchKernel:
-// its start and end, no marker packets in the queue)
+// e0 / e1 (may be null): HIP events recorded on s right before and after the scan kernel
 hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d_bytes, const KParams &p, const Tables &t,
                        hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 bool scan_dense_inline(ScanGeom g, const KParams &p);      // the scan passes dense tiles itself

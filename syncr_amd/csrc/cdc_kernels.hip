@@ -17,7 +17,6 @@
 #include <mutex>
 #include <set>
 
-#include <hip/hip_ext.h>
 
 #include "../../include/syncr_cdc.h"
 #include "cdc_internal.h"
@@ -3803,7 +3802,7 @@ constexpr int SCAN_CU_WAVES = 8;
 // a lock: multi-device ingest opens and launches handles from several threads.
 template <int RUN, int MODE>
 static hipError_t launch_scan_cu(uint32_t wave_grid, const uint8_t *d, const KParams &p, const Tables &t,
-                                 hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+                                 hipStream_t s) {
     const size_t lds = (size_t)SCAN_CU_WAVES * lds_wave_bytes(RUN) + 16 + 8 * CU_NSLOT;
     const void *f = (const void *)&cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>;
     {
@@ -3820,7 +3819,7 @@ static hipError_t launch_scan_cu(uint32_t wave_grid, const uint8_t *d, const KPa
         }
     }
     uint32_t grid = (wave_grid + SCAN_CU_WAVES - 1) / SCAN_CU_WAVES;
-    hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>), dim3(grid), dim3(64 * SCAN_CU_WAVES), lds, s, e0, e1, 0u,
+    hipLaunchKernelGGL((cdc_scan_kernel<RUN, MODE, SCAN_CU_WAVES>), dim3(grid), dim3(64 * SCAN_CU_WAVES), lds, s,
                        d, p, t);
     return hipGetLastError();
 }
@@ -3872,90 +3871,90 @@ static const void *scan_kernel_ptr(ScanGeom g) {
 }
 
 template <int RUN>
-static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
     const size_t lds = lds_wave_bytes(RUN);
     if (p.ablate == 1u)                                              // timing only: staging, no roll
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, 1>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 1>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 2u)                                         // timing only: roll, no DMA
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, 2>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 3u)                                         // timing only: staging, nt
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, 5>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 5>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 4u)                                         // A/B: static stride always (exact)
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 8u)                                         // A/B: dynamic groups always (exact)
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 5u)                                         // A/B: round-1 roll (two dependent mads, exact)
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 11u)                                        // A/B: dense tiles passed by the scan wave
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 128>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 128>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 6u)                                         // timing only: roll, no DMA
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 17u)                                        // A/B: stream-tile scan (exact)
-        hipExtLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else if (p.ablate == 15u) {                                      // A/B: CU schedule (exact)
-        (void)launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s, e0, e1);
+        (void)launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s);
     } else if (p.ablate == 16u) {                                    // timing only: CU schedule, no warm-up/halo
-        (void)launch_scan_cu<RUN, 4 | 16 | 256 | 512>(grid, d, p, t, s, e0, e1);
+        (void)launch_scan_cu<RUN, 4 | 16 | 256 | 512>(grid, d, p, t, s);
     }
     else if (p.ablate == 12u)                                        // timing only: no closed-form warm-up
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 13u)                                        // timing only: no warm-up, no halo bytes
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256 | 512>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d,
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256 | 512>), dim3(grid), dim3(64), lds, s, d,
                            p, t);
     else if (p.ablate == 7u)                                         // A/B: product + 3 waves per SIMD hint
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p,
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, d, p,
                            t);
     else if (p.nt && p.scan_tiles && scan_dynamic(t.ntiles, grid))   // product, dense-heavy data: tiles
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.nt && !p.scan_tiles && scan_stream_tiles(t.ntiles, grid) && RUN == DEFAULT_RUN)   // product: stream tiles
-        hipExtLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else if (p.nt && scan_dynamic(t.ntiles, grid))                   // other geometries: nt + dynamic groups + ROLL2
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.nt)                                                   // product, small batch: CU schedule
-        (void)launch_scan_cu<RUN, SCAN_STATIC_MODE>(grid, d, p, t, s, e0, e1);
+        (void)launch_scan_cu<RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);
     else
-        hipExtLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE & ~4>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE & ~4>), dim3(grid), dim3(64), lds, s, d, p, t);
 }
 
-static void launch_scan3(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+static void launch_scan3(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
     const size_t lds = lds3_wave_bytes(W3_RUN);
     if (p.ablate == 6u)                                              // timing only: roll, no DMA
-        hipExtLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8 | 2>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8 | 2>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (scan_dynamic(t.ntiles, grid))
-        hipExtLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8>), dim3(grid), dim3(64), lds, s, d, p, t);
     else
-        hipExtLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4>), dim3(grid), dim3(64), lds, s, d, p, t);
 }
 
 template <int NB, int V>
-static void launch_mfma_v(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+static void launch_mfma_v(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
     constexpr int VM = ((V & MFV_SINGLE) ? 8 : 0) | ((V & MFV_NOPIPE) ? 16 : 0);
     const size_t lds = mf_lds_bytes(NB, (V & MFV_SINGLE) ? 1 : 2);
     const bool low16 = p.bits >= 16;
     if (p.ablate == 1u || p.ablate == 3u)
-        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 5, true>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 5, true>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 2u)
-        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 2, true>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 2, true>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (low16 && p.nt)
-        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, true>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, true>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (low16)
-        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, true>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, true>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.nt)
-        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, false>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, false>), dim3(grid), dim3(64), lds, s, d, p, t);
     else
-        hipExtLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, false>), dim3(grid), dim3(64), lds, s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, false>), dim3(grid), dim3(64), lds, s, d, p, t);
 }
 
 template <int NB>
 static void launch_mfma_t(int var, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
-                          hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+                          hipStream_t s) {
     switch (var & 3) {
-        case 0: launch_mfma_v<NB, 0>(grid, d, p, t, s, e0, e1); break;
-        case 1: launch_mfma_v<NB, 1>(grid, d, p, t, s, e0, e1); break;
-        case 2: launch_mfma_v<NB, 2>(grid, d, p, t, s, e0, e1); break;
-        default: launch_mfma_v<NB, 3>(grid, d, p, t, s, e0, e1); break;
+        case 0: launch_mfma_v<NB, 0>(grid, d, p, t, s); break;
+        case 1: launch_mfma_v<NB, 1>(grid, d, p, t, s); break;
+        case 2: launch_mfma_v<NB, 2>(grid, d, p, t, s); break;
+        default: launch_mfma_v<NB, 3>(grid, d, p, t, s); break;
     }
 }
 
@@ -3963,28 +3962,27 @@ bool scan_dense_inline(ScanGeom g, const KParams &p) {
     return g.kind == SCAN_VALU && g.param != W3_RUN && p.ablate == 11u;     // the mode-128 instance
 }
 
-hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
-                       hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    if (!t.ntiles) return hipSuccess;
+static hipError_t launch_scan_kernel(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
+                                     hipStream_t s) {
     grid = grid < t.ntiles ? grid : t.ntiles;
     if (g.kind == SCAN_MFMA) {
         switch (g.param) {
-            case 4: launch_mfma_t<4>(g.var, grid, d, p, t, s, e0, e1); break;
-            case 6: launch_mfma_t<6>(g.var, grid, d, p, t, s, e0, e1); break;
-            case 8: launch_mfma_t<8>(g.var, grid, d, p, t, s, e0, e1); break;
-            case 10: launch_mfma_t<10>(g.var, grid, d, p, t, s, e0, e1); break;
-            case 12: launch_mfma_t<12>(g.var, grid, d, p, t, s, e0, e1); break;
+            case 4: launch_mfma_t<4>(g.var, grid, d, p, t, s); break;
+            case 6: launch_mfma_t<6>(g.var, grid, d, p, t, s); break;
+            case 8: launch_mfma_t<8>(g.var, grid, d, p, t, s); break;
+            case 10: launch_mfma_t<10>(g.var, grid, d, p, t, s); break;
+            case 12: launch_mfma_t<12>(g.var, grid, d, p, t, s); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
     }
     switch (g.param) {
-        case 48: launch_scan_t<48>(grid, d, p, t, s, e0, e1); break;
-        case 80: launch_scan_t<80>(grid, d, p, t, s, e0, e1); break;
-        case W3_RUN: launch_scan3(grid, d, p, t, s, e0, e1); break;
-        case 112: launch_scan_t<112>(grid, d, p, t, s, e0, e1); break;
-        case 144: launch_scan_t<144>(grid, d, p, t, s, e0, e1); break;
-        case 176: launch_scan_t<176>(grid, d, p, t, s, e0, e1); break;
+        case 48: launch_scan_t<48>(grid, d, p, t, s); break;
+        case 80: launch_scan_t<80>(grid, d, p, t, s); break;
+        case W3_RUN: launch_scan3(grid, d, p, t, s); break;
+        case 112: launch_scan_t<112>(grid, d, p, t, s); break;
+        case 144: launch_scan_t<144>(grid, d, p, t, s); break;
+        case 176: launch_scan_t<176>(grid, d, p, t, s); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -3996,22 +3994,31 @@ int scan_lds_bytes(ScanGeom) { return lds_wave_bytes(DEFAULT_RUN); }
 static const void *scan_kernel_ptr(ScanGeom) { return (const void *)&cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>; }
 bool scan_dense_inline(ScanGeom, const KParams &) { return false; }
 
-hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
-                       hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    if (!t.ntiles) return hipSuccess;
+static hipError_t launch_scan_kernel(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
+                                     hipStream_t s) {
     if (!scan_supported(g)) return hipErrorInvalidValue;
     const int kind = scan_kind(g, grid, p, t);
     grid = grid < t.ntiles ? grid : t.ntiles;
     if (kind == SYNCR_CDC_SCAN_TILES)             // the handle's last batch was dense-heavy: tiles
-        hipExtLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
-                           lds_wave_bytes(DEFAULT_RUN), s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
+                           lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
     else if (kind == SYNCR_CDC_SCAN_STREAM_TILES) // >= 3 stream tiles per wave (§4.6)
-        hipExtLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, e0, e1, 0u, d, p, t);
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
     else                                          // small batch: the CU schedule (per-wave static shares end
-        return launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s, e0, e1);   // with the slow waves alone)
+        return launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);   // with the slow waves alone)
     return hipGetLastError();
 }
 #endif
+
+// The scan launch of do_launch; e0 / e1 (may be null): HIP events recorded around it.
+hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
+                       hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (!t.ntiles) return hipSuccess;
+    hipError_t e = e0 ? hipEventRecord(e0, s) : hipSuccess;
+    if (e == hipSuccess) e = launch_scan_kernel(g, grid, d, p, t, s);
+    if (e == hipSuccess && e1) e = hipEventRecord(e1, s);
+    return e;
+}
 
 // The product's choice between its three exact scans (the dev library's
 // variants, other geometries and ablations report SYNCR_CDC_SCAN_DEV).
