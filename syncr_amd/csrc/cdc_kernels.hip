@@ -977,7 +977,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     const bool stamp = blockIdx.x < (uint32_t)DBG_SCAN_N;              // timeline slot (dev)
     if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x, wall_clock64());
 #ifdef SYNCR_CDC_DEV
-    uint32_t nst_done = 0;
+    uint32_t nst_done = 0, seg_done = 0;
 #endif
     issue_seg(st, un.g0);
     load_halo(st, un.g0);
@@ -1000,6 +1000,10 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             wait_vmcnt<0>();                                         // segment g landed (and, at 0, the halo)
 #ifdef SYNCR_CDC_DEV
             if (stamp && first && nst_done == 0) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 1, wall_clock64());
+            // every segment landing of the first DBG_TILE_W waves (unit switches vs. steady segments)
+            if (blockIdx.x < (uint32_t)DBG_TILE_W && seg_done < (uint32_t)DBG_TILE_N)
+                SCAN_STAMP(T, DBG_TILE + DBG_TILE_N * blockIdx.x + seg_done, wall_clock64() | ((uint64_t)g << 56));
+            ++seg_done;
 #endif
             if (first) {                                             // warm-up from the halo (closed form)
                 uint32_t SA = 0, WA = 0, SB = 0, WB = 0;

@@ -66,12 +66,18 @@ def summarize(d, grid):
     t0 = sc[:, 0].min()
     us = lambda v: (v - t0) / 100.0                                  # noqa: E731
     ends = us(sc[:, 2])
-    tiles = d[DBG_TILE:DBG_TILE + DBG_TILE_W * DBG_TILE_N].reshape(DBG_TILE_W, DBG_TILE_N).astype(np.int64)
+    tiles = d[DBG_TILE:DBG_TILE + DBG_TILE_W * DBG_TILE_N].reshape(DBG_TILE_W, DBG_TILE_N).astype(np.uint64)
     per_tile = []
+    seg_by_g = {}                                   # stream-tile scan: landing-to-landing time by segment index
     for w in range(DBG_TILE_W):
-        t = tiles[w][tiles[w] > 0]
+        raw = tiles[w][tiles[w] > 0]
+        g = (raw >> np.uint64(56)).astype(np.int64)
+        t = (raw & np.uint64((1 << 56) - 1)).astype(np.int64)
         if t.size > 2:
-            per_tile.extend(np.diff(t).tolist())
+            dt = np.diff(t)
+            per_tile.extend(dt.tolist())
+            for k in range(1, t.size):
+                seg_by_g.setdefault(int(g[k]), []).append(float(dt[k - 1]) / 100.0)
     per_tile = np.array(per_tile, np.float64) / 100.0
     res = int(d[0])
     out = {
@@ -87,6 +93,10 @@ def summarize(d, grid):
                      "p90": round(float(np.percentile(per_tile, 90)), 3), "first": round(float(per_tile[0]), 3)}
                     if per_tile.size else None),
         "resolve_start_after_scan_us": round((res - sc[:, 2].max()) / 100.0, 2) if res else None,
+        # the time from the previous segment's landing to segment g's landing (g = 0: a new
+        # unit's first segment, after the last segment of the previous one)
+        "seg_landing_gap_us_by_g": {g: {"median": round(float(np.median(v)), 3), "n": len(v)}
+                                    for g, v in sorted(seg_by_g.items())},
     }
     # per-wave rate (tiles per us of the wave's life) by placement: which waves are slow?
     rate = sc[:, 3] / np.maximum((sc[:, 2] - sc[:, 0]) / 100.0, 1e-3)
