@@ -332,8 +332,9 @@ int32_t syncr_cdc_fetch_reruns(syncr_cdc *h, uint64_t *reruns);
 /* Which scan kernel the last launch ran (the library's own choice, made per
  * launch from the batch size and the handle's history; a capacity re-run inside
  * fetch counts as a launch).  kind: one of SYNCR_CDC_SCAN_*; info4 (may be NULL) =
- * [kind, tiles, scan waves launched, tiles per wave x 1000]; *name (may be NULL)
- * = the kernel's symbol name as a profiler shows it. */
+ * [kind, tiles, scan waves launched, segments per stream of a stream-tile scan
+ * (9 or 18; 0 for the other scans)]; *name (may be NULL) = the kernel's symbol
+ * name as a profiler shows it. */
 #define SYNCR_CDC_SCAN_NONE 0         /* no launch yet, or an empty batch             */
 #define SYNCR_CDC_SCAN_STREAM_TILES 1 /* cdc_scan_st_kernel: batches >= 24 tiles/wave */
 #define SYNCR_CDC_SCAN_CU 2           /* cdc_scan_kernel, CU schedule: small batches  */

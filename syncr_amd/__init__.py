@@ -382,7 +382,9 @@ class Chunker:
         name = ctypes.c_char_p()
         _check(library().syncr_cdc_last_scan(self._h, v, ctypes.byref(name)), "syncr_cdc_last_scan")
         return {"kind": SCAN_KINDS.get(int(v[0]), str(int(v[0]))), "kernel": (name.value or b"").decode(),
-                "tiles": int(v[1]), "waves": int(v[2]), "tiles_per_wave": int(v[3]) / 1000.0}
+                "tiles": int(v[1]), "waves": int(v[2]),
+                "tiles_per_wave": round(int(v[1]) / int(v[2]), 3) if int(v[2]) else 0.0,
+                "st_segments": int(v[3])}
 
     def synchronize(self) -> None:
         _check(library().syncr_cdc_synchronize(self._h), "syncr_cdc_synchronize")

@@ -206,6 +206,7 @@ size_t split_ctr_offset(const syncr_cdc *h) {
 size_t sched_offset(const syncr_cdc *h) { return (split_ctr_offset(h) + SPL_WORDS * 4 + 127) & ~size_t(127); }
 // the stream-tile scan's split last round: per-part counts of at most one ST per scan wave
 uint32_t nst_of(const syncr_cdc *h) { return (h->ntiles + ST_TILES - 1) / ST_TILES; }
+uint32_t st_tiles_of(int segs) { return (uint32_t)segs * 8u / 9u; }
 size_t tail_offset(const syncr_cdc *h) { return sched_offset(h) + (size_t)SCHED_REGIONS * COARSE_STRIDE * 4; }
 size_t tail_tiles_cap(const syncr_cdc *h) { return (size_t)std::min<uint32_t>(h->scan_grid, nst_of(h)) * ST_TILES; }
 size_t tscan_offset(const syncr_cdc *h) { return (tail_offset(h) + tail_tiles_cap(h) * 4 + 127) & ~size_t(127); }
@@ -482,10 +483,14 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
         h->scan_info[0] = (uint64_t)kind;
         h->scan_info[1] = t.ntiles;
         h->scan_info[2] = kind == SYNCR_CDC_SCAN_NONE ? 0u : waves;
-        h->scan_info[3] = waves ? (uint64_t)t.ntiles * 1000u / waves : 0u;
-        // stream tiles: the batch's last round of STs (one per wave) in st_parts parts each
-        const uint32_t nst = nst_of(h);
-        if (kind == SYNCR_CDC_SCAN_STREAM_TILES && kp.st_parts > 1 && nst > waves) {
+        h->scan_info[3] = 0;
+        // stream tiles: STs of the launch's geometry; the batch's last round of STs (one
+        // per wave) in st_parts parts each (9-segment streams only)
+        const int segs = kind == SYNCR_CDC_SCAN_STREAM_TILES ? st_segs(h->scan_grid, kp, t) : ST_SEGS;
+        const uint32_t nst = (h->ntiles + st_tiles_of(segs) - 1) / st_tiles_of(segs);
+        t.st_full = nst;
+        if (kind == SYNCR_CDC_SCAN_STREAM_TILES) h->scan_info[3] = (uint64_t)segs;
+        if (kind == SYNCR_CDC_SCAN_STREAM_TILES && segs == ST_SEGS && kp.st_parts > 1 && nst > waves) {
             t.st_tail = std::min<uint32_t>((uint32_t)waves, nst - (uint32_t)waves);
             t.st_full = nst - t.st_tail;
             t.st_parts = std::min<uint32_t>(kp.st_parts, ST_MAX_PARTS);
@@ -604,6 +609,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_CDC_NOSKIP")) h->kp.no_skip = atoi(a) != 0;                    // A/B only
     if (const char *a = getenv("SYNCR_CDC_DENSE_FUSE")) h->kp.dense_fuse = atoi(a) != 0;           // A/B only
     if (const char *a = getenv("SYNCR_CDC_ST_PRIO")) h->kp.st_prio = atoi(a) != 0;               // A/B only
+    if (const char *a = getenv("SYNCR_CDC_ST_SEGS")) h->kp.st_segs = (uint32_t)atoi(a);          // A/B only
     if (const char *a = getenv("SYNCR_CDC_ST_PARTS"))                                         // A/B only
         h->kp.st_parts = (uint32_t)std::min(std::max(atoi(a), 1), (int)ST_MAX_PARTS);
     if (const char *a = getenv("SYNCR_CDC_TRACE"))                                              // timeline

@@ -89,6 +89,7 @@ __host__ __device__ constexpr int scan_lds_for_run(int run) {
 // and registers the tile for the dense pass once; later parts publish nothing.
 constexpr int ST_TILES = 8;                   // batch tiles per ST
 constexpr int ST_SEGS = 9;                    // segments per stream
+constexpr uint32_t ST18_MIN_TILES_PER_WAVE = 0xffffffffu;   // 18-segment streams from this many tiles per wave
 constexpr uint32_t ST_MAX_PARTS = 4;
 constexpr uint32_t ST_PARTS = 1;              // product: parts per ST of the last round
 constexpr uint32_t TAIL_PART_BITS = 7;
@@ -140,6 +141,7 @@ struct KParams {
                                //   the resolve walk loads ahead (0: RESOLVE_PF)
     uint32_t st_prio;          // (dev A/B: SYNCR_CDC_ST_PRIO) a wave in the batch's last round of stream-tile
                                //   units raises its issue priority the later it took its unit
+    uint32_t st_segs;          // (dev A/B: SYNCR_CDC_ST_SEGS) 9 or 18 segments per stream forced; 0: st_segs()
     uint32_t st_parts;         // stream-tile scan: the batch's last round of STs is handed out in this many
                                //   parts each (segment ranges; 1 = whole STs; ST_MAX_PARTS at most)
 };
@@ -357,6 +359,7 @@ bool scan_dense_inline(ScanGeom g, const KParams &p);      // the scan passes de
 // Which scan kernel launch_scan runs for this launch (SYNCR_CDC_SCAN_* of include/syncr_cdc.h):
 // the one decision, reported through syncr_cdc_last_scan so callers never restate it.
 int scan_kind(ScanGeom g, uint32_t grid, const KParams &p, const Tables &t);
+int st_segs(uint32_t grid, const KParams &p, const Tables &t);   // stream-tile geometry of a launch
 hipError_t launch_post(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s, bool dense_inline);
 hipError_t launch_resolve(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s);
 bool resolve_splits(const KParams &p, const Tables &t);   // launch_resolve starts split workers

@@ -824,8 +824,12 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 constexpr int ST_RUN = 128;                   // bytes per segment and stream (ST_SEGS of them: 1152-byte streams)
 constexpr int ST_LISTCAP = 32;                // candidate slots per tile (more: dense)
 constexpr int ST_DIRTYCAP = 6;                // side slots per segment
-constexpr uint32_t ST_L = ST_SEGS * ST_RUN;   // stream bytes
-static_assert(16 * ST_L == (uint32_t)tile_bytes(DEFAULT_RUN), "16 streams = one batch tile");
+// ST geometry by segments per stream: 9 (1152-byte streams, 16 per batch tile, 8
+// tiles per ST) or 18 (2304-byte streams, 16 tiles per ST: half the stream
+// starts, so half the warm-ups, halo re-reads and ST switches per byte)
+__host__ __device__ constexpr int st_tiles(int segs) { return segs * 8 / 9; }
+static_assert(16 * ST_SEGS * ST_RUN == tile_bytes(DEFAULT_RUN), "16 streams of 9 segments = one batch tile");
+static_assert(st_tiles(ST_SEGS) == ST_TILES && st_tiles(18) == 16, "ST geometry");
 struct DirtySlotST {                          // 144 bytes
     uint32_t dp[16];                          // dropped bytes, packed pairs (run A low, run B high)
     uint32_t xp[16];                          // new bytes, packed pairs
@@ -834,8 +838,9 @@ struct DirtySlotST {                          // 144 bytes
     uint32_t pad;
 };
 static_assert(sizeof(DirtySlotST) == 144, "slot size");
-__host__ __device__ constexpr int st_lds_bytes() {
-    return RUNS * ST_RUN + ST_DIRTYCAP * (int)sizeof(DirtySlotST) + ST_TILES * ST_LISTCAP * 4 + ST_TILES * 4 + 16;
+__host__ __device__ constexpr int st_lds_bytes(int segs) {
+    return RUNS * ST_RUN + ST_DIRTYCAP * (int)sizeof(DirtySlotST) + st_tiles(segs) * ST_LISTCAP * 4 +
+           st_tiles(segs) * 4 + 16;
 }
 
 __device__ __forceinline__ uint32_t xpair32(const uint32_t (&XA)[ST_RUN / 4], const uint32_t (&XB)[ST_RUN / 4], int j) {
@@ -903,28 +908,30 @@ __device__ __forceinline__ void publish_part(const Tables &T, uint32_t tile, con
 struct StUnit {
     uint32_t st, g0, g1, part;
 };
+template <int SEGS>
 __device__ __forceinline__ StUnit st_unit(const Tables &T, uint32_t u) {
-    if (u < T.st_full) return {u, 0u, (uint32_t)ST_SEGS, ~0u};
+    if (u < T.st_full) return {u, 0u, (uint32_t)SEGS, ~0u};
     const uint32_t v = u - T.st_full, part = v / T.st_tail;
-    return {T.st_full + v % T.st_tail, part * (uint32_t)ST_SEGS / T.st_parts,
-            (part + 1u) * (uint32_t)ST_SEGS / T.st_parts, part};
+    return {T.st_full + v % T.st_tail, part * (uint32_t)SEGS / T.st_parts,
+            (part + 1u) * (uint32_t)SEGS / T.st_parts, part};
 }
 
-template <int MODE>
+template <int MODE, int SEGS = ST_SEGS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUN = ST_RUN;
     constexpr int NW = RUN / 4;                  // words per segment and run
     constexpr int NG = RUN / 16;                 // 16-byte groups per segment
-    constexpr uint32_t L = ST_L;
+    constexpr int TILES = st_tiles(SEGS);        // batch tiles per ST
+    constexpr uint32_t L = SEGS * ST_RUN;        // stream bytes
     constexpr uint32_t STB = RUNS * L;           // ST bytes
     constexpr int NDMA = RUNS * RUN / 1024;      // DMA instructions per segment (8 streams each)
     const int lane = threadIdx.x;
     uint8_t *wl = smem;
     DirtySlotST *dslots = (DirtySlotST *)(smem + RUNS * RUN);
     uint32_t *tlist = (uint32_t *)(smem + RUNS * RUN + ST_DIRTYCAP * sizeof(DirtySlotST));
-    uint32_t *tcnt = tlist + ST_TILES * ST_LISTCAP;
+    uint32_t *tcnt = tlist + TILES * ST_LISTCAP;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
     // work units: st_full whole STs, then st_tail STs in st_parts parts each
     const uint32_t nunits = T.st_full + T.st_tail * T.st_parts;
@@ -972,7 +979,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     };
     scan_time_entry(T);
     if (blockIdx.x >= nunits) return;
-    StUnit un = st_unit(T, blockIdx.x);
+    StUnit un = st_unit<SEGS>(T, blockIdx.x);
     uint32_t st = un.st;
     const bool stamp = blockIdx.x < (uint32_t)DBG_SCAN_N;              // timeline slot (dev)
     if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x, wall_clock64());
@@ -995,7 +1002,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 #pragma unroll 1
         for (uint32_t g = un.g0; g < un.g1; ++g) {
             const bool first = g == un.g0;
-            if (first && lane < ST_TILES) tcnt[lane] = 0u;
+            if (first && lane < TILES) tcnt[lane] = 0u;
             uint32_t have = 0;                                       // dirty slots taken (wave-uniform)
             wait_vmcnt<0>();                                         // segment g landed (and, at 0, the halo)
 #ifdef SYNCR_CDC_DEV
@@ -1049,7 +1056,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 nextu = nunits > gridDim.x ? gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nunits;
                 more = nextu < nunits;
                 if (more) {
-                    nun = st_unit(T, nextu);
+                    nun = st_unit<SEGS>(T, nextu);
                     issue_seg(nun.st, nun.g0);
                     load_halo(nun.st, nun.g0);
                 }
@@ -1084,8 +1091,8 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                         // no room for this group's dirty streams: their tiles go to the dense
                         // pass (lane l's streams l and l + 64 lie in tiles l / 16 and 4 + l / 16;
                         // the marks are applied when the ST is published)
-                        dmark |= ((a & 0xffffu) == 0u ? 1u << (lane >> 4) : 0u) |
-                                 ((a >> 16) == 0u ? 16u << (lane >> 4) : 0u);
+                        dmark |= ((a & 0xffffu) == 0u ? 1u << ((uint32_t)lane * SEGS / 144u) : 0u) |
+                                 ((a >> 16) == 0u ? 1u << (((uint32_t)lane + 64u) * SEGS / 144u) : 0u);
                     } else {
                         if (z) {                                           // slot: have + rank among z lanes
                             const uint32_t idx = have + __builtin_amdgcn_mbcnt_hi(
@@ -1145,16 +1152,16 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 if (__builtin_expect(__ballot(dmark != 0u) != 0ull, 0)) {   // tiles with unrecorded dirty groups
                     uint32_t m = 0;
 #pragma unroll
-                    for (int t = 0; t < ST_TILES; ++t)
+                    for (int t = 0; t < TILES; ++t)
                         if (__ballot((dmark >> t) & 1u)) m |= 1u << t;
-                    if (lane < ST_TILES && ((m >> lane) & 1u)) atomicOr(&tcnt[lane], 0x80000000u);
+                    if (lane < TILES && ((m >> lane) & 1u)) atomicOr(&tcnt[lane], 0x80000000u);
                     dmark = 0u;
                 }
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll 1
-                for (uint32_t t = 0; t < (uint32_t)ST_TILES; ++t) {
-                    const uint32_t tile = st * ST_TILES + t;
+                for (uint32_t t = 0; t < (uint32_t)TILES; ++t) {
+                    const uint32_t tile = st * TILES + t;
                     if (tile >= T.ntiles) break;
                     const uint32_t c = __builtin_amdgcn_readfirstlane(
                         __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)&tcnt[t], __ATOMIC_RELAXED,
@@ -1178,7 +1185,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                                  : "=s"(hwid), "=s"(xcc));
                     SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 2, wall_clock64());
                     SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 3,
-                               (uint64_t)(8u * (nst_done + 1u)) | ((uint64_t)hwid << 32) | ((uint64_t)(xcc & 0xf) << 28));
+                               (uint64_t)(TILES * (nst_done + 1u)) | ((uint64_t)hwid << 32) | ((uint64_t)(xcc & 0xf) << 28));
                 }
 #endif
                 return;
@@ -3802,6 +3809,15 @@ hipError_t launch_read_probe(const uint8_t *d, uint64_t bytes, bool nt, uint32_t
 // The CU schedule: one workgroup of SCAN_CU_WAVES waves per CU (grid = the
 // per-wave grid / SCAN_CU_WAVES), plus the LDS tile counter.
 constexpr int SCAN_CU_WAVES = 8;
+// The stream-tile scan with the geometry st_segs() picks for this launch.
+static void launch_st(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
+    if (st_segs(grid, p, t) == 18)
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4, 18>), dim3(grid), dim3(64), st_lds_bytes(18), s, d, p, t);
+    else
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4, ST_SEGS>), dim3(grid), dim3(64), st_lds_bytes(ST_SEGS), s, d, p,
+                           t);
+}
+
 // The > 64 KB dynamic-LDS attribute is set once per (kernel instance, device), under
 // a lock: multi-device ingest opens and launches handles from several threads.
 template <int RUN, int MODE>
@@ -3896,7 +3912,7 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
     else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.ablate == 17u)                                        // A/B: stream-tile scan (exact)
-        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
+        launch_st(grid, d, p, t, s);
     else if (p.ablate == 15u) {                                      // A/B: CU schedule (exact)
         (void)launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s);
     } else if (p.ablate == 16u) {                                    // timing only: CU schedule, no warm-up/halo
@@ -3913,7 +3929,7 @@ static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, con
     else if (p.nt && p.scan_tiles && scan_dynamic(t.ntiles, grid))   // product, dense-heavy data: tiles
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.nt && !p.scan_tiles && scan_stream_tiles(t.ntiles, grid) && RUN == DEFAULT_RUN)   // product: stream tiles
-        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
+        launch_st(grid, d, p, t, s);
     else if (p.nt && scan_dynamic(t.ntiles, grid))                   // other geometries: nt + dynamic groups + ROLL2
         hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
     else if (p.nt)                                                   // product, small batch: CU schedule
@@ -4007,12 +4023,21 @@ static hipError_t launch_scan_kernel(ScanGeom g, uint32_t grid, const uint8_t *d
         hipLaunchKernelGGL((cdc_scan_kernel<DEFAULT_RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64),
                            lds_wave_bytes(DEFAULT_RUN), s, d, p, t);
     else if (kind == SYNCR_CDC_SCAN_STREAM_TILES) // >= 3 stream tiles per wave (§4.6)
-        hipLaunchKernelGGL((cdc_scan_st_kernel<4>), dim3(grid), dim3(64), st_lds_bytes(), s, d, p, t);
+        launch_st(grid, d, p, t, s);
     else                                          // small batch: the CU schedule (per-wave static shares end
         return launch_scan_cu<DEFAULT_RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);   // with the slow waves alone)
     return hipGetLastError();
 }
 #endif
+
+// Segments per stream of the stream-tile scan (9 or 18, see st_tiles): 18 from
+// ST18_MIN_TILES_PER_WAVE tiles per scan wave (the dev library's KParams::st_segs
+// forces one).
+int st_segs(uint32_t grid, const KParams &p, const Tables &t) {
+    if (p.st_segs == 9u || p.st_segs == 18u) return (int)p.st_segs;
+    grid = grid < t.ntiles ? grid : t.ntiles;
+    return (uint64_t)t.ntiles >= (uint64_t)grid * ST18_MIN_TILES_PER_WAVE ? 18 : ST_SEGS;
+}
 
 // The scan launch of do_launch; e0 / e1 (may be null): HIP events recorded around it.
 hipError_t launch_scan(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,

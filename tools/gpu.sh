@@ -13,7 +13,8 @@
 #   ab|<workload>|<rounds>|<V1>|<V2>... tools/dip_ab.py variants (dev library) in the driver's condition
 #   trace|<workload>[|<shard>[|--no-events]]  kernel trace of one small-batch leg (tools/legs_trace.py, product)
 #   sttrace|<workload>|<ENV=V,...>      per-wave stream-tile scan timeline (tools/scan_timeline.py, dev)
-#   prof|<PROFTAG>[|<extra flags>]      tools/prof.sh: trace + traffic + SQ passes of the driver's command
+#   prof|<PROFTAG>[|<extra flags>[|<ENV=V,...>]]  tools/prof.sh: trace + traffic + SQ passes of the driver's
+#                                       command (e.g. "prof|r05_st18|--dev-lib|SYNCR_CDC_ST_SEGS=18")
 #   build                               python -m syncr_amd.build (+ --dev) on the box (normally built here)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -80,7 +81,7 @@ PY
             || { echo "sttrace failed rc=$?"; tail -20 "$out.err"; exit 17; }
         head -c 1500 "$out.json"; echo ;;
     prof)
-        bash tools/prof.sh "${a[1]}" ${a[2]} || { echo "prof failed rc=$?"; exit 18; } ;;
+        envrun "${a[3]}" bash tools/prof.sh "${a[1]}" ${a[2]} || { echo "prof failed rc=$?"; exit 18; } ;;
     build)
         timeout -k 10 900 python -m syncr_amd.build --force > "$out.log" 2>&1 && \
         timeout -k 10 900 python -m syncr_amd.build --force --dev >> "$out.log" 2>&1 || { echo "build failed"; exit 19; } ;;
