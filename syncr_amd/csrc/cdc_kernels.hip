@@ -822,14 +822,16 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 // in registers then) and its entry state.
 // ---------------------------------------------------------------------------
 constexpr int ST_RUN = 128;                   // bytes per segment and stream (ST_SEGS of them: 1152-byte streams)
-constexpr int ST_LISTCAP = 32;                // candidate slots per tile (more: dense)
+constexpr int ST_LISTCAP = 32;                // candidate slots per tile (more: dense); 16 from 36 segments
+__host__ __device__ constexpr int st_listcap(int segs) { return segs >= 36 ? 16 : ST_LISTCAP; }
 constexpr int ST_DIRTYCAP = 6;                // side slots per segment
 // ST geometry by segments per stream: 9 (1152-byte streams, 16 per batch tile, 8
 // tiles per ST) or 18 (2304-byte streams, 16 tiles per ST: half the stream
 // starts, so half the warm-ups, halo re-reads and ST switches per byte)
 __host__ __device__ constexpr int st_tiles(int segs) { return segs * 8 / 9; }
 static_assert(16 * ST_SEGS * ST_RUN == tile_bytes(DEFAULT_RUN), "16 streams of 9 segments = one batch tile");
-static_assert(st_tiles(ST_SEGS) == ST_TILES && st_tiles(18) == 16, "ST geometry");
+static_assert(st_tiles(ST_SEGS) == ST_TILES && st_tiles(18) == 16 && st_tiles(27) == 24 && st_tiles(36) == 32,
+              "ST geometry");
 struct DirtySlotST {                          // 144 bytes
     uint32_t dp[16];                          // dropped bytes, packed pairs (run A low, run B high)
     uint32_t xp[16];                          // new bytes, packed pairs
@@ -839,7 +841,7 @@ struct DirtySlotST {                          // 144 bytes
 };
 static_assert(sizeof(DirtySlotST) == 144, "slot size");
 __host__ __device__ constexpr int st_lds_bytes(int segs) {
-    return RUNS * ST_RUN + ST_DIRTYCAP * (int)sizeof(DirtySlotST) + st_tiles(segs) * ST_LISTCAP * 4 +
+    return RUNS * ST_RUN + ST_DIRTYCAP * (int)sizeof(DirtySlotST) + st_tiles(segs) * st_listcap(segs) * 4 +
            st_tiles(segs) * 4 + 16;
 }
 
@@ -850,10 +852,10 @@ __device__ __forceinline__ uint32_t xpair32(const uint32_t (&XA)[ST_RUN / 4], co
 // Publish one tile's list (n candidates, tile-relative positions) or mark it dense.
 template <class DS>
 __device__ __forceinline__ void publish_list(const Tables &T, uint32_t tile, const uint32_t *list, uint32_t n,
-                                             int lane, bool force_dense, DS &ds) {
+                                             int lane, bool force_dense, DS &ds, uint32_t cap = ST_LISTCAP) {
     if (n == 0u && !force_dense) return;
     if (lane == 0) atomicOr(&T.nonempty[tile >> 6], 1ull << (tile & 63));
-    if (n > (uint32_t)ST_LISTCAP || force_dense) {
+    if (n > cap || force_dense) {
         dense_mark(T, tile, lane, ds);
         return;
     }
@@ -873,9 +875,10 @@ __device__ __forceinline__ void publish_list(const Tables &T, uint32_t tile, con
 // pass for the tile (ST_TILES comment in cdc_internal.h).
 template <class DS>
 __device__ __forceinline__ void publish_part(const Tables &T, uint32_t tile, const uint32_t *list, uint32_t n,
-                                             int lane, bool force_dense, uint32_t part, DS &ds) {
+                                             int lane, bool force_dense, uint32_t part, DS &ds,
+                                             uint32_t cap = ST_LISTCAP) {
     const uint32_t ss = (uint32_t)LISTCAP / T.st_parts;        // slots per part
-    const bool dense = force_dense || n > ss || n > (uint32_t)ST_LISTCAP;
+    const bool dense = force_dense || n > ss || n > cap;
     if (n == 0u && !dense) return;
     uint32_t old = 0;
     if (lane == 0)
@@ -925,13 +928,14 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     constexpr int NG = RUN / 16;                 // 16-byte groups per segment
     constexpr int TILES = st_tiles(SEGS);        // batch tiles per ST
     constexpr uint32_t L = SEGS * ST_RUN;        // stream bytes
+    constexpr int LC = st_listcap(SEGS);         // candidate slots per tile in LDS
     constexpr uint32_t STB = RUNS * L;           // ST bytes
     constexpr int NDMA = RUNS * RUN / 1024;      // DMA instructions per segment (8 streams each)
     const int lane = threadIdx.x;
     uint8_t *wl = smem;
     DirtySlotST *dslots = (DirtySlotST *)(smem + RUNS * RUN);
     uint32_t *tlist = (uint32_t *)(smem + RUNS * RUN + ST_DIRTYCAP * sizeof(DirtySlotST));
-    uint32_t *tcnt = tlist + TILES * ST_LISTCAP;
+    uint32_t *tcnt = tlist + TILES * LC;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
     // work units: st_full whole STs, then st_tail STs in st_parts parts each
     const uint32_t nunits = T.st_full + T.st_tail * T.st_parts;
@@ -1089,10 +1093,12 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                     const uint32_t nz = (uint32_t)__builtin_popcountll(bz);
                     if (have + nz > (uint32_t)ST_DIRTYCAP) {
                         // no room for this group's dirty streams: their tiles go to the dense
-                        // pass (lane l's streams l and l + 64 lie in tiles l / 16 and 4 + l / 16;
+                        // pass (the tiles of the dirty groups of this lane's two streams;
                         // the marks are applied when the ST is published)
-                        dmark |= ((a & 0xffffu) == 0u ? 1u << ((uint32_t)lane * SEGS / 144u) : 0u) |
-                                 ((a >> 16) == 0u ? 1u << (((uint32_t)lane + 64u) * SEGS / 144u) : 0u);
+                        constexpr uint32_t TB = (uint32_t)tile_bytes(DEFAULT_RUN);
+                        const uint32_t ga = relA0 + 16u * (uint32_t)gg;        // the group's ST-relative position
+                        dmark |= ((a & 0xffffu) == 0u ? 1u << (ga / TB) : 0u) |
+                                 ((a >> 16) == 0u ? 1u << ((ga + 64u * L) / TB) : 0u);
                     } else {
                         if (z) {                                           // slot: have + rank among z lanes
                             const uint32_t idx = have + __builtin_amdgcn_mbcnt_hi(
@@ -1138,12 +1144,12 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                         if (t.x == 0 && ((1984u + (s & 0xffffu)) & P.m1) == P.m1 && (int64_t)(relA + jj) < lim_rel) {
                             const uint32_t p = relA + jj, tt = p / TB;
                             const uint32_t idx = atomicAdd(&tcnt[tt], 1u) & 0x7fffffffu;
-                            if (idx < (uint32_t)ST_LISTCAP) tlist[tt * ST_LISTCAP + idx] = p - tt * TB;
+                            if (idx < (uint32_t)LC) tlist[tt * LC + idx] = p - tt * TB;
                         }
                         if (t.y == 0 && ((1984u + (s >> 16)) & P.m1) == P.m1 && (int64_t)(relB + jj) < lim_rel) {
                             const uint32_t p = relB + jj, tt = p / TB;
                             const uint32_t idx = atomicAdd(&tcnt[tt], 1u) & 0x7fffffffu;
-                            if (idx < (uint32_t)ST_LISTCAP) tlist[tt * ST_LISTCAP + idx] = p - tt * TB;
+                            if (idx < (uint32_t)LC) tlist[tt * LC + idx] = p - tt * TB;
                         }
                     }
                 }
@@ -1167,11 +1173,11 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                         __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)&tcnt[t], __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WAVEFRONT));
                     if (un.part == ~0u)
-                        publish_list(T, tile, tlist + t * ST_LISTCAP, c & 0x7fffffffu, lane, (c >> 31) != 0u,
-                                     dslots_alloc);
+                        publish_list(T, tile, tlist + t * LC, c & 0x7fffffffu, lane, (c >> 31) != 0u,
+                                     dslots_alloc, (uint32_t)LC);
                     else
-                        publish_part(T, tile, tlist + t * ST_LISTCAP, c & 0x7fffffffu, lane, (c >> 31) != 0u,
-                                     un.part, dslots_alloc);
+                        publish_part(T, tile, tlist + t * LC, c & 0x7fffffffu, lane, (c >> 31) != 0u,
+                                     un.part, dslots_alloc, (uint32_t)LC);
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -3811,8 +3817,15 @@ hipError_t launch_read_probe(const uint8_t *d, uint64_t bytes, bool nt, uint32_t
 constexpr int SCAN_CU_WAVES = 8;
 // The stream-tile scan with the geometry st_segs() picks for this launch.
 static void launch_st(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    if (st_segs(grid, p, t) == 18)
+    const int segs = st_segs(grid, p, t);
+    if (segs == 18)
         hipLaunchKernelGGL((cdc_scan_st_kernel<4, 18>), dim3(grid), dim3(64), st_lds_bytes(18), s, d, p, t);
+#ifdef SYNCR_CDC_DEV
+    else if (segs == 27)
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4, 27>), dim3(grid), dim3(64), st_lds_bytes(27), s, d, p, t);
+    else if (segs == 36)
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4, 36>), dim3(grid), dim3(64), st_lds_bytes(36), s, d, p, t);
+#endif
     else
         hipLaunchKernelGGL((cdc_scan_st_kernel<4, ST_SEGS>), dim3(grid), dim3(64), st_lds_bytes(ST_SEGS), s, d, p,
                            t);
@@ -4035,6 +4048,9 @@ static hipError_t launch_scan_kernel(ScanGeom g, uint32_t grid, const uint8_t *d
 // forces one).
 int st_segs(uint32_t grid, const KParams &p, const Tables &t) {
     if (p.st_segs == 9u || p.st_segs == 18u) return (int)p.st_segs;
+#ifdef SYNCR_CDC_DEV
+    if (p.st_segs == 27u || p.st_segs == 36u) return (int)p.st_segs;
+#endif
     grid = grid < t.ntiles ? grid : t.ntiles;
     return (uint64_t)t.ntiles >= (uint64_t)grid * ST18_MIN_TILES_PER_WAVE ? 18 : ST_SEGS;
 }
