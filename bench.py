@@ -243,11 +243,14 @@ def cpu_baseline(dbuf, offs, lens, cuts, hcuts, sample_gib: float, skip=None):
                   f"`value` single thread (the reference chunks one file at a time, file_operations.rs:599-605), "
                   f"`threads_value` one file per thread on `threads` threads",
         "threads_value": round(gib / dtn, 4), "threads": nthr, **hw,
-        "all_cores_value": round(gib / dta, 4), "all_cores_threads": nall,
+        # (the key says what bounds it: one file per thread, so the sample's largest file -- chunked
+        # serially, as the reference does -- sets the time however many cores there are)
+        "all_cores_value_bounded_by_largest_file": round(gib / dta, 4), "all_cores_threads": nall,
+        "all_cores_largest_file_bytes": int(s_lens.max()) if s_lens.size else 0,
         "all_cores_note": (f"SURVEY §8d's 'one file per thread on all nproc cores' leg, measured: {nall} threads "
                            f"(every CPU in this process's affinity mask; nproc {nproc}) over the same sample; "
                            f"the largest sample file's serial walk bounds it (one file per thread, as the "
-                           f"reference chunks a file serially)"),
+                           f"reference chunks a file serially), so it can read below threads_value"),
         "gpu_cuts_match_sample": mism == 0, "sample_files_mismatched": int(mism),
     }
     if skip is not None:
