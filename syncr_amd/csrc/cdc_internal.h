@@ -89,7 +89,7 @@ __host__ __device__ constexpr int scan_lds_for_run(int run) {
 // and registers the tile for the dense pass once; later parts publish nothing.
 constexpr int ST_TILES = 8;                   // batch tiles per ST
 constexpr int ST_SEGS = 9;                    // segments per stream
-constexpr uint32_t ST18_MIN_TILES_PER_WAVE = 0xffffffffu;   // 18-segment streams from this many tiles per wave
+constexpr uint32_t ST27_MIN_TILES_PER_WAVE = 96;   // 27-segment streams from this many tiles per wave
 constexpr uint32_t ST_MAX_PARTS = 4;
 constexpr uint32_t ST_PARTS = 1;              // product: parts per ST of the last round
 constexpr uint32_t TAIL_PART_BITS = 7;
@@ -141,7 +141,7 @@ struct KParams {
                                //   the resolve walk loads ahead (0: RESOLVE_PF)
     uint32_t st_prio;          // (dev A/B: SYNCR_CDC_ST_PRIO) a wave in the batch's last round of stream-tile
                                //   units raises its issue priority the later it took its unit
-    uint32_t st_segs;          // (dev A/B: SYNCR_CDC_ST_SEGS) 9 or 18 segments per stream forced; 0: st_segs()
+    uint32_t st_segs;          // (dev A/B: SYNCR_CDC_ST_SEGS) 9 / 18 / 27 / 36 segments per stream forced; 0: st_segs()
     uint32_t st_parts;         // stream-tile scan: the batch's last round of STs is handed out in this many
                                //   parts each (segment ranges; 1 = whole STs; ST_MAX_PARTS at most)
 };

@@ -3818,11 +3818,11 @@ constexpr int SCAN_CU_WAVES = 8;
 // The stream-tile scan with the geometry st_segs() picks for this launch.
 static void launch_st(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
     const int segs = st_segs(grid, p, t);
-    if (segs == 18)
-        hipLaunchKernelGGL((cdc_scan_st_kernel<4, 18>), dim3(grid), dim3(64), st_lds_bytes(18), s, d, p, t);
-#ifdef SYNCR_CDC_DEV
-    else if (segs == 27)
+    if (segs == 27)
         hipLaunchKernelGGL((cdc_scan_st_kernel<4, 27>), dim3(grid), dim3(64), st_lds_bytes(27), s, d, p, t);
+#ifdef SYNCR_CDC_DEV
+    else if (segs == 18)
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4, 18>), dim3(grid), dim3(64), st_lds_bytes(18), s, d, p, t);
     else if (segs == 36)
         hipLaunchKernelGGL((cdc_scan_st_kernel<4, 36>), dim3(grid), dim3(64), st_lds_bytes(36), s, d, p, t);
 #endif
@@ -4043,16 +4043,21 @@ static hipError_t launch_scan_kernel(ScanGeom g, uint32_t grid, const uint8_t *d
 }
 #endif
 
-// Segments per stream of the stream-tile scan (9 or 18, see st_tiles): 18 from
-// ST18_MIN_TILES_PER_WAVE tiles per scan wave (the dev library's KParams::st_segs
-// forces one).
+// Segments per stream of the stream-tile scan (see st_tiles): 27 (3456-byte
+// streams, 24-tile STs) from ST27_MIN_TILES_PER_WAVE tiles per scan wave, else 9.
+// Same-process A/B, scan ms, 9 / 18 / 27 / 36 segments (profiles/r05i_*): zipf10k
+// (277 tiles per wave) 1.734 / 1.712 / 1.704 / 1.721, config 4's N = 2 shard
+// (138) 0.933 / 0.923 / 0.921, N = 4 (69) 0.513 / 0.512, N = 8 (35) 0.269 / 0.272
+// (r05h), uniform1k (28) 0.228 / 0.243: longer streams read fewer halo lines and
+// switch STs less often, but their last grabs are coarser.  (The dev library's
+// KParams::st_segs forces one of 9 / 18 / 27 / 36.)
 int st_segs(uint32_t grid, const KParams &p, const Tables &t) {
-    if (p.st_segs == 9u || p.st_segs == 18u) return (int)p.st_segs;
+    if (p.st_segs == 9u || p.st_segs == 27u) return (int)p.st_segs;
 #ifdef SYNCR_CDC_DEV
-    if (p.st_segs == 27u || p.st_segs == 36u) return (int)p.st_segs;
+    if (p.st_segs == 18u || p.st_segs == 36u) return (int)p.st_segs;
 #endif
     grid = grid < t.ntiles ? grid : t.ntiles;
-    return (uint64_t)t.ntiles >= (uint64_t)grid * ST18_MIN_TILES_PER_WAVE ? 18 : ST_SEGS;
+    return (uint64_t)t.ntiles >= (uint64_t)grid * ST27_MIN_TILES_PER_WAVE ? 27 : ST_SEGS;
 }
 
 // The scan launch of do_launch; e0 / e1 (may be null): HIP events recorded around it.

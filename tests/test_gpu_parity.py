@@ -716,15 +716,19 @@ def test_small_batches_back_to_back_stable():
 # library's choice at these thresholds through syncr_cdc_last_scan (the host never restates it)
 SCAN_ST_MIN_TILES_PER_WAVE = 24
 SCAN_DYN_MIN_TILES_PER_WAVE = 96
+ST27_MIN_TILES_PER_WAVE = 96          # cdc_internal.h: 27-segment streams from here
 
-@pytest.mark.parametrize("below", [False, True])
-def test_stream_tile_threshold_edge_vs_oracle(below):
-    """The two scans either side of SCAN_ST_MIN_TILES_PER_WAVE (cdc_kernels.hip
-    launch_scan): a batch of exactly grid x 24 tiles whose last tile holds one
-    byte (stream tiles; the batch's last stream tile is mostly past the span:
-    the clamped DMA path) and one tile less (the CU schedule), random files with
-    periodic-64 and constant ones at chunk_bits 13: every file's cuts vs the
-    oracle."""
+@pytest.mark.parametrize("per_wave,below", [(SCAN_ST_MIN_TILES_PER_WAVE, False), (SCAN_ST_MIN_TILES_PER_WAVE, True),
+                                            (ST27_MIN_TILES_PER_WAVE, False), (ST27_MIN_TILES_PER_WAVE, True)])
+def test_stream_tile_threshold_edge_vs_oracle(per_wave, below):
+    """The scans either side of the library's thresholds (cdc_kernels.hip
+    launch_scan / st_segs), as syncr_cdc_last_scan reports them: a batch of
+    exactly grid x 24 tiles whose last tile holds one byte (stream tiles of
+    9-segment streams; the batch's last stream tile is mostly past the span: the
+    clamped DMA path) and one tile less (the CU schedule); grid x 96 tiles
+    (27-segment streams, whose streams straddle batch tiles) and one less
+    (9-segment streams).  Random files with periodic-64 and constant ones at
+    chunk_bits 13: every file's cuts vs the oracle."""
     from benchlib.workloads import periodic_pattern
     bits, cap = 13, 256 << 10
     rng = np.random.default_rng(24 + below)
@@ -732,7 +736,7 @@ def test_stream_tile_threshold_edge_vs_oracle(below):
     try:
         info = ch.info()
         tb = info["tile_bytes"]
-        ntiles = info["scan_grid"] * SCAN_ST_MIN_TILES_PER_WAVE
+        ntiles = info["scan_grid"] * per_wave
         span = (ntiles - 1) * tb + (0 if below else 1)
         lens = []
         while sum(lens) < span:
@@ -744,7 +748,11 @@ def test_stream_tile_threshold_edge_vs_oracle(below):
         offs = np.zeros_like(lens)
         offs[1:] = np.cumsum(lens)[:-1]
         assert int(lens.sum()) == span
-        want = "cdc_scan_kernel" if below else "cdc_scan_st_kernel"
+        if per_wave == SCAN_ST_MIN_TILES_PER_WAVE:
+            want, kind, segs = (("cdc_scan_kernel", "cu_schedule", 0) if below else
+                                ("cdc_scan_st_kernel", "stream_tiles", 9))
+        else:
+            want, kind, segs = "cdc_scan_st_kernel", "stream_tiles", (9 if below else 27)
         buf = syncr_amd.DeviceBuffer(ch, span)
         try:
             buf.gen_corpus(offs, lens, indices=np.arange(lens.size, dtype=np.uint64) + 7001)
@@ -758,7 +766,7 @@ def test_stream_tile_threshold_edge_vs_oracle(below):
             ch.launch(buf.ptr)
             res = ch.fetch()
             rep = ch.last_scan()                   # the library's own report (syncr_cdc_last_scan)
-            assert rep["kernel"] == want and rep["kind"] == ("cu_schedule" if below else "stream_tiles"), rep
+            assert rep["kernel"] == want and rep["kind"] == kind and rep["st_segments"] == segs, rep
             assert rep["tiles"] == ntiles - below and rep["waves"] == info["scan_grid"], rep
             host = buf.download(span)
             print(f"{want} edge batch: {lens.size} files, {span} bytes; oracle next", flush=True)
@@ -803,7 +811,7 @@ def test_large_batch_stream_tiles_vs_oracle(bits, cap):
             ch.plan(offs, lens, span)
             ch.launch(buf.ptr)
             res = ch.fetch()
-            assert ch.last_scan()["kind"] == "stream_tiles", ch.last_scan()
+            assert ch.last_scan()["kind"] == "stream_tiles" and ch.last_scan()["st_segments"] == 27, ch.last_scan()
             host = buf.download(span)
             print(f"stream-tile batch: {lens.size} files, {span / 2**30:.2f} GiB chunked; oracle next", flush=True)
         finally:
