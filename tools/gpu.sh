@@ -13,6 +13,7 @@
 #   ab|<workload>|<rounds>|<V1>|<V2>... tools/dip_ab.py variants (dev library) in the driver's condition
 #   trace|<workload>[|<shard>[|--no-events]]  kernel trace of one small-batch leg (tools/legs_trace.py, product)
 #   sttrace|<workload>|<ENV=V,...>      per-wave stream-tile scan timeline (tools/scan_timeline.py, dev)
+#   restl|<workload>                    resolve timeline (tools/resolve_timeline.py, dev library)
 #   prof|<PROFTAG>[|<extra flags>[|<ENV=V,...>]]  tools/prof.sh: trace + traffic + SQ passes of the driver's
 #                                       command (e.g. "prof|r05_st18|--dev-lib|SYNCR_CDC_ST_SEGS=18")
 #   build                               python -m syncr_amd.build (+ --dev) on the box (normally built here)
@@ -80,6 +81,10 @@ PY
         envrun "${a[2]}" timeout -k 10 300 python -u tools/scan_timeline.py --workload "${a[1]}" > "$out.json" 2> "$out.err" \
             || { echo "sttrace failed rc=$?"; tail -20 "$out.err"; exit 17; }
         head -c 1500 "$out.json"; echo ;;
+    restl)
+        timeout -k 10 300 python -u tools/resolve_timeline.py --workload "${a[1]}" --launches 3 > "$out.txt" 2> "$out.err" \
+            || { echo "restl failed rc=$?"; tail -20 "$out.err"; exit 20; }
+        cat "$out.txt" ;;
     prof)
         envrun "${a[3]}" bash tools/prof.sh "${a[1]}" ${a[2]} || { echo "prof failed rc=$?"; exit 18; } ;;
     build)

@@ -40,7 +40,13 @@ def main():
         k, v = kv.split("=", 1)
         os.environ[k] = v
     os.environ["SYNCR_CDC_TRACE"] = "1"
-    sizes, idx, _ = bench.workload(args.workload, 1)
+    if args.workload == "shard8":                   # BASELINE config 4's rank-0 batch at N = 8
+        from benchlib import workloads as WL
+        z = WL.zipf_sizes()
+        sh = WL.lpt_shard(z, 8)[0]
+        sizes, idx = z[sh], sh.astype(np.uint64)
+    else:
+        sizes, idx, _ = bench.workload(args.workload, 1)
     offs = np.zeros_like(sizes)
     offs[1:] = np.cumsum(sizes)[:-1]
     span = int(sizes.sum())
@@ -85,6 +91,10 @@ def main():
         order = np.argsort(-sizes.astype(np.int64), kind="stable")
         print("  latest file walkers (end us, order index, size KiB, corpus index): " +
               ", ".join(f"{e:.1f}/{k}/{int(sizes[order[k]]) >> 10}/{int(idx[order[k]])}" for e, k in ends))
+        allw = np.array([us(v) for v in fw if v])
+        if allw.size:
+            print(f"  file walker ends ({allw.size}): p50 {np.percentile(allw, 50):.1f} p90 {np.percentile(allw, 90):.1f} "
+                  f"p99 {np.percentile(allw, 99):.1f} max {allw.max():.1f}; resolve end {us(d[DBG_RES_END])}")
     buf.free()
 
 
