@@ -11,7 +11,8 @@
 #   smoke                               __graft_entry__.smoke()
 #   bench[|<extra bench.py flags>]      the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 #   ab|<workload>|<rounds>|<V1>|<V2>... tools/dip_ab.py variants (dev library) in the driver's condition
-#   trace|<workload>[|<shard>[|--no-events]]  kernel trace of one small-batch leg (tools/legs_trace.py, product)
+#   trace|<workload>[|<shard>[|--no-events[|<checkout>]]]  kernel trace of one small-batch leg
+#                                       (tools/legs_trace.py, product; <checkout>: e.g. build/r04src)
 #   sttrace|<workload>|<ENV=V,...>      per-wave stream-tile scan timeline (tools/scan_timeline.py, dev)
 #   restl|<workload>                    resolve timeline (tools/resolve_timeline.py, dev library)
 #   prof|<PROFTAG>[|<extra flags>[|<ENV=V,...>]]  tools/prof.sh: trace + traffic + SQ passes of the driver's
@@ -71,8 +72,9 @@ PY
         P=$O/${TAG}_${n}_trace_${a[1]}
         mkdir -p "$P"
         SH=${a[2]:-0}
+        LROOT=$R/${a[4]:-.}                        # another checkout's leg (e.g. build/r04src: before/after)
         ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$P" -o run -- \
-            python3 "$R/tools/legs_trace.py" --workload "${a[1]}" --shard "$SH" ${a[3]} > "$P/leg.json" 2> "$P/leg.err" ) \
+            python3 "$LROOT/tools/legs_trace.py" --workload "${a[1]}" --shard "$SH" ${a[3]} > "$P/leg.json" 2> "$P/leg.err" ) \
             || { echo "trace failed rc=$?"; tail -20 "$P/leg.err"; exit 16; }
         f=$(find "$P" -name '*kernel_trace.csv' | head -1)
         nb=$(python3 -c "import json;print(json.loads(open('$P/leg.json').read().strip().splitlines()[-1])['bytes'])")
