@@ -184,7 +184,6 @@ KParams make_kparams(const syncr_cdc_params &p) {
     k.resolve_lane = (p.flags & SYNCR_CDC_FLAG_RESOLVE_LANE) ? 1u : 0u;
     k.resolve_noburst = (p.flags & SYNCR_CDC_FLAG_RESOLVE_NOBURST) ? 1u : 0u;
     k.resolve_nosplit = (p.flags & SYNCR_CDC_FLAG_RESOLVE_NOSPLIT) ? 1u : 0u;
-    k.st_parts = ST_PARTS;
     return k;
 }
 
@@ -204,12 +203,8 @@ size_t split_ctr_offset(const syncr_cdc *h) {
     return coarse_offset(h) + (size_t)ncoarse(h) * COARSE_STRIDE * 4;
 }
 size_t sched_offset(const syncr_cdc *h) { return (split_ctr_offset(h) + SPL_WORDS * 4 + 127) & ~size_t(127); }
-// the stream-tile scan's split last round: per-part counts of at most one ST per scan wave
-uint32_t nst_of(const syncr_cdc *h) { return (h->ntiles + ST_TILES - 1) / ST_TILES; }
 uint32_t st_tiles_of(int segs) { return (uint32_t)segs * 8u / 9u; }
-size_t tail_offset(const syncr_cdc *h) { return sched_offset(h) + (size_t)SCHED_REGIONS * COARSE_STRIDE * 4; }
-size_t tail_tiles_cap(const syncr_cdc *h) { return (size_t)std::min<uint32_t>(h->scan_grid, nst_of(h)) * ST_TILES; }
-size_t tscan_offset(const syncr_cdc *h) { return (tail_offset(h) + tail_tiles_cap(h) * 4 + 127) & ~size_t(127); }
+size_t tscan_offset(const syncr_cdc *h) { return sched_offset(h) + (size_t)SCHED_REGIONS * COARSE_STRIDE * 4; }
 size_t zeroed_bytes(const syncr_cdc *h) { return tscan_offset(h) + 128; }
 size_t zstride(const syncr_cdc *h) { return (zeroed_bytes(h) + 255) & ~size_t(255); }
 uint8_t *zblock(const syncr_cdc *h, uint32_t par) { return h->zeroed.as<uint8_t>() + par * zstride(h); }
@@ -266,11 +261,7 @@ Tables make_tables(syncr_cdc *h) {
     t.runs_cap = (h->n_elig && h->seg_cap) ? h->runs_cap : 0u;     // deferral only when the copy launch runs
     t.split = reinterpret_cast<uint32_t *>(zb + split_ctr_offset(h));
     t.sched = reinterpret_cast<uint32_t *>(zb + sched_offset(h));
-    t.tail_meta = reinterpret_cast<uint32_t *>(zb + tail_offset(h));
-    t.st_full = nst_of(h);                 // no split round unless do_launch sets one
-    t.st_tail = 0;
-    t.st_parts = 1;
-    t.tail_tile0 = h->ntiles;
+    t.nst = (h->ntiles + ST_TILES - 1) / ST_TILES;   // do_launch sets the launch's geometry
     t.tscan = reinterpret_cast<uint64_t *>(zb + tscan_offset(h));
     t.tacc = (h->timing && h->timing_clock) ? h->tacc.as<uint64_t>() : nullptr;
     t.znext = reinterpret_cast<uint4 *>(zblock(h, h->zpar ^ 1u));
@@ -484,18 +475,10 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
         h->scan_info[1] = t.ntiles;
         h->scan_info[2] = kind == SYNCR_CDC_SCAN_NONE ? 0u : waves;
         h->scan_info[3] = 0;
-        // stream tiles: STs of the launch's geometry; the batch's last round of STs (one
-        // per wave) in st_parts parts each (9-segment streams only)
+        // stream tiles: STs of the launch's geometry
         const int segs = kind == SYNCR_CDC_SCAN_STREAM_TILES ? st_segs(h->scan_grid, kp, t) : ST_SEGS;
-        const uint32_t nst = (h->ntiles + st_tiles_of(segs) - 1) / st_tiles_of(segs);
-        t.st_full = nst;
+        t.nst = (h->ntiles + st_tiles_of(segs) - 1) / st_tiles_of(segs);
         if (kind == SYNCR_CDC_SCAN_STREAM_TILES) h->scan_info[3] = (uint64_t)segs;
-        if (kind == SYNCR_CDC_SCAN_STREAM_TILES && segs == ST_SEGS && kp.st_parts > 1 && nst > waves) {
-            t.st_tail = std::min<uint32_t>((uint32_t)waves, nst - (uint32_t)waves);
-            t.st_full = nst - t.st_tail;
-            t.st_parts = std::min<uint32_t>(kp.st_parts, ST_MAX_PARTS);
-            t.tail_tile0 = t.st_full * ST_TILES;
-        }
     }
     CHECK_HIP(launch_scan(h->geom, h->scan_grid, d_bytes, kp, t, s, bound ? pt.ev[0] : nullptr,
                           bound ? pt.ev[1] : nullptr));
@@ -608,10 +591,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_CDC_SPLIT_FIRST")) h->kp.split_first = (uint32_t)atoi(a) != 0; // A/B only
     if (const char *a = getenv("SYNCR_CDC_NOSKIP")) h->kp.no_skip = atoi(a) != 0;                    // A/B only
     if (const char *a = getenv("SYNCR_CDC_DENSE_FUSE")) h->kp.dense_fuse = atoi(a) != 0;           // A/B only
-    if (const char *a = getenv("SYNCR_CDC_ST_PRIO")) h->kp.st_prio = atoi(a) != 0;               // A/B only
     if (const char *a = getenv("SYNCR_CDC_ST_SEGS")) h->kp.st_segs = (uint32_t)atoi(a);          // A/B only
-    if (const char *a = getenv("SYNCR_CDC_ST_PARTS"))                                         // A/B only
-        h->kp.st_parts = (uint32_t)std::min(std::max(atoi(a), 1), (int)ST_MAX_PARTS);
     if (const char *a = getenv("SYNCR_CDC_TRACE"))                                              // timeline
         if (atoi(a)) CHECK_HIP(h->dbg.ensure(DBG_WORDS * sizeof(uint64_t)));
     if (const char *a = getenv("SYNCR_CDC_SPLIT_SEGC")) h->split_segc = std::max(256, atoi(a));        // A/B only

@@ -76,27 +76,15 @@ __host__ __device__ constexpr int scan_lds_for_run(int run) {
 
 // ---- stream-tile scan (cdc_scan_st_kernel) --------------------------------
 // A stream tile (ST) is ST_TILES consecutive batch tiles cut into 128 streams
-// of ST_SEGS segments.  The batch's last round of STs (Tables::st_tail of them,
-// about one per scan wave) is handed out in Tables::st_parts parts each: part
-// p is segments [p * ST_SEGS / parts, (p + 1) * ST_SEGS / parts) of all 128
-// streams, rolled by whichever wave grabs it (a part warms up from the 64
-// bytes before its first segment like any stream start).  Smaller last units
-// end the waves closer together.  Each part publishes its own sorted list per
-// tile into slots [p * LISTCAP / parts, ...) of the tile, its count into
-// Tables::tail_meta (TAIL_PART_BITS per part; zeroed per launch), and the
-// compaction merges the parts' lists.  A part that finds the tile dense sets
-// TAIL_DENSE: the first such part takes back the counts the other parts added
-// and registers the tile for the dense pass once; later parts publish nothing.
+// of ST_SEGS segments (27 from ST27_MIN_TILES_PER_WAVE tiles per scan wave:
+// st_segs()), handed out whole from a counter.  (Round 5 measured handing the
+// batch's last round out in segment-range parts, to end the waves closer
+// together, and a raised issue priority for the last round's late waves: both
+// null or slower -- DESIGN.md §4.1 -- and removed, with the extra branches and
+// runtime loop bounds they put in the hot loop.)
 constexpr int ST_TILES = 8;                   // batch tiles per ST
 constexpr int ST_SEGS = 9;                    // segments per stream
 constexpr uint32_t ST27_MIN_TILES_PER_WAVE = 96;   // 27-segment streams from this many tiles per wave
-constexpr uint32_t ST_MAX_PARTS = 4;
-constexpr uint32_t ST_PARTS = 1;              // product: parts per ST of the last round
-constexpr uint32_t TAIL_PART_BITS = 7;
-constexpr uint32_t TAIL_DENSE = 0x40000000u;
-__host__ __device__ constexpr uint32_t tail_part_count(uint32_t tm, uint32_t p) {
-    return (tm >> (TAIL_PART_BITS * p)) & ((1u << TAIL_PART_BITS) - 1u);
-}
 
 // ctr[] words (zeroed by the per-launch memset)
 enum { CTR_DENSE = 0, CTR_FLAGS = 1, CTR_CANDS_LO = 2, CTR_CANDS_HI = 3 };
@@ -139,11 +127,7 @@ struct KParams {
                                //   SYNCR_CDC_DENSE_FUSE=0)
     uint32_t resolve_pf;       // development library only (SYNCR_CDC_RESOLVE_PF): candidate windows
                                //   the resolve walk loads ahead (0: RESOLVE_PF)
-    uint32_t st_prio;          // (dev A/B: SYNCR_CDC_ST_PRIO) a wave in the batch's last round of stream-tile
-                               //   units raises its issue priority the later it took its unit
     uint32_t st_segs;          // (dev A/B: SYNCR_CDC_ST_SEGS) 9 / 18 / 27 / 36 segments per stream forced; 0: st_segs()
-    uint32_t st_parts;         // stream-tile scan: the batch's last round of STs is handed out in this many
-                               //   parts each (segment ranges; 1 = whole STs; ST_MAX_PARTS at most)
 };
 constexpr int RESOLVE_PF = 8;  // product: candidate windows in the resolve walk's LDS ring (PF-1 ahead)
 
@@ -276,12 +260,7 @@ struct Tables {
     uint64_t *hzero;               // [B3C_WORDS] hash counters of this launch (hashed launches), or nullptr
     uint64_t *dbg;                 // development library only (SYNCR_CDC_TRACE=1): [DBG_WORDS] resolve
                                    //   timeline (wall_clock64 stamps, DBG_*), else nullptr
-    // stream-tile scan's split last round (see ST_TILES above); tail_tile0 = ntiles: none
-    uint32_t st_full;              // STs handed out whole: [0, st_full)
-    uint32_t st_tail;              // STs handed out in st_parts parts: [st_full, st_full + st_tail)
-    uint32_t st_parts;
-    uint32_t tail_tile0;           // first tile of the split STs (st_full * ST_TILES)
-    uint32_t *tail_meta;           // [st_tail * ST_TILES] per-part counts | TAIL_DENSE (zeroed per launch)
+    uint32_t nst;                  // stream-tile scan: STs of the batch (launch geometry)
     // scan timing by the device clock (syncr_cdc_set_timing mode 2; null: off): the scan's
     // waves stamp wall_clock64 -- tscan[0] = ~0 - the earliest entry, tscan[1] = the
     // latest exit (atomic max, zeroed per launch) -- and the resolve adds exit - entry

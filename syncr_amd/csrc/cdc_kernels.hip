@@ -870,55 +870,6 @@ __device__ __forceinline__ void publish_list(const Tables &T, uint32_t tile, con
     }
 }
 
-// Publish part `part` (of T.st_parts) of a split ST's tile: its sorted list into
-// the part's slot range and its count into T.tail_meta, or request the dense
-// pass for the tile (ST_TILES comment in cdc_internal.h).
-template <class DS>
-__device__ __forceinline__ void publish_part(const Tables &T, uint32_t tile, const uint32_t *list, uint32_t n,
-                                             int lane, bool force_dense, uint32_t part, DS &ds,
-                                             uint32_t cap = ST_LISTCAP) {
-    const uint32_t ss = (uint32_t)LISTCAP / T.st_parts;        // slots per part
-    const bool dense = force_dense || n > ss || n > cap;
-    if (n == 0u && !dense) return;
-    uint32_t old = 0;
-    if (lane == 0)
-        old = atomicOr(&T.tail_meta[tile - T.tail_tile0], dense ? TAIL_DENSE : n << (TAIL_PART_BITS * part));
-    old = (uint32_t)__builtin_amdgcn_readfirstlane(old);
-    if (old & TAIL_DENSE) return;                              // another part sent the tile to the dense pass
-    if (lane == 0) atomicOr(&T.nonempty[tile >> 6], 1ull << (tile & 63));
-    if (dense) {
-        // the first part to find the tile dense takes back what the parts before it added
-        uint32_t prior = 0;
-        for (uint32_t q = 0; q < T.st_parts; ++q) prior += tail_part_count(old, q);
-        if (lane == 0 && prior) {
-            atomicSub(&T.super_cnt[tile >> 6], prior);
-            atomicSub(&T.coarse[(tile >> 12) * COARSE_STRIDE], prior);
-        }
-        dense_mark(T, tile, lane, ds);
-        return;
-    }
-    const uint32_t e = (uint32_t)lane < n ? list[lane] : 0xffffffffu;
-    uint32_t rank = 0;
-    for (uint32_t m = 0; m < n; ++m) rank += list[m] < e;
-    if ((uint32_t)lane < n) T.slots[(size_t)tile * LISTCAP + part * ss + rank] = make_uint2(e, 0u);
-    if (lane == 0) {
-        atomicAdd(&T.super_cnt[tile >> 6], n);
-        atomicAdd(&T.coarse[(tile >> 12) * COARSE_STRIDE], n);
-    }
-}
-
-// Work unit u of the stream-tile scan: ST `st`, segments [g0, g1); part ~0u: a whole ST
-struct StUnit {
-    uint32_t st, g0, g1, part;
-};
-template <int SEGS>
-__device__ __forceinline__ StUnit st_unit(const Tables &T, uint32_t u) {
-    if (u < T.st_full) return {u, 0u, (uint32_t)SEGS, ~0u};
-    const uint32_t v = u - T.st_full, part = v / T.st_tail;
-    return {T.st_full + v % T.st_tail, part * (uint32_t)SEGS / T.st_parts,
-            (part + 1u) * (uint32_t)SEGS / T.st_parts, part};
-}
-
 template <int MODE, int SEGS = ST_SEGS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
@@ -937,8 +888,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     uint32_t *tlist = (uint32_t *)(smem + RUNS * RUN + ST_DIRTYCAP * sizeof(DirtySlotST));
     uint32_t *tcnt = tlist + TILES * LC;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
-    // work units: st_full whole STs, then st_tail STs in st_parts parts each
-    const uint32_t nunits = T.st_full + T.st_tail * T.st_parts;
+    const uint32_t nst = T.nst;
     const int64_t span = (int64_t)T.span;
     // DMA instruction i, lane l fills slot 64 i + l = stream 8 i + l / 8, physical piece l % 8,
     // which holds logical piece (l % 8) ^ ((l / 8) & 7): a per-lane offset fixed for the kernel
@@ -967,10 +917,10 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             }
         }
     };
-    // the 64 bytes before segment g0 of each of this lane's two streams (the unit's warm-up)
+    // the 64 bytes before each of this lane's two streams (the stream's warm-up)
     uint32_t HA[16], HB[16];
-    auto load_halo = [&](uint32_t st, uint32_t g0) {
-        const int64_t sa = (int64_t)st * STB + (int64_t)lane * L + (int64_t)g0 * RUN - 64, sbb = sa + 64 * (int64_t)L;
+    auto load_halo = [&](uint32_t st) {
+        const int64_t sa = (int64_t)st * STB + (int64_t)lane * L - 64, sbb = sa + 64 * (int64_t)L;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             uint4 va, vb;
@@ -982,18 +932,16 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         }
     };
     scan_time_entry(T);
-    if (blockIdx.x >= nunits) return;
-    StUnit un = st_unit<SEGS>(T, blockIdx.x);
-    uint32_t st = un.st;
+    if (blockIdx.x >= nst) return;
+    uint32_t st = blockIdx.x;
     const bool stamp = blockIdx.x < (uint32_t)DBG_SCAN_N;              // timeline slot (dev)
     if (stamp) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x, wall_clock64());
 #ifdef SYNCR_CDC_DEV
     uint32_t nst_done = 0, seg_done = 0;
 #endif
-    issue_seg(st, un.g0);
-    load_halo(st, un.g0);
-    uint32_t pend = 0, nextu = 0;
-    StUnit nun = un;
+    issue_seg(st, 0);
+    load_halo(st);
+    uint32_t pend = 0, nextst = 0;
     uint32_t nth = 0;                              // this wave's STs so far (wave-uniform)
     DensePend dslots_alloc;
     // (a ping-pong of two carried arrays, segments unrolled in pairs to drop the 64 moves
@@ -1004,8 +952,8 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     uint32_t dmark = 0;                            // tiles (bit t) holding a dirty group no slot took
     for (;;) {
 #pragma unroll 1
-        for (uint32_t g = un.g0; g < un.g1; ++g) {
-            const bool first = g == un.g0;
+        for (uint32_t g = 0; g < (uint32_t)SEGS; ++g) {
+            const bool first = g == 0u;
             if (first && lane < TILES) tcnt[lane] = 0u;
             uint32_t have = 0;                                       // dirty slots taken (wave-uniform)
             wait_vmcnt<0>();                                         // segment g landed (and, at 0, the halo)
@@ -1042,7 +990,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // segment in registers: buffer free
             bool more = true;
-            if (g + 1 < un.g1) {
+            if (g + 1 < (uint32_t)SEGS) {
                 issue_seg(st, g + 1);
                 // the next ST comes from a counter, grabbed behind the next segment's DMAs and
                 // late in the ST (a wave that binds its next ST early can be a slow one holding
@@ -1050,19 +998,17 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 // (grabbing at segment 0 before its landing wait put every wave of the grid on
                 // one address at launch: the first segment landed 18.7 us after entry, median,
                 // tools/scan_timeline.py)
-                // (a part of a split ST grabs at its second-to-last segment too: parts have >= 2)
-                if (g == (nth == 0u ? 4u + (blockIdx.x & 3u) : un.g1 - 2u) && nunits > gridDim.x) {
+                if (g == (nth == 0u ? 4u + (blockIdx.x & 3u) : (uint32_t)SEGS - 2u) && nst > gridDim.x) {
                     // (the compiler waits for the result at once -- its copy into the
                     // loop-carried register -- but segment 1's DMAs are in flight by then)
                     if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
                 }
             } else {
-                nextu = nunits > gridDim.x ? gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nunits;
-                more = nextu < nunits;
+                nextst = nst > gridDim.x ? gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nst;
+                more = nextst < nst;
                 if (more) {
-                    nun = st_unit<SEGS>(T, nextu);
-                    issue_seg(nun.st, nun.g0);
-                    load_halo(nun.st, nun.g0);
+                    issue_seg(nextst, 0);
+                    load_halo(nextst);
                 }
             }
             // ---- roll segment g: positions 0..63 drop Pd, later ones this segment's own pairs
@@ -1154,7 +1100,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                     }
                 }
             }
-            if (g + 1 == un.g1) {                                    // the unit's tiles are complete: publish
+            if (g + 1 == (uint32_t)SEGS) {                           // the ST's tiles are complete: publish
                 if (__builtin_expect(__ballot(dmark != 0u) != 0ull, 0)) {   // tiles with unrecorded dirty groups
                     uint32_t m = 0;
 #pragma unroll
@@ -1172,12 +1118,8 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                     const uint32_t c = __builtin_amdgcn_readfirstlane(
                         __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)&tcnt[t], __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WAVEFRONT));
-                    if (un.part == ~0u)
-                        publish_list(T, tile, tlist + t * LC, c & 0x7fffffffu, lane, (c >> 31) != 0u,
-                                     dslots_alloc, (uint32_t)LC);
-                    else
-                        publish_part(T, tile, tlist + t * LC, c & 0x7fffffffu, lane, (c >> 31) != 0u,
-                                     un.part, dslots_alloc, (uint32_t)LC);
+                    publish_list(T, tile, tlist + t * LC, c & 0x7fffffffu, lane, (c >> 31) != 0u,
+                                 dslots_alloc, (uint32_t)LC);
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -1197,17 +1139,8 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 return;
             }
         }
-        un = nun;
-        st = un.st;
+        st = nextst;
         ++nth;
-        if (P.st_prio && nextu + gridDim.x >= nunits) {
-            // the last round: the later a wave took its unit, the more of it is left when
-            // the others finish -- it gets the SIMD's issue slots first (dev A/B)
-            const uint32_t r = (nextu + gridDim.x - nunits) * 3u / gridDim.x;   // 0 .. 2
-            if (r >= 2u) __builtin_amdgcn_s_setprio(3);
-            else if (r == 1u) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(1);
-        }
 #ifdef SYNCR_CDC_DEV
         ++nst_done;
 #endif
@@ -2250,48 +2183,15 @@ __device__ __forceinline__ uint64_t word_prefix(const Tables &T, uint32_t w, int
     return readlane64(wave_sum64(a), 0);
 }
 
-// A nonempty tile's candidate count for the compaction, its tile_meta (DENSE_BIT |
-// dense index, else 0 or the count) and, for a tile of the stream-tile scan's split
-// last round (not sent to the dense pass), its tail_meta word (else 0).
-__device__ __forceinline__ uint32_t tile_cands(const Tables &T, uint32_t tile, uint32_t &meta, uint32_t &tm) {
-    tm = 0u;
-    if (tile >= T.tail_tile0) {
-        const uint32_t w = T.tail_meta[tile - T.tail_tile0];
-        if (!(w & TAIL_DENSE)) {
-            uint32_t c = 0;
-            for (uint32_t q = 0; q < T.st_parts; ++q) c += tail_part_count(w, q);
-            meta = 0u;
-            tm = w;
-            return c;
-        }
-    }
+// A nonempty tile's candidate count for the compaction and its tile_meta (DENSE_BIT |
+// dense index, else 0 or the count).
+__device__ __forceinline__ uint32_t tile_cands(const Tables &T, uint32_t tile, uint32_t &meta) {
     meta = T.tile_meta[tile];
     if (meta & DENSE_BIT) {
         const uint32_t idx = meta & ~DENSE_BIT;
         return (!T.dense_off && idx < T.dense_cap) ? T.dense_cnt[idx] & ~DENSE_FIXED : 0u;
     }
     return meta;
-}
-
-// The candidates of a split tile in position order: each part's list is sorted,
-// so an element's rank is its index plus the elements of the other parts below it.
-__device__ __forceinline__ void copy_split_tile(const Tables &T, uint32_t tile, uint32_t tm, uint64_t base) {
-    const uint32_t ss = (uint32_t)LISTCAP / T.st_parts;
-    const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
-    const uint64_t t0 = (uint64_t)tile * T.tile;
-    for (uint32_t p = 0; p < T.st_parts; ++p) {
-        const uint32_t np = tail_part_count(tm, p);
-        for (uint32_t i = 0; i < np; ++i) {
-            const uint32_t e = sl[p * ss + i].x;
-            uint32_t rank = i;
-            for (uint32_t q = 0; q < T.st_parts; ++q) {
-                if (q == p) continue;
-                const uint32_t nq = tail_part_count(tm, q);
-                for (uint32_t j = 0; j < nq; ++j) rank += sl[q * ss + j].x < e;
-            }
-            T.cand[base + rank] = t0 + e;
-        }
-    }
 }
 
 // Dense tiles are expanded by the blocks past the word blocks, one wave per
@@ -2310,8 +2210,8 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
         const uint32_t tl = w * 64 + (uint32_t)lane;
         uint32_t c = 0;
         if ((bits >> lane) & 1ull) {
-            uint32_t meta, tm;
-            c = tile_cands(T, tl, meta, tm);
+            uint32_t meta;
+            c = tile_cands(T, tl, meta);
         }
         const uint32_t incl = wave_incl_scan(c, lane);
         const uint32_t j = tile & 63u;
@@ -2370,19 +2270,15 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
     if (!bits) return;
     const uint32_t tile = w * 64 + lane;
     const bool has = (bits >> lane) & 1ull;
-    uint32_t meta = 0, c = 0, tm = 0;
-    if (has) c = tile_cands(T, tile, meta, tm);
+    uint32_t meta = 0, c = 0;
+    if (has) c = tile_cands(T, tile, meta);
     const uint32_t incl = wave_incl_scan(c, lane);
     const uint64_t base = pre + (incl - c);
     const bool dense = has && (meta & DENSE_BIT) && c;
     if (has && c && !dense && base + c <= T.cand_cap) {   // overflow is flagged by prefix; host re-runs
-        if (__builtin_expect(tm != 0u, 0)) {
-            copy_split_tile(T, tile, tm, base);               // parts of a split ST: merge
-        } else {
-            const uint64_t t0 = (uint64_t)tile * T.tile;
-            const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
-            for (uint32_t j = 0; j < c; ++j) T.cand[base + j] = t0 + sl[j].x;    // fix-up: cdc_fix_kernel
-        }
+        const uint64_t t0 = (uint64_t)tile * T.tile;
+        const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
+        for (uint32_t j = 0; j < c; ++j) T.cand[base + j] = t0 + sl[j].x;    // fix-up: cdc_fix_kernel
     }
     (void)dense;                                               // dense tiles: gather_dense
 }
@@ -2444,8 +2340,8 @@ __global__ __launch_bounds__(256) void cdc_gather_fix_kernel(const uint8_t *__re
     if (!bits) return;
     const uint32_t tile = w * 64 + (uint32_t)lane;
     const bool has = (bits >> lane) & 1ull;
-    uint32_t meta = 0, c = 0, tm = 0;
-    if (has) c = tile_cands(T, tile, meta, tm);              // (dense_off: a dense tile counts 0; fetch re-runs)
+    uint32_t meta = 0, c = 0;
+    if (has) c = tile_cands(T, tile, meta);                  // (dense_off: a dense tile counts 0; fetch re-runs)
     if (meta & DENSE_BIT) c = 0u;
     const uint32_t incl = wave_incl_scan(c, lane);
     const uint32_t ctot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -2453,30 +2349,12 @@ __global__ __launch_bounds__(256) void cdc_gather_fix_kernel(const uint8_t *__re
     const uint64_t wbase = (uint64_t)w * 64u * T.tile;
     const uint32_t trel = (uint32_t)lane * T.tile;           // this tile's offset in the word
     const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
-    const uint32_t ss = (uint32_t)LISTCAP / T.st_parts;
     for (uint32_t k0 = 0; k0 < ctot; k0 += 128) {
         // stage positions k0 .. k0 + 127 of the word's ordered candidates
         if (c && b0 < k0 + 128 && b0 + c > k0) {
-            if (!tm) {
-                for (uint32_t j = 0; j < c; ++j) {
-                    const uint32_t i = b0 + j;
-                    if (i >= k0 && i < k0 + 128) lpos[wv][i - k0] = trel + sl[j].x;
-                }
-            } else {                                          // a split ST's tile: merge its parts
-                for (uint32_t p = 0; p < T.st_parts; ++p) {
-                    const uint32_t np = tail_part_count(tm, p);
-                    for (uint32_t j = 0; j < np; ++j) {
-                        const uint32_t e = sl[p * ss + j].x;
-                        uint32_t rank = j;
-                        for (uint32_t q = 0; q < T.st_parts; ++q) {
-                            if (q == p) continue;
-                            const uint32_t nq = tail_part_count(tm, q);
-                            for (uint32_t m = 0; m < nq; ++m) rank += sl[q * ss + m].x < e;
-                        }
-                        const uint32_t i = b0 + rank;
-                        if (i >= k0 && i < k0 + 128) lpos[wv][i - k0] = trel + e;
-                    }
-                }
+            for (uint32_t j = 0; j < c; ++j) {
+                const uint32_t i = b0 + j;
+                if (i >= k0 && i < k0 + 128) lpos[wv][i - k0] = trel + sl[j].x;
             }
         }
         __builtin_amdgcn_wave_barrier();
