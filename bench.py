@@ -138,9 +138,12 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
     return rc
 
 
-def load_traffic(workload_name: str, span: int, run_bytes: int, kernel: str = "cdc::cdc_scan_kernel"):
+def load_traffic(workload_name: str, span: int, run_bytes: int, kernel: str = "cdc::cdc_scan_kernel",
+                 st_segments: int | None = None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    of the same workload, span and scan geometry (profiles/*_pmc_traffic.json)."""
+    of the same workload, span and scan geometry (profiles/*_pmc_traffic.json);
+    for the stream-tile scan also the same segments per stream (summaries
+    without the key were measured with 9)."""
     import glob
     import re
 
@@ -157,7 +160,8 @@ def load_traffic(workload_name: str, span: int, run_bytes: int, kernel: str = "c
         dk = d.get("kernel", "cdc::cdc_scan_kernel")     # the summary's main kernel
         if (d.get("workload") == workload_name and int(d.get("span", -1)) == span
                 and d.get("run_bytes") == run_bytes
-                and (kernel == dk or kernel in d.get("per_kernel_hbm_bytes", {}))):
+                and (kernel == dk or kernel in d.get("per_kernel_hbm_bytes", {}))
+                and (not st_segments or kernel != dk or int(d.get("st_segments") or 9) == st_segments)):
             best = dict(d)
             best["hbm_bytes_per_launch"] = (d["hbm_bytes_per_launch"] if kernel == dk
                                             else d["per_kernel_hbm_bytes"][kernel])
@@ -577,7 +581,8 @@ def main(argv=None):
     scan_ms = kms[0] / max(nl, 1)
     achieved = span / (scan_ms / 1e3) / 1e9 if scan_ms > 0 else 0.0
     scan_kernel = scan_info["kernel"]           # syncr_cdc_last_scan of the last timed launch
-    tr = load_traffic(args.workload, span, engine_info["run_bytes"], kernel="cdc::" + scan_kernel)
+    tr = load_traffic(args.workload, span, engine_info["run_bytes"], kernel="cdc::" + scan_kernel,
+                      st_segments=scan_info.get("st_segments"))
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),

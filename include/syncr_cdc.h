@@ -333,11 +333,10 @@ int32_t syncr_cdc_fetch_reruns(syncr_cdc *h, uint64_t *reruns);
  * launch from the batch size and the handle's history; a capacity re-run inside
  * fetch counts as a launch).  kind: one of SYNCR_CDC_SCAN_*; info4 (may be NULL) =
  * [kind, tiles, scan waves launched, segments per stream of a stream-tile scan
- * (9 or 27; 0 for the other scans)]; *name (may be NULL) = the kernel's symbol
+ * (9; 0 for the other scans)]; *name (may be NULL) = the kernel's symbol
  * name as a profiler shows it. */
 #define SYNCR_CDC_SCAN_NONE 0         /* no launch yet, or an empty batch             */
-#define SYNCR_CDC_SCAN_STREAM_TILES 1 /* cdc_scan_st_kernel: batches >= 24 tiles/wave
-                                         (27-segment streams from 96)                  */
+#define SYNCR_CDC_SCAN_STREAM_TILES 1 /* cdc_scan_st_kernel: batches >= 24 tiles/wave  */
 #define SYNCR_CDC_SCAN_CU 2           /* cdc_scan_kernel, CU schedule: small batches  */
 #define SYNCR_CDC_SCAN_TILES 3        /* cdc_scan_kernel, dynamic tile groups: large
                                          batches after a >= 1 % dense-tile batch      */

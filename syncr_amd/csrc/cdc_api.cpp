@@ -492,7 +492,7 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     // an event record costs ~6 us of queue idle: the scan-only mode has only the
     // two bound to the scan dispatch (no markers); the phase mode adds markers
     const bool phases = events && !h->timing_scan_only;
-    CHECK_HIP(launch_post(d_bytes, kp, t, s, scan_dense_inline(h->geom, kp)));
+    CHECK_HIP(launch_post(d_bytes, kp, t, s, scan_dense_inline(h->geom, kp), h->scan_grid));
     h->last_dense_off = t.dense_off != 0u;
     if (phases) CHECK_HIP(hipEventRecord(pt.ev[2], s));
     CHECK_HIP(launch_resolve(d_bytes, kp, t, s));

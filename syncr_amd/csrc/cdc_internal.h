@@ -76,15 +76,14 @@ __host__ __device__ constexpr int scan_lds_for_run(int run) {
 
 // ---- stream-tile scan (cdc_scan_st_kernel) --------------------------------
 // A stream tile (ST) is ST_TILES consecutive batch tiles cut into 128 streams
-// of ST_SEGS segments (27 from ST27_MIN_TILES_PER_WAVE tiles per scan wave:
-// st_segs()), handed out whole from a counter.  (Round 5 measured handing the
+// of ST_SEGS segments (st_segs(); 18 / 27 / 36 in the dev library), handed out
+// whole from a counter.  (Round 5 measured handing the
 // batch's last round out in segment-range parts, to end the waves closer
 // together, and a raised issue priority for the last round's late waves: both
 // null or slower -- DESIGN.md §4.1 -- and removed, with the extra branches and
 // runtime loop bounds they put in the hot loop.)
 constexpr int ST_TILES = 8;                   // batch tiles per ST
 constexpr int ST_SEGS = 9;                    // segments per stream
-constexpr uint32_t ST27_MIN_TILES_PER_WAVE = 96;   // 27-segment streams from this many tiles per wave
 
 // ctr[] words (zeroed by the per-launch memset)
 enum { CTR_DENSE = 0, CTR_FLAGS = 1, CTR_CANDS_LO = 2, CTR_CANDS_HI = 3 };
@@ -339,7 +338,8 @@ bool scan_dense_inline(ScanGeom g, const KParams &p);      // the scan passes de
 // the one decision, reported through syncr_cdc_last_scan so callers never restate it.
 int scan_kind(ScanGeom g, uint32_t grid, const KParams &p, const Tables &t);
 int st_segs(uint32_t grid, const KParams &p, const Tables &t);   // stream-tile geometry of a launch
-hipError_t launch_post(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s, bool dense_inline);
+hipError_t launch_post(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s, bool dense_inline,
+                       uint32_t scan_grid);
 hipError_t launch_resolve(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s);
 bool resolve_splits(const KParams &p, const Tables &t);   // launch_resolve starts split workers
 hipError_t launch_gen(uint8_t *d_base, const uint64_t *d_foff, const uint64_t *d_flen,

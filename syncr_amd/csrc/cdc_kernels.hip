@@ -3695,18 +3695,22 @@ hipError_t launch_read_probe(const uint8_t *d, uint64_t bytes, bool nt, uint32_t
 constexpr int SCAN_CU_WAVES = 8;
 // The stream-tile scan with the geometry st_segs() picks for this launch.
 static void launch_st(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    const int segs = st_segs(grid, p, t);
-    if (segs == 27)
-        hipLaunchKernelGGL((cdc_scan_st_kernel<4, 27>), dim3(grid), dim3(64), st_lds_bytes(27), s, d, p, t);
 #ifdef SYNCR_CDC_DEV
-    else if (segs == 18)
+    switch (st_segs(grid, p, t)) {
+    case 18:
         hipLaunchKernelGGL((cdc_scan_st_kernel<4, 18>), dim3(grid), dim3(64), st_lds_bytes(18), s, d, p, t);
-    else if (segs == 36)
+        return;
+    case 27:
+        hipLaunchKernelGGL((cdc_scan_st_kernel<4, 27>), dim3(grid), dim3(64), st_lds_bytes(27), s, d, p, t);
+        return;
+    case 36:
         hipLaunchKernelGGL((cdc_scan_st_kernel<4, 36>), dim3(grid), dim3(64), st_lds_bytes(36), s, d, p, t);
+        return;
+    default:
+        break;
+    }
 #endif
-    else
-        hipLaunchKernelGGL((cdc_scan_st_kernel<4, ST_SEGS>), dim3(grid), dim3(64), st_lds_bytes(ST_SEGS), s, d, p,
-                           t);
+    hipLaunchKernelGGL((cdc_scan_st_kernel<4, ST_SEGS>), dim3(grid), dim3(64), st_lds_bytes(ST_SEGS), s, d, p, t);
 }
 
 // The > 64 KB dynamic-LDS attribute is set once per (kernel instance, device), under
@@ -3921,21 +3925,24 @@ static hipError_t launch_scan_kernel(ScanGeom g, uint32_t grid, const uint8_t *d
 }
 #endif
 
-// Segments per stream of the stream-tile scan (see st_tiles): 27 (3456-byte
-// streams, 24-tile STs) from ST27_MIN_TILES_PER_WAVE tiles per scan wave, else 9.
-// Same-process A/B, scan ms, 9 / 18 / 27 / 36 segments (profiles/r05i_*): zipf10k
-// (277 tiles per wave) 1.734 / 1.712 / 1.704 / 1.721, config 4's N = 2 shard
-// (138) 0.933 / 0.923 / 0.921, N = 4 (69) 0.513 / 0.512, N = 8 (35) 0.269 / 0.272
-// (r05h), uniform1k (28) 0.228 / 0.243: longer streams read fewer halo lines and
-// switch STs less often, but their last grabs are coarser.  (The dev library's
-// KParams::st_segs forces one of 9 / 18 / 27 / 36.)
+// Segments per stream of the stream-tile scan (see st_tiles): 9 in the product.
+// Longer streams read fewer halo lines (27 segments: traffic 1.027x against
+// 1.07x, profiles/r05_v1_pmc_traffic.json) but ran slower once the hot loop lost
+// its split-round branches: same-process A/B in the driver's condition, zipf10k
+// scan 1.652 ms (9) vs 1.667 (27), and the sustained rate of round 4's 9-segment
+// code 6002-6030 GiB/s vs 5822-5847 with 27 on the same boxes
+// (profiles/r05_st_segments_ab.jsonl, r05_zipf10k_bisect_traces.json).  Small
+// batches lose more (coarser last grabs: uniform1k 0.228 / 0.243 ms at 9 / 18).
+// (The dev library's KParams::st_segs forces one of 9 / 18 / 27 / 36.)
 int st_segs(uint32_t grid, const KParams &p, const Tables &t) {
-    if (p.st_segs == 9u || p.st_segs == 27u) return (int)p.st_segs;
+    (void)grid;
+    (void)t;
 #ifdef SYNCR_CDC_DEV
-    if (p.st_segs == 18u || p.st_segs == 36u) return (int)p.st_segs;
+    if (p.st_segs == 18u || p.st_segs == 27u || p.st_segs == 36u) return (int)p.st_segs;
+#else
+    (void)p;
 #endif
-    grid = grid < t.ntiles ? grid : t.ntiles;
-    return (uint64_t)t.ntiles >= (uint64_t)grid * ST27_MIN_TILES_PER_WAVE ? 27 : ST_SEGS;
+    return ST_SEGS;
 }
 
 // The scan launch of do_launch; e0 / e1 (may be null): HIP events recorded around it.
@@ -3967,7 +3974,8 @@ int scan_blocks_per_cu(ScanGeom g) {
     return n > 0 ? n : 1;
 }
 
-hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s, bool dense_inline) {
+hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s, bool dense_inline,
+                       uint32_t scan_grid) {
     if (!t.ntiles) return hipSuccess;
     const uint32_t dblocks = t.dense_cap < 2048u ? (t.dense_cap ? t.dense_cap : 1u) : 2048u;
     if (dense_inline) {
@@ -3989,10 +3997,15 @@ hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipS
     // + up to 2048 blocks (one wave per dense tile) that expand dense tiles; they
     // exit at once when there are none.  (256 blocks left ~33 serial tile
     // expansions per wave on the dense workload: 0.2 ms.)
-    if (t.dense_off && !t.linkw && !dense_inline) {
-        // no dense pass, no chain links: compaction and fix-ups in one launch
-        const uint32_t gblocks = std::min<uint32_t>((t.ngrid + 511) / 512, 1024u);
-        hipLaunchKernelGGL(cdc_gather_fix_kernel, dim3((t.nwords + 3) / 4 + gblocks), dim3(256), 0, s, d, p, t);
+    // No dense pass, no chain links: compaction and fix-ups in one launch when its
+    // blocks fit one round on the device (4 per CU at its 119 VGPRs = scan_grid / 2).
+    // Past that each extra round repeats the word waves' chain of dependent loads: on
+    // zipf10k (2216 word blocks) it ran 26 us against 9.6 + 8.8 us for the two
+    // kernels (profiles/r05_zipf10k_bisect_traces.json).
+    const uint32_t gblocks = std::min<uint32_t>((t.ngrid + 511) / 512, 1024u);
+    const uint32_t fused_blocks = (t.nwords + 3) / 4 + gblocks;
+    if (t.dense_off && !t.linkw && !dense_inline && fused_blocks <= std::max(scan_grid / 2u, 1u)) {
+        hipLaunchKernelGGL(cdc_gather_fix_kernel, dim3(fused_blocks), dim3(256), 0, s, d, p, t);
         return hipGetLastError();
     }
     const uint32_t dgb = t.dense_off ? 0u : std::min<uint32_t>((t.dense_cap + 3) / 4, 2048u);

@@ -716,18 +716,14 @@ def test_small_batches_back_to_back_stable():
 # library's choice at these thresholds through syncr_cdc_last_scan (the host never restates it)
 SCAN_ST_MIN_TILES_PER_WAVE = 24
 SCAN_DYN_MIN_TILES_PER_WAVE = 96
-ST27_MIN_TILES_PER_WAVE = 96          # cdc_internal.h: 27-segment streams from here
 
-@pytest.mark.parametrize("per_wave,below", [(SCAN_ST_MIN_TILES_PER_WAVE, False), (SCAN_ST_MIN_TILES_PER_WAVE, True),
-                                            (ST27_MIN_TILES_PER_WAVE, False), (ST27_MIN_TILES_PER_WAVE, True)])
+@pytest.mark.parametrize("per_wave,below", [(SCAN_ST_MIN_TILES_PER_WAVE, False), (SCAN_ST_MIN_TILES_PER_WAVE, True)])
 def test_stream_tile_threshold_edge_vs_oracle(per_wave, below):
     """The scans either side of the library's thresholds (cdc_kernels.hip
     launch_scan / st_segs), as syncr_cdc_last_scan reports them: a batch of
     exactly grid x 24 tiles whose last tile holds one byte (stream tiles of
     9-segment streams; the batch's last stream tile is mostly past the span: the
-    clamped DMA path) and one tile less (the CU schedule); grid x 96 tiles
-    (27-segment streams, whose streams straddle batch tiles) and one less
-    (9-segment streams).  Random files with periodic-64 and constant ones at
+    clamped DMA path) and one tile less (the CU schedule).  Random files with periodic-64 and constant ones at
     chunk_bits 13: every file's cuts vs the oracle."""
     from benchlib.workloads import periodic_pattern
     bits, cap = 13, 256 << 10
@@ -748,11 +744,8 @@ def test_stream_tile_threshold_edge_vs_oracle(per_wave, below):
         offs = np.zeros_like(lens)
         offs[1:] = np.cumsum(lens)[:-1]
         assert int(lens.sum()) == span
-        if per_wave == SCAN_ST_MIN_TILES_PER_WAVE:
-            want, kind, segs = (("cdc_scan_kernel", "cu_schedule", 0) if below else
-                                ("cdc_scan_st_kernel", "stream_tiles", 9))
-        else:
-            want, kind, segs = "cdc_scan_st_kernel", "stream_tiles", (9 if below else 27)
+        want, kind, segs = (("cdc_scan_kernel", "cu_schedule", 0) if below else
+                            ("cdc_scan_st_kernel", "stream_tiles", 9))
         buf = syncr_amd.DeviceBuffer(ch, span)
         try:
             buf.gen_corpus(offs, lens, indices=np.arange(lens.size, dtype=np.uint64) + 7001)
@@ -811,7 +804,7 @@ def test_large_batch_stream_tiles_vs_oracle(bits, cap):
             ch.plan(offs, lens, span)
             ch.launch(buf.ptr)
             res = ch.fetch()
-            assert ch.last_scan()["kind"] == "stream_tiles" and ch.last_scan()["st_segments"] == 27, ch.last_scan()
+            assert ch.last_scan()["kind"] == "stream_tiles" and ch.last_scan()["st_segments"] == 9, ch.last_scan()
             host = buf.download(span)
             print(f"stream-tile batch: {lens.size} files, {span / 2**30:.2f} GiB chunked; oracle next", flush=True)
         finally:

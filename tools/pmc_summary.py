@@ -110,6 +110,8 @@ def main(tag, src=None):
     kernels = sorted({kk[0] for kk in f})
     out = {
         "kernel": k, "workload": fb.get("config", {}).get("workload", "").split(":")[0],
+        # the stream-tile geometry the library reported for the headline launches
+        "st_segments": (fb.get("roofline", {}).get("scan_schedule") or {}).get("st_segments"),
         "run_bytes": fb.get("config", {}).get("engine", {}).get("run_bytes"),
         "span": span, "read_bytes": int(read_b), "write_size_kib": write_kib,
         "hbm_bytes_per_launch": int(scan_hbm), "algorithmic_bytes_per_launch": span,
