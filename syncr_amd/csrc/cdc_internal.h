@@ -277,7 +277,8 @@ enum { DBG_RES_START = 0, DBG_RES_END = 1, DBG_W_ENTRY = 2, DBG_W_SETUP = 3, DBG
        DBG_W_BLK = 8, DBG_MAXBLK = 120, DBG_COPY_START = 248, DBG_COPY_END = 249, DBG_REC = 256,
        DBG_NREC = 1024, DBG_FW = DBG_REC + 2 * DBG_NREC, DBG_NFW = 1024, DBG_SCAN = DBG_FW + DBG_NFW,
        DBG_SCAN_N = 4096, DBG_TILE = DBG_SCAN + 4 * DBG_SCAN_N, DBG_TILE_W = 16, DBG_TILE_N = 128,
-       DBG_WORDS = DBG_TILE + DBG_TILE_W * DBG_TILE_N };
+       DBG_CW = DBG_TILE + DBG_TILE_W * DBG_TILE_N, DBG_NCW = 4096,   // split copy waves: end, cuts (p1 << 32 | p2)
+       DBG_WORDS = DBG_CW + 2 * DBG_NCW };
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------
 // A lane TASK is B3_LANE_LEAVES consecutive 1 KiB leaves of one chunk.  A chunk

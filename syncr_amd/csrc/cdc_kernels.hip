@@ -3468,6 +3468,9 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
     const uint32_t nruns = T.runs_cap ? min(T.split[SPL_RUNS], T.runs_cap) : 0u;
     if (nsplit == 0u && nruns == 0u) return;                  // nothing split or deferred
     if (blockIdx.x == 0 && threadIdx.x < 64) DBG_STAMP(T, DBG_COPY_START);
+#ifdef SYNCR_CDC_DEV
+    uint64_t dbg_c1 = 0, dbg_c2 = 0;                          // cuts this wave copied / expanded
+#endif
     const uint32_t nrec = nsplit ? min(T.split[SPL_RESERVED], T.seg_cap) : 0u;
     // several waves per record / run (up to 3 x 4096 cuts: one wave each left
     // most of the grid idle and each wave latency-bound)
@@ -3484,6 +3487,9 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
         const uint64_t a = (uint64_t)part * per, e = min(n, a + per);
         const DevCut *src = T.seg_cuts + (uint64_t)q * T.seg_scap;
         DevCut *dst = T.cuts + T.cut_base[i];
+#ifdef SYNCR_CDC_DEV
+        dbg_c1 += e > a ? e - a : 0u;
+#endif
         for (uint64_t t = a + (uint64_t)lane; t < e; t += 64u * U1) {
             DevCut v[U1];
 #pragma unroll
@@ -3511,6 +3517,9 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
         const uint64_t a = (uint64_t)part * per, e = min((uint64_t)j.n, a + per);
         DevCut *dst = T.cuts + T.cut_base[i] + rel;
         const uint64_t lim = cap > rel ? cap - rel : 0ull;
+#ifdef SYNCR_CDC_DEV
+        dbg_c2 += e > a ? e - a : 0u;
+#endif
         // one load per cut: the previous candidate comes from the lane before
         // (DPP) or the previous 64 (readlane); eight 64-candidate blocks in flight
         constexpr int U = 8;
@@ -3537,6 +3546,12 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
             }
         }
     }
+#ifdef SYNCR_CDC_DEV
+    if (wid < (uint32_t)DBG_NCW) {
+        SCAN_STAMP(T, DBG_CW + 2 * wid, wall_clock64());
+        SCAN_STAMP(T, DBG_CW + 2 * wid + 1, (dbg_c1 << 32) | dbg_c2);
+    }
+#endif
 }
 
 // One wave per file; files below 4 GiB walk in 32-bit offsets.  Blocks past

@@ -13,6 +13,7 @@
 #   ab|<workload>|<rounds>|<V1>|<V2>... tools/dip_ab.py variants (dev library) in the driver's condition
 #   trace|<workload>[|<shard>[|--no-events[|<checkout>]]]  kernel trace of one small-batch leg
 #                                       (tools/legs_trace.py, product; <checkout>: e.g. build/r04src)
+#   pmc|<workload>|<counters>          one rocprofv3 --pmc pass over a legs_trace.py leg (per-kernel means)
 #   sttrace|<workload>|<ENV=V,...>      per-wave stream-tile scan timeline (tools/scan_timeline.py, dev)
 #   restl|<workload>                    resolve timeline (tools/resolve_timeline.py, dev library)
 #   prof|<PROFTAG>[|<extra flags>[|<ENV=V,...>]]  tools/prof.sh: trace + traffic + SQ passes of the driver's
@@ -80,6 +81,14 @@ PY
         f=$(find "$P" -name '*kernel_trace.csv' | head -1)
         nb=$(python3 -c "import json;print(json.loads(open('$P/leg.json').read().strip().splitlines()[-1])['bytes'])")
         python3 tools/legs_trace_show.py "$f" 20 5 "$nb" > "$P/steps.json" && cat "$P/steps.json" | head -30 ;;
+    pmc)                                         # pmc|<workload>|<counters, space-separated>: one PMC pass
+        P=$O/${TAG}_${n}_pmc_${a[1]}
+        mkdir -p "$P"
+        ( cd /tmp && timeout -s KILL 120 rocprofv3 --pmc ${a[2]} --output-format csv -d "$P" -o run -- \
+            python3 "$R/tools/legs_trace.py" --workload "${a[1]}" --steps 5 --warmup 2 > "$P/leg.json" 2> "$P/leg.err" ) \
+            || { echo "pmc failed rc=$?"; tail -20 "$P/leg.err"; exit 21; }
+        f=$(find "$P" -name '*counter_collection.csv' | head -1)
+        python3 tools/pmc_kernels.py "$f" > "$P/kernels.json" && cat "$P/kernels.json" ;;
     sttrace)
         envrun "${a[2]}" timeout -k 10 300 python -u tools/scan_timeline.py --workload "${a[1]}" > "$out.json" 2> "$out.err" \
             || { echo "sttrace failed rc=$?"; tail -20 "$out.err"; exit 17; }

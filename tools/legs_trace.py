@@ -5,7 +5,7 @@ bench.py's leg timing (benchlib/legs.py time_steps: 1 launch + fetch, W-1
 launches, K timed launches, 5 phase-timed launches).  tools/legs_trace_show.py
 turns the trace into where each timed step's time goes.
 
-    python tools/legs_trace.py --workload uniform1k|shard8 [--shard R] [--steps K] [--warmup W]
+    python tools/legs_trace.py --workload uniform1k|shard8|zipf10k|dense|dense1 [--shard R] [--steps K] [--warmup W]
 """
 import argparse
 import json
@@ -24,7 +24,7 @@ from benchlib import workloads as WL  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="uniform1k", choices=["uniform1k", "shard8", "zipf10k"])
+    ap.add_argument("--workload", default="uniform1k", choices=["uniform1k", "shard8", "zipf10k", "dense", "dense1"])
     ap.add_argument("--shard", type=int, default=0)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
@@ -37,14 +37,21 @@ def main():
     elif args.workload == "shard8":
         sh = WL.lpt_shard(sizes, 8)[args.shard]
         lens, idx = sizes[sh], sh.astype(np.uint64)
-    else:
+    elif args.workload == "dense1":                # one 128 MiB periodic-64 file (bench dense1 leg)
+        lens, idx = np.full(1, WL.DENSE1_BYTES, np.uint64), np.zeros(1, np.uint64)
+    else:                                          # zipf10k / dense: the config-3 file table
         lens, idx = sizes, np.arange(sizes.size, dtype=np.uint64)
     offs = WL.offsets_of(lens)
     span = int(lens.sum())
     with syncr_amd.Chunker() as ch:
         b = syncr_amd.DeviceBuffer(ch, span)
         try:
-            b.gen_corpus(offs, lens, indices=idx)
+            if args.workload == "dense1":
+                b.upload(np.resize(WL.periodic_pattern(), span))
+            else:
+                b.gen_corpus(offs, lens, indices=idx)
+                if args.workload == "dense":
+                    L.fill_dense(b, offs, lens, idx)
             ch.plan(offs, lens, span)
             if args.no_events:
                 import time

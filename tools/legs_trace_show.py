@@ -40,7 +40,9 @@ def main():
             gap[f"{a[0]} -> {b[0]}"].append((b[1] - a[2]) / 1e3)
         for name, s, e in st:
             dur[name].append((e - s) / 1e3)
-        nxt = steps[W + j + 1][0][1] if W + j + 1 < len(steps) else None
+        # the next step inside the window only: the window's last launch is followed by the
+        # host's synchronize (and the phase-timed launches), not by a timed step
+        nxt = steps[W + j + 1][0][1] if j + 1 < len(window) else None
         if nxt:
             period.append((nxt - t0) / 1e3)
             gap["last -> next scan"].append((nxt - st[-1][2]) / 1e3)

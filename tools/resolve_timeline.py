@@ -27,7 +27,9 @@ syncr_amd.use_dev_library()
 DBG_RES_START, DBG_RES_END, DBG_W_ENTRY, DBG_W_SETUP, DBG_W_END, DBG_W_NBLK = 0, 1, 2, 3, 4, 5
 DBG_W_BLK, DBG_COPY_START, DBG_COPY_END, DBG_REC, DBG_NREC = 8, 248, 249, 256, 1024
 DBG_FW, DBG_NFW = DBG_REC + 2 * DBG_NREC, 1024
-WORDS = DBG_FW + DBG_NFW
+DBG_SCAN = DBG_FW + DBG_NFW
+DBG_CW, DBG_NCW = DBG_SCAN + 4 * 4096 + 16 * 128, 4096      # split copy waves: end, cuts (p1 << 32 | p2)
+WORDS = DBG_CW + 2 * DBG_NCW
 
 
 def main():
@@ -86,6 +88,16 @@ def main():
             print(f"  worker walks ({have.sum()}): start min {st.min():.1f} med {np.median(st):.1f} "
                   f"max {st.max():.1f}; end max {en.max():.1f}; duration med {np.median(dur):.1f} max {dur.max():.1f}")
         print(f"  copy start {us(d[DBG_COPY_START])}")
+        cw = d[DBG_CW:DBG_CW + 2 * DBG_NCW].reshape(-1, 2)
+        live = cw[:, 0] > 0
+        if live.any():
+            ce = np.array([us(v) for v in cw[live, 0]])
+            c1, c2 = (cw[live, 1] >> np.uint64(32)).astype(np.int64), (cw[live, 1] & np.uint64(0xffffffff)).astype(np.int64)
+            wid = np.nonzero(live)[0]
+            top = np.argsort(-ce)[:6]
+            print(f"  copy wave ends ({live.sum()}): p50 {np.percentile(ce, 50):.1f} p90 {np.percentile(ce, 90):.1f} "
+                  f"max {ce.max():.1f}; cuts copied {int(c1.sum())} expanded {int(c2.sum())}; busiest waves "
+                  + ", ".join(f"w{int(wid[k])}:{ce[k]:.1f}us/{int(c1[k])}+{int(c2[k])}" for k in top))
         fw = d[DBG_FW:DBG_FW + DBG_NFW]
         ends = sorted(((us(v), k) for k, v in enumerate(fw) if v), reverse=True)[:6]
         order = np.argsort(-sizes.astype(np.int64), kind="stable")
