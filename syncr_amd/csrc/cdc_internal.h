@@ -127,6 +127,8 @@ struct KParams {
     uint32_t resolve_pf;       // development library only (SYNCR_CDC_RESOLVE_PF): candidate windows
                                //   the resolve walk loads ahead (0: RESOLVE_PF)
     uint32_t st_segs;          // (dev A/B: SYNCR_CDC_ST_SEGS) 9 / 18 / 27 / 36 segments per stream forced; 0: st_segs()
+    uint32_t nt_out;           // 1: candidate words and cuts are stored non-temporally (dev A/B:
+                               //   SYNCR_CDC_NT_OUT=1; product 0); Tables::nt_out carries it to the kernels
 };
 constexpr int RESOLVE_PF = 8;  // product: candidate windows in the resolve walk's LDS ring (PF-1 ahead)
 
@@ -260,6 +262,7 @@ struct Tables {
     uint64_t *dbg;                 // development library only (SYNCR_CDC_TRACE=1): [DBG_WORDS] resolve
                                    //   timeline (wall_clock64 stamps, DBG_*), else nullptr
     uint32_t nst;                  // stream-tile scan: STs of the batch (launch geometry)
+    uint32_t nt_out;               // KParams::nt_out: non-temporal stores of candidate words and cuts
     // scan timing by the device clock (syncr_cdc_set_timing mode 2; null: off): the scan's
     // waves stamp wall_clock64 -- tscan[0] = ~0 - the earliest entry, tscan[1] = the
     // latest exit (atomic max, zeroed per launch) -- and the resolve adds exit - entry
@@ -277,7 +280,7 @@ enum { DBG_RES_START = 0, DBG_RES_END = 1, DBG_W_ENTRY = 2, DBG_W_SETUP = 3, DBG
        DBG_W_BLK = 8, DBG_MAXBLK = 120, DBG_COPY_START = 248, DBG_COPY_END = 249, DBG_REC = 256,
        DBG_NREC = 1024, DBG_FW = DBG_REC + 2 * DBG_NREC, DBG_NFW = 1024, DBG_SCAN = DBG_FW + DBG_NFW,
        DBG_SCAN_N = 4096, DBG_TILE = DBG_SCAN + 4 * DBG_SCAN_N, DBG_TILE_W = 16, DBG_TILE_N = 128,
-       DBG_CW = DBG_TILE + DBG_TILE_W * DBG_TILE_N, DBG_NCW = 4096,   // split copy waves: end, cuts (p1 << 32 | p2)
+       DBG_CW = DBG_TILE + DBG_TILE_W * DBG_TILE_N, DBG_NCW = 4096,   // split copy waves: end, start
        DBG_WORDS = DBG_CW + 2 * DBG_NCW };
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------

@@ -45,6 +45,27 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 }
 
 // Whole-wave shifts by one lane as DPP moves (wave_shr:1 / wave_shl:1), not
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Output stores of candidate words and cuts; nt (Tables::nt_out, dev A/B
+// SYNCR_CDC_NT_OUT=1): non-temporal.  Nothing re-reads them through this XCD's
+// L2 before the end-of-kernel release, so streaming them past it looked free; the
+// same-process A/B (order alternated, 8 rounds) says otherwise: dense1 0.2099 vs
+// 0.2145 ms per step, dense 2.099 vs 2.090, shard8 / uniform1k within noise
+// (profiles/r05_nt_stores_ab.jsonl).  The product stores plainly.
+__device__ __forceinline__ void st_u64(uint64_t *p, uint64_t v, uint32_t nt) {
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ void st_cut(DevCut *p, const DevCut &v, uint32_t nt) {
+    if (nt) {
+        const u32x4 w = {(uint32_t)v.offset, (uint32_t)(v.offset >> 32), v.len, v.file};
+        __builtin_nontemporal_store(w, (u32x4 *)p);
+    } else {
+        *p = v;
+    }
+}
+
 // ds_bpermute round trips through the LDS unit: lane l gets lane l-1's value
 // (up1; lane 0 gets 0) or lane l+1's (down1; lane 63 gets 0).  All lanes active.
 __device__ __forceinline__ uint32_t up1(uint32_t v) {
@@ -1742,7 +1763,7 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
         for (int h = 0; h < 2; ++h) {
             const uint64_t i = 2 * q + (uint64_t)h;
             const uint32_t f = h ? fB : fA;
-            if (i < n) T.cand[i] = ((h ? aB : aA) - 1) | ((uint64_t)f << 48) | CAND_KNOWN | ((h ? lB : lA) ? CAND_LINK : 0ull);
+            if (i < n) st_u64(&T.cand[i], ((h ? aB : aA) - 1) | ((uint64_t)f << 48) | CAND_KNOWN | ((h ? lB : lA) ? CAND_LINK : 0ull), T.nt_out);
             else if (i < items) T.gfix[i - n] = (uint8_t)f;
         }
         // the wave's 128 consecutive candidates (lane l: 2l, 2l+1) as two link words
@@ -2225,7 +2246,7 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
             const uint16_t *ps = T.dense_pos + (size_t)idx * FIXCAP;
             const uint8_t *fx = T.dense_fix + (size_t)idx * FIXCAP;
             for (uint32_t r = (uint32_t)lane; r < tc; r += 64)
-                T.cand[tb + r] = (t0 + ps[r]) | ((uint64_t)fx[r] << 48) | CAND_KNOWN;
+                st_u64(&T.cand[tb + r], (t0 + ps[r]) | ((uint64_t)fx[r] << 48) | CAND_KNOWN, T.nt_out);
             continue;
         }
         uint64_t o = tb;
@@ -2236,7 +2257,7 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
             const uint32_t ic = wave_incl_scan(pc, lane);
             uint64_t q = o + (ic - pc);
             while (m) {
-                T.cand[q++] = t0 + wi * 32u + (uint32_t)__builtin_ctz(m);
+                st_u64(&T.cand[q++], t0 + wi * 32u + (uint32_t)__builtin_ctz(m), T.nt_out);
                 m &= m - 1;
             }
             o += (uint32_t)__builtin_amdgcn_readlane((int)ic, 63);
@@ -2278,7 +2299,7 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
     if (has && c && !dense && base + c <= T.cand_cap) {   // overflow is flagged by prefix; host re-runs
         const uint64_t t0 = (uint64_t)tile * T.tile;
         const uint2 *sl = T.slots + (size_t)tile * LISTCAP;
-        for (uint32_t j = 0; j < c; ++j) T.cand[base + j] = t0 + sl[j].x;    // fix-up: cdc_fix_kernel
+        for (uint32_t j = 0; j < c; ++j) st_u64(&T.cand[base + j], t0 + sl[j].x, T.nt_out);   // fix-up: cdc_fix_kernel
     }
     (void)dense;                                               // dense tiles: gather_dense
 }
@@ -2381,7 +2402,7 @@ __global__ __launch_bounds__(256) void cdc_gather_fix_kernel(const uint8_t *__re
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint64_t o = pre + k0 + 2u * (uint32_t)lane + (uint32_t)h;
-            if (in[h] && o < T.cand_cap) T.cand[o] = (a[h] - 1) | ((uint64_t)(h ? fB : fA) << 48) | CAND_KNOWN;
+            if (in[h] && o < T.cand_cap) st_u64(&T.cand[o], (a[h] - 1) | ((uint64_t)(h ? fB : fA) << 48) | CAND_KNOWN, T.nt_out);
         }
         __builtin_amdgcn_wave_barrier();                       // (the staging is reused)
     }
@@ -2486,7 +2507,7 @@ __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restri
             d.offset = s;
             d.len = (uint32_t)(cut - s);
             d.file = i;
-            out[cnt] = d;
+            st_cut(out + cnt, d, T.nt_out);
         }
         ++cnt;
         s = cut;                                          // copy_within :771
@@ -2806,7 +2827,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
             d.offset = (uint64_t)bo;
             d.len = bl;
             d.file = i;
-            out[k] = d;
+            st_cut(out + k, d, T.nt_out);
         }
     };
     Off R = min(min(Fo, MAX), CAP);                          // first read (file_operations.rs:738)
@@ -3035,7 +3056,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                                         d.offset = pp[u] + 1 - g0;
                                         d.len = (uint32_t)(pk[u] - pp[u]);
                                         d.file = i;
-                                        out[idx] = d;
+                                        st_cut(out + idx, d, T.nt_out);
                                     }
                                 }
                             }
@@ -3082,7 +3103,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                             d.offset = (uint64_t)pw + 1;
                             d.len = (uint32_t)(wr - pw);
                             d.file = i;
-                            out[idx] = d;
+                            st_cut(out + idx, d, T.nt_out);
                         }
                     }
                     cnt += (Off)n;
@@ -3243,7 +3264,7 @@ __device__ __forceinline__ void resolve_walk(const uint8_t *__restrict__ data, c
                             d.offset = (uint64_t)st;
                             d.len = (uint32_t)(wr + 1 - st);
                             d.file = i;
-                            out[idx] = d;
+                            st_cut(out + idx, d, T.nt_out);
                         }
                     }
                     bstart = (uint32_t)cnt & 63u;
@@ -3457,9 +3478,88 @@ __device__ void split_worker(const uint8_t *__restrict__ data, const KParams &P,
 }
 
 // After the resolve launch (so after every walker): copy the cuts of every
-// segment walk a file walker adopted into that file's output.  PARTS waves per
-// record / run, U 16-byte loads in flight per lane (dev A/B: SYNCR_CDC_ABLATE=18
-// runs <16, 16>).
+// segment walk a file walker adopted into that file's output, and expand the
+// deferred runs.  PARTS waves per record / run (up to 3 x 4096 cuts: one wave
+// each left most of the grid idle), U1 16-byte loads in flight per lane (dev A/B:
+// SYNCR_CDC_ABLATE=18: U1 8).  The units of both kinds form ONE grid-
+// stride range (a wave of the usual grid takes one unit, not one of each), and a
+// run's candidate loads go out with its record / file loads: a wave's chain is
+// two dependent load rounds and its stores (dense1: the last of 4096 waves ended
+// 33 us after the launch when each wave walked one record unit, then one run
+// unit, each four dependent rounds deep; profiles/r05_dense1_resolve_copy_timeline.txt).
+template <uint32_t COPY_PARTS, int U1>
+__device__ __forceinline__ void copy_record_part(const Tables &T, uint32_t q, uint32_t part, int lane) {
+    const SplitSeg &g = T.segs[q];
+    if (g.k == 0u || g.verdict != 1u || g.ready != T.epoch) return;    // not adopted (or a stale record)
+    const uint32_t i = g.file;
+    const uint64_t o = g.out_off, rl = g.run_len, rp = g.run_pre, nr = seg_res_n(g.res);
+    const uint64_t n = nr > rl ? nr - rl : 0ull;                      // scratch cuts
+    const uint64_t per = ((n + COPY_PARTS - 1) / COPY_PARTS + 255) & ~255ull;
+    const uint64_t a = (uint64_t)part * per, e = min(n, a + per);
+    if (a >= e) return;
+    const DevCut *src = T.seg_cuts + (uint64_t)q * T.seg_scap;
+    for (uint64_t t = a + (uint64_t)lane; t < e; t += 64u * U1) {
+        DevCut v[U1];
+#pragma unroll
+        for (int u = 0; u < U1; ++u)
+            if (t + 64u * u < e) v[u] = src[t + 64u * u];
+        const uint64_t cap = T.cut_cap[i];                          // (issued with the block's loads)
+        DevCut *dst = T.cuts + T.cut_base[i];
+#pragma unroll
+        for (int u = 0; u < U1; ++u) {
+            const uint64_t tt = t + 64u * u, d = o + tt + (tt < rp ? 0u : rl);
+            if (tt < e && d < cap) st_cut(dst + d, v[u], T.nt_out);
+        }
+    }
+}
+
+// Deferred run r, part `part`: cut k starts right after candidate k-1 (file-relative).
+template <uint32_t COPY_PARTS>
+__device__ __forceinline__ void expand_run_part(const Tables &T, uint32_t r, uint32_t part, int lane) {
+    const RunJob j = T.runs[r];
+    const uint32_t i = j.file;
+    const uint64_t per = (((uint64_t)j.n + COPY_PARTS - 1) / COPY_PARTS + 255) & ~255ull;
+    const uint64_t a = (uint64_t)part * per, e = min((uint64_t)j.n, a + per);
+    if (a >= e) return;
+    // one load per cut: the previous candidate comes from the lane before (DPP) or
+    // the previous 64 (readlane); eight 64-candidate blocks in flight, issued with the
+    // record / file loads below
+    constexpr int U = 8;
+    for (uint64_t t0 = a; t0 < e; t0 += 64u * U) {
+        uint64_t pk[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = j.a + min(t0 + 64u * u + (uint64_t)lane, (uint64_t)j.n - 1);
+            pk[u] = T.cand[k] & CAND_POS_MASK;
+        }
+        const uint64_t before = T.cand[j.a + t0 - 1] & CAND_POS_MASK;     // the cut before this block
+        bool ok = true;
+        uint64_t rel = j.out - T.cut_base[i];                            // slot within the file's output
+        if (j.rec != SPLIT_END) {
+            const SplitSeg &g = T.segs[j.rec];
+            ok = g.k != 0u && g.verdict == 1u && g.ready == T.epoch;
+            rel = g.out_off + j.out;
+        }
+        const uint64_t cap = T.cut_cap[i], g0 = T.foff[i];
+        if (!ok) return;                                             // (wave-uniform)
+        DevCut *dst = T.cuts + T.cut_base[i] + rel;
+        const uint64_t lim = cap > rel ? cap - rel : 0ull;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t up = ((uint64_t)up1((uint32_t)(pk[u] >> 32)) << 32) | up1((uint32_t)pk[u]);
+            const uint64_t pp = lane ? up : (u ? readlane64(pk[u - 1], 63) : before);
+            const uint64_t tt = t0 + 64u * u + (uint64_t)lane;
+            if (tt < e && tt < lim) {
+                DevCut d;
+                d.offset = pp + 1 - g0;
+                d.len = (uint32_t)(pk[u] - pp);
+                d.file = i;
+                st_cut(dst + tt, d, T.nt_out);
+            }
+        }
+    }
+}
+
 template <uint32_t COPY_PARTS, int U1>
 __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
     const int lane = threadIdx.x & 63;
@@ -3469,87 +3569,23 @@ __global__ __launch_bounds__(256) void cdc_split_copy_kernel(Tables T) {
     if (nsplit == 0u && nruns == 0u) return;                  // nothing split or deferred
     if (blockIdx.x == 0 && threadIdx.x < 64) DBG_STAMP(T, DBG_COPY_START);
 #ifdef SYNCR_CDC_DEV
-    uint64_t dbg_c1 = 0, dbg_c2 = 0;                          // cuts this wave copied / expanded
+    const uint64_t dbg_t0 = wall_clock64();
 #endif
     const uint32_t nrec = nsplit ? min(T.split[SPL_RESERVED], T.seg_cap) : 0u;
-    // several waves per record / run (up to 3 x 4096 cuts: one wave each left
-    // most of the grid idle and each wave latency-bound)
-    // 1. scratch cuts of every adopted segment walk (its deferred run, if any,
-    //    leaves a gap of run_len slots after its first run_pre cuts)
-    for (uint32_t w = wid; w < nrec * COPY_PARTS; w += nw) {
-        const uint32_t q = w / COPY_PARTS, part = w % COPY_PARTS;
-        const SplitSeg &g = T.segs[q];
-        if (g.k == 0u || g.verdict != 1u || g.ready != T.epoch) continue;
-        const uint32_t i = g.file;
-        const uint64_t cap = T.cut_cap[i], o = g.out_off, rl = g.run_len, rp = g.run_pre;
-        const uint64_t n = seg_res_n(g.res) - rl;                    // scratch cuts
-        const uint64_t per = ((n + COPY_PARTS - 1) / COPY_PARTS + 255) & ~255ull;
-        const uint64_t a = (uint64_t)part * per, e = min(n, a + per);
-        const DevCut *src = T.seg_cuts + (uint64_t)q * T.seg_scap;
-        DevCut *dst = T.cuts + T.cut_base[i];
-#ifdef SYNCR_CDC_DEV
-        dbg_c1 += e > a ? e - a : 0u;
-#endif
-        for (uint64_t t = a + (uint64_t)lane; t < e; t += 64u * U1) {
-            DevCut v[U1];
-#pragma unroll
-            for (int u = 0; u < U1; ++u)
-                if (t + 64u * u < e) v[u] = src[t + 64u * u];
-#pragma unroll
-            for (int u = 0; u < U1; ++u) {
-                const uint64_t tt = t + 64u * u, d = o + tt + (tt < rp ? 0u : rl);
-                if (tt < e && d < cap) dst[d] = v[u];
-            }
-        }
-    }
-    // 2. deferred runs: cut k starts right after candidate k-1 (file-relative)
-    for (uint32_t w = wid; w < nruns * COPY_PARTS; w += nw) {
-        const RunJob j = T.runs[w / COPY_PARTS];
-        const uint32_t part = w % COPY_PARTS, i = j.file;
-        uint64_t rel = j.out - T.cut_base[i];                        // slot within the file's output
-        if (j.rec != SPLIT_END) {
-            const SplitSeg &g = T.segs[j.rec];
-            if (g.k == 0u || g.verdict != 1u || g.ready != T.epoch) continue;
-            rel = g.out_off + j.out;
-        }
-        const uint64_t cap = T.cut_cap[i], g0 = T.foff[i];
-        const uint64_t per = (((uint64_t)j.n + COPY_PARTS - 1) / COPY_PARTS + 255) & ~255ull;
-        const uint64_t a = (uint64_t)part * per, e = min((uint64_t)j.n, a + per);
-        DevCut *dst = T.cuts + T.cut_base[i] + rel;
-        const uint64_t lim = cap > rel ? cap - rel : 0ull;
-#ifdef SYNCR_CDC_DEV
-        dbg_c2 += e > a ? e - a : 0u;
-#endif
-        // one load per cut: the previous candidate comes from the lane before
-        // (DPP) or the previous 64 (readlane); eight 64-candidate blocks in flight
-        constexpr int U = 8;
-        for (uint64_t t0 = a; t0 < e; t0 += 64u * U) {
-            uint64_t pk[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint64_t k = j.a + min(t0 + 64u * u + (uint64_t)lane, (uint64_t)j.n - 1);
-                pk[u] = T.cand[k] & CAND_POS_MASK;
-            }
-            const uint64_t before = T.cand[j.a + t0 - 1] & CAND_POS_MASK;     // the cut before this block
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint64_t up = ((uint64_t)up1((uint32_t)(pk[u] >> 32)) << 32) | up1((uint32_t)pk[u]);
-                const uint64_t pp = lane ? up : (u ? readlane64(pk[u - 1], 63) : before);
-                const uint64_t tt = t0 + 64u * u + (uint64_t)lane;
-                if (tt < e && tt < lim) {
-                    DevCut d;
-                    d.offset = pp + 1 - g0;
-                    d.len = (uint32_t)(pk[u] - pp);
-                    d.file = i;
-                    dst[tt] = d;
-                }
-            }
-        }
+    // units [0, n1): scratch cuts of every adopted segment walk (its deferred run, if
+    // any, leaves a gap of run_len slots after its first run_pre cuts); [n1, n1 + n2):
+    // the deferred runs
+    const uint32_t n1 = nrec * COPY_PARTS, n2 = nruns * COPY_PARTS;
+    for (uint32_t w = wid; w < n1 + n2; w += nw) {
+        if (w < n1)
+            copy_record_part<COPY_PARTS, U1>(T, w / COPY_PARTS, w % COPY_PARTS, lane);
+        else
+            expand_run_part<COPY_PARTS>(T, (w - n1) / COPY_PARTS, (w - n1) % COPY_PARTS, lane);
     }
 #ifdef SYNCR_CDC_DEV
     if (wid < (uint32_t)DBG_NCW) {
         SCAN_STAMP(T, DBG_CW + 2 * wid, wall_clock64());
-        SCAN_STAMP(T, DBG_CW + 2 * wid + 1, (dbg_c1 << 32) | dbg_c2);
+        SCAN_STAMP(T, DBG_CW + 2 * wid + 1, dbg_t0);
     }
 #endif
 }
@@ -3657,7 +3693,6 @@ __global__ __launch_bounds__(256) void cdc_gen_kernel(uint8_t *__restrict__ base
 // only if it equals an impossible sentinel, so the loads cannot be dropped and
 // nothing is written.  NT selects the non-temporal policy (as the scan uses).
 // ---------------------------------------------------------------------------
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <bool NT>
 __global__ __launch_bounds__(256) void cdc_read_probe_kernel(const u32x4 *__restrict__ src, uint64_t nvec,
@@ -4058,8 +4093,8 @@ hipError_t launch_resolve(const uint8_t *d, const KParams &p, const Tables &t, h
             hipLaunchKernelGGL((cdc_resolve_wave_kernel<RESOLVE_PF, true>), grid, dim3(256), 0, s, d, p, t);
         else
             hipLaunchKernelGGL((cdc_resolve_wave_kernel<RESOLVE_PF, false>), grid, dim3(256), 0, s, d, p, t);
-        if (split && p.ablate == 18u)
-            hipLaunchKernelGGL((cdc_split_copy_kernel<16, 16>), dim3(1024), dim3(256), 0, s, t);
+        if (split && p.ablate == 18u)          // (dev A/B: 8 blocks of 64 cuts in flight per lane)
+            hipLaunchKernelGGL((cdc_split_copy_kernel<8, 8>), dim3(1024), dim3(256), 0, s, t);
         else if (split)
             hipLaunchKernelGGL((cdc_split_copy_kernel<8, 4>), dim3(1024), dim3(256), 0, s, t);
     }

@@ -72,8 +72,8 @@ def main():
         c.fetch()
         handles.append((v, c))
     res = {v: {"scan": [], "step": []} for v, _ in handles}
-    for _ in range(args.rounds):
-        for v, c in handles:
+    for rnd in range(args.rounds):
+        for v, c in (handles if rnd % 2 == 0 else handles[::-1]):     # alternate the order (no first-slot bias)
             c.synchronize()
             time.sleep(args.idle)
             for _ in range(args.warmup):
@@ -93,7 +93,7 @@ def main():
     for v, _ in handles:
         sc, st = res[v]["scan"], res[v]["step"]
         out["variants"][v] = {"scan_ms_med": round(statistics.median(sc), 4), "scan_ms": [round(x, 4) for x in sc],
-                              "step_ms_med": round(statistics.median(st), 4),
+                              "step_ms_med": round(statistics.median(st), 4), "step_ms": [round(x, 4) for x in st],
                               "scan_frac_med": round(span / (statistics.median(sc) / 1e3) / 8e12, 4)}
     print(json.dumps(out))
     buf.free()

@@ -28,7 +28,7 @@ DBG_RES_START, DBG_RES_END, DBG_W_ENTRY, DBG_W_SETUP, DBG_W_END, DBG_W_NBLK = 0,
 DBG_W_BLK, DBG_COPY_START, DBG_COPY_END, DBG_REC, DBG_NREC = 8, 248, 249, 256, 1024
 DBG_FW, DBG_NFW = DBG_REC + 2 * DBG_NREC, 1024
 DBG_SCAN = DBG_FW + DBG_NFW
-DBG_CW, DBG_NCW = DBG_SCAN + 4 * 4096 + 16 * 128, 4096      # split copy waves: end, cuts (p1 << 32 | p2)
+DBG_CW, DBG_NCW = DBG_SCAN + 4 * 4096 + 16 * 128, 4096      # split copy waves: end, start
 WORDS = DBG_CW + 2 * DBG_NCW
 
 
@@ -92,12 +92,13 @@ def main():
         live = cw[:, 0] > 0
         if live.any():
             ce = np.array([us(v) for v in cw[live, 0]])
-            c1, c2 = (cw[live, 1] >> np.uint64(32)).astype(np.int64), (cw[live, 1] & np.uint64(0xffffffff)).astype(np.int64)
-            wid = np.nonzero(live)[0]
-            top = np.argsort(-ce)[:6]
+            cs = np.array([us(v) for v in cw[live, 1]])
+            dur = ce - cs
             print(f"  copy wave ends ({live.sum()}): p50 {np.percentile(ce, 50):.1f} p90 {np.percentile(ce, 90):.1f} "
-                  f"max {ce.max():.1f}; cuts copied {int(c1.sum())} expanded {int(c2.sum())}; busiest waves "
-                  + ", ".join(f"w{int(wid[k])}:{ce[k]:.1f}us/{int(c1[k])}+{int(c2[k])}" for k in top))
+                  f"max {ce.max():.1f}; starts p50 {np.percentile(cs, 50):.1f} p90 {np.percentile(cs, 90):.1f} "
+                  f"max {cs.max():.1f}; durations p50 {np.percentile(dur, 50):.1f} p90 {np.percentile(dur, 90):.1f} "
+                  f"max {dur.max():.1f}; waves by wid/1024: "
+                  + ", ".join(f"{np.median(dur[(np.nonzero(live)[0] // 1024) == b]):.1f}" for b in range(4)))
         fw = d[DBG_FW:DBG_FW + DBG_NFW]
         ends = sorted(((us(v), k) for k, v in enumerate(fw) if v), reverse=True)[:6]
         order = np.argsort(-sizes.astype(np.int64), kind="stable")
