@@ -849,9 +849,15 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
                 rerun = true;
             }
             if (ctr[CTR_FLAGS] & FLAG_DENSE_OVERFLOW) {
-                // the counter holds every dense tile of the launch: enough
+                // the counter holds every dense tile of the launch: enough (the list has
+                // at most one slot per tile; the dev library's DenseSlots scans pad
+                // 8-slot chunks, up to 8 per scan wave)
                 const uint64_t need = (uint64_t)ctr[CTR_DENSE] + ctr[CTR_DENSE] / 4 + 16;
+#ifdef SYNCR_CDC_DEV
                 const uint64_t lim = (uint64_t)h->ntiles + 8ull * h->scan_grid + 64;
+#else
+                const uint64_t lim = (uint64_t)h->ntiles + 64;
+#endif
                 const uint32_t want = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(need, 2ull * h->dense_cap), lim);
                 int32_t rc = ensure_dense(h, want);
                 if (rc) return rc;

@@ -150,7 +150,9 @@ constexpr uint32_t SPLIT_ABORT = 0xfffffffeu;           // (segment walk state: 
 // published), so one relaxed read gives both; segment records reserved;
 // queue head; split walkers done; worker give-ups; segments walked by workers;
 // segments adopted by file walkers; deferred runs; dense tiles the dense pass
-// rolled (ctr[CTR_DENSE] counts list slots, DENSE_HOLE padding included)
+// rolled (ctr[CTR_DENSE] counts list slots: the product's deferred DensePend
+// slots leave no holes; only the dev library's DenseSlots scans pad 8-slot
+// chunks with DENSE_HOLE)
 enum { SPL_PUB64 = 0, SPL_RESERVED = 2, SPL_HEAD = 3, SPL_DONE = 4, SPL_GIVEUP = 5, SPL_WALKED = 6,
        SPL_ADOPTED = 7, SPL_RUNS = 8, SPL_DENSE_TILES = 9, SPL_WORDS = 10 };
 struct SplitSeg {            // 64 bytes
