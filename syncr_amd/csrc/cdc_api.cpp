@@ -265,6 +265,7 @@ Tables make_tables(syncr_cdc *h) {
     t.nst = (h->ntiles + ST_TILES - 1) / ST_TILES;   // do_launch sets the launch's geometry
     t.tscan = reinterpret_cast<uint64_t *>(zb + tscan_offset(h));
     t.nt_out = h->kp.nt_out;
+    t.gapmax = (h->kp.read_cap && h->kp.read_cap < h->kp.max_chunk) ? h->kp.read_cap : h->kp.max_chunk;
     t.tacc = (h->timing && h->timing_clock) ? h->tacc.as<uint64_t>() : nullptr;
     t.znext = reinterpret_cast<uint4 *>(zblock(h, h->zpar ^ 1u));
     t.znext_vec = (uint32_t)(zstride(h) / 16);

@@ -101,6 +101,10 @@ constexpr uint64_t CAND_KNOWN = 1ull << 63;
 // or not: the resolve bounds runs by its file).  Tables::linkw holds the same
 // bits 64 candidates per word.
 constexpr uint64_t CAND_LINK = 1ull << 62;
+// the word's CAND_LINK bit is final (set with it by the compaction for a dense
+// tile's candidates but its last, whose next candidate lies in another tile):
+// cdc_fix_kernel neither recomputes nor rewrites such a complete word
+constexpr uint64_t CAND_LDEC = 1ull << 61;
 
 struct KParams {
     uint32_t bits;     // chunk_bits
@@ -265,6 +269,7 @@ struct Tables {
                                    //   timeline (wall_clock64 stamps, DBG_*), else nullptr
     uint32_t nst;                  // stream-tile scan: STs of the batch (launch geometry)
     uint32_t nt_out;               // KParams::nt_out: non-temporal stores of candidate words and cuts
+    uint64_t gapmax;               // chain links: the next candidate at most min(MAX, read_cap) past
     // scan timing by the device clock (syncr_cdc_set_timing mode 2; null: off): the scan's
     // waves stamp wall_clock64 -- tscan[0] = ~0 - the earliest entry, tscan[1] = the
     // latest exit (atomic max, zeroed per launch) -- and the resolve adds exit - entry

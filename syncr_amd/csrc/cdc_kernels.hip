@@ -1617,8 +1617,9 @@ __global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__rest
 // lengthen the gather's critical path; profiles/r02_ab_run_fusefix.log.)
 // known = the fix-up the dense pass already stored with a candidate (CAND_KNOWN), else ~0u
 __device__ __forceinline__ void fix_item(const Tables &T, uint64_t n, uint64_t i, uint64_t &a, uint32_t &cnt,
-                                         uint32_t &known) {
+                                         uint32_t &known, uint32_t &dec) {
     known = ~0u;
+    dec = 0u;                                             // bit 0: link decided (CAND_LDEC), bit 1: its value
     if (i < n) {                                          // a candidate e: chunk starts at e + 1
         const uint64_t w = T.cand[i];
         a = (w & CAND_POS_MASK) + 1;
@@ -1626,6 +1627,7 @@ __device__ __forceinline__ void fix_item(const Tables &T, uint64_t n, uint64_t i
         if (w & CAND_KNOWN) {
             known = (uint32_t)(w >> 48) & 0xffu;
             cnt = 0u;
+            if (w & CAND_LDEC) dec = 1u | ((w & CAND_LINK) ? 2u : 0u);
         }
     } else if (i < n + T.ngrid) {                         // a grid point p: chunk starts at p, ends by the file's end
         a = T.gpos[i - n];
@@ -1736,9 +1738,9 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
     const uint64_t items = n + T.ngrid;
     for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; 2 * q < items; q += (uint64_t)gridDim.x * 256) {
         uint64_t aA, aB;
-        uint32_t nA, nB, kA, kB;
-        fix_item(T, n, 2 * q, aA, nA, kA);
-        fix_item(T, n, 2 * q + 1, aB, nB, kB);
+        uint32_t nA, nB, kA, kB, dA, dB;
+        fix_item(T, n, 2 * q, aA, nA, kA, dA);
+        fix_item(T, n, 2 * q + 1, aB, nB, kB, dB);
         uint32_t fA = 0u, fB = 0u;
         if (__ballot(nA != 0u || nB != 0u)) {             // (candidates of the dense pass's tiles come known)
             uint32_t A[16], B[16];
@@ -1749,13 +1751,14 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
         if (kA != ~0u) fA = kA;
         if (kB != ~0u) fB = kB;
         // chain links (CAND_LINK): empty fix-up, next candidate 64 .. gapmax past
-        const uint64_t gapmax = P.read_cap && P.read_cap < P.max_chunk ? P.read_cap : P.max_chunk;
-        bool lA = false, lB = false;
-        if (T.linkw && 2 * q + 1 < n) {
+        // (a dense tile's candidates come with theirs decided, CAND_LDEC, but the last)
+        const uint64_t gapmax = T.gapmax;
+        bool lA = (dA & 2u) != 0u, lB = (dB & 2u) != 0u;
+        if (T.linkw && !dA && 2 * q + 1 < n) {
             const uint64_t d = aB - aA;                       // positions 2q+1 and 2q
             lA = fA == 0u && d >= 64u && d <= gapmax;
         }
-        if (T.linkw && 2 * q + 2 < n) {
+        if (T.linkw && !dB && 2 * q + 2 < n) {
             const uint64_t d = (T.cand[2 * q + 2] & CAND_POS_MASK) - (aB - 1);
             lB = fB == 0u && d >= 64u && d <= gapmax;
         }
@@ -1763,8 +1766,10 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
         for (int h = 0; h < 2; ++h) {
             const uint64_t i = 2 * q + (uint64_t)h;
             const uint32_t f = h ? fB : fA;
-            if (i < n) st_u64(&T.cand[i], ((h ? aB : aA) - 1) | ((uint64_t)f << 48) | CAND_KNOWN | ((h ? lB : lA) ? CAND_LINK : 0ull), T.nt_out);
-            else if (i < items) T.gfix[i - n] = (uint8_t)f;
+            if (i < n && !(h ? dB : dA))                      // (a decided word is complete already)
+                st_u64(&T.cand[i], ((h ? aB : aA) - 1) | ((uint64_t)f << 48) | CAND_KNOWN |
+                                       ((h ? lB : lA) ? CAND_LINK : 0ull), T.nt_out);
+            else if (i >= n && i < items) T.gfix[i - n] = (uint8_t)f;
         }
         // the wave's 128 consecutive candidates (lane l: 2l, 2l+1) as two link words
         if (T.linkw) {
@@ -2245,8 +2250,17 @@ __device__ __forceinline__ void gather_dense(const Tables &T, int lane, uint32_t
             // the dense pass stored rank r's position and head fix-up (dense_pos / dense_fix)
             const uint16_t *ps = T.dense_pos + (size_t)idx * FIXCAP;
             const uint8_t *fx = T.dense_fix + (size_t)idx * FIXCAP;
-            for (uint32_t r = (uint32_t)lane; r < tc; r += 64)
-                st_u64(&T.cand[tb + r], (t0 + ps[r]) | ((uint64_t)fx[r] << 48) | CAND_KNOWN, T.nt_out);
+            // and, with chain links on, each candidate's link but the tile's last
+            // (its next candidate is in another tile: cdc_fix_kernel decides it)
+            for (uint32_t r = (uint32_t)lane; r < tc; r += 64) {
+                const uint32_t p = ps[r], f = fx[r];
+                uint64_t lk = 0;
+                if (T.linkw && r + 1 < tc) {
+                    const uint32_t d = (uint32_t)ps[r + 1] - p;
+                    lk = CAND_LDEC | ((f == 0u && d >= 64u && (uint64_t)d <= T.gapmax) ? CAND_LINK : 0ull);
+                }
+                st_u64(&T.cand[tb + r], (t0 + p) | ((uint64_t)f << 48) | CAND_KNOWN | lk, T.nt_out);
+            }
             continue;
         }
         uint64_t o = tb;
