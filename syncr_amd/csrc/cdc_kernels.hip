@@ -1037,7 +1037,11 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             const uint32_t relA0 = (uint32_t)lane * L + g * RUN;
             uint32_t S = Sc;
             u16x2 Tv = Tc;
-            uint32_t xs[RUN];
+            // positions 64..127 go straight into Pd as the next segment's dropped pairs:
+            // Pd[j - 64] was last read as position j - 64's (no carry copies after the
+            // segment: those were 64 moves per segment, 7 % of the kernel's VALU)
+            static_assert(RUN == 128, "two halves of 64 pairs");
+            uint32_t xl[64];                                           // pairs of positions 0..63
 #pragma unroll
             for (int gg = 0; gg < NG; ++gg) {
                 const uint32_t S0 = S;
@@ -1046,24 +1050,33 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 #pragma unroll
                 for (int jj = 0; jj < 16; ++jj) {
                     const int j = gg * 16 + jj;
-                    xs[j] = xpair32(XA, XB, j);
-                    const uint32_t d = j < 64 ? Pd[j < 64 ? j : 0] : xs[j >= 64 ? j - 64 : 0];
-                    S = S + xs[j] - d;
+                    const uint32_t x = xpair32(XA, XB, j);
+                    const uint32_t d = j < 64 ? Pd[j < 64 ? j : 0] : xl[j >= 64 ? j - 64 : 0];
+                    if (j < 64) xl[j < 64 ? j : 0] = x;
+                    else Pd[j >= 64 ? j - 64 : 0] = x;
+                    S = S + x - d;
                     const u16x2 V = pk_mad(d, 0xFFC0FFC0u, as_u16x2(S));
                     Tv = pk_mad(as_u32(V), P.kk, Tv);
                     acc = __builtin_elementwise_min(acc, Tv);
                 }
                 const uint32_t a = as_u32(acc);
-                const bool z = (a & 0xffffu) == 0u || (a >> 16) == 0u;
-                const uint64_t bz = __ballot(z);
+                // (two ballots of plain compares: one of their OR went through a 0/1
+                // VGPR and a compare; the lane's own bit and the marks below are
+                // derived inside the rare branch, not per group)
+                const uint64_t bz = __builtin_amdgcn_ballot_w64((a & 0xffffu) == 0u) |
+                                    __builtin_amdgcn_ballot_w64(a < 0x10000u);
                 if (__builtin_expect(bz != 0ull, 0)) {
                     const uint32_t nz = (uint32_t)__builtin_popcountll(bz);
+                    uint64_t bzs = bz;
+                    asm volatile("" : "+s"(bzs));            // (else folded back to the lane's condition, kept live per group)
+                    const bool z = ((bzs >> lane) & 1ull) != 0ull;
                     if (have + nz > (uint32_t)ST_DIRTYCAP) {
                         // no room for this group's dirty streams: their tiles go to the dense
                         // pass (the tiles of the dirty groups of this lane's two streams;
                         // the marks are applied when the ST is published)
                         constexpr uint32_t TB = (uint32_t)tile_bytes(DEFAULT_RUN);
-                        const uint32_t ga = relA0 + 16u * (uint32_t)gg;        // the group's ST-relative position
+                        uint32_t ga = relA0 + 16u * (uint32_t)gg;              // the group's ST-relative position
+                        asm volatile("" : "+v"(ga));                            // (computed here, not per segment)
                         dmark |= ((a & 0xffffu) == 0u ? 1u << (ga / TB) : 0u) |
                                  ((a >> 16) == 0u ? 1u << ((ga + 64u * L) / TB) : 0u);
                     } else {
@@ -1074,8 +1087,8 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 #pragma unroll
                             for (int jj = 0; jj < 16; ++jj) {
                                 const int j = gg * 16 + jj;
-                                ds.dp[jj] = j < 64 ? Pd[j < 64 ? j : 0] : xs[j >= 64 ? j - 64 : 0];
-                                ds.xp[jj] = xs[j];
+                                ds.dp[jj] = j < 64 ? Pd[j < 64 ? j : 0] : xl[j >= 64 ? j - 64 : 0];
+                                ds.xp[jj] = j < 64 ? xl[j < 64 ? j : 0] : Pd[j >= 64 ? j - 64 : 0];
                             }
                             ds.S0 = S0;
                             ds.T0 = as_u32(T0);
@@ -1085,9 +1098,6 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                     }
                 }
             }
-            // carry the window: the pairs of positions RUN-64 .. RUN-1 are the next segment's dropped bytes
-#pragma unroll
-            for (int j = 0; j < 64; ++j) Pd[j] = xs[RUN - 64 + j];
             Sc = S;
             Tc = Tv;
             // ---- exact re-walk of the captured groups

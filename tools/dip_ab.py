@@ -29,6 +29,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("variants", nargs="+")
     ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--events", action="store_true",
+                    help="time the scan by HIP events bound to its dispatch (kernels without device-clock stamps)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--idle", type=float, default=0.5)
@@ -79,7 +81,7 @@ def main():
             for _ in range(args.warmup):
                 c.launch(buf.ptr)
             c.synchronize()
-            c.set_timing(True, scan_only=True)
+            c.set_timing(True, scan_only=True, events=args.events)
             t0 = time.perf_counter()
             for _ in range(args.steps):
                 c.launch(buf.ptr)
@@ -87,7 +89,7 @@ def main():
             dt = (time.perf_counter() - t0) / args.steps * 1e3
             ms, n = c.kernel_times()
             c.set_timing(False)
-            res[v]["scan"].append(ms[0] / n)
+            res[v]["scan"].append(ms[0] / n if n else float("nan"))
             res[v]["step"].append(dt)
     out = {"workload": args.workload, "bytes": span, "steps": args.steps, "warmup": args.warmup, "variants": {}}
     for v, _ in handles:

@@ -10,7 +10,8 @@
 #   devtests|<ENV=V,...>[|<-k expr>]    the GPU suite on libsyncr_cdc_dev.so with a variant forced
 #   smoke                               __graft_entry__.smoke()
 #   bench[|<extra bench.py flags>[|<checkout>]]  the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
-#   ab|<workload>|<rounds>|<V1>|<V2>... tools/dip_ab.py variants (dev library) in the driver's condition
+#   ab|<workload>|<rounds>[e]|<V1>|<V2>... tools/dip_ab.py variants (dev library) in the driver's condition
+#                                       (rounds suffix e: scan timed by HIP events)
 #   trace|<workload>[|<shard>[|--no-events[|<checkout>]]]  kernel trace of one small-batch leg
 #                                       (tools/legs_trace.py, product; <checkout>: e.g. build/r04src)
 #   pmc|<workload>|<counters>          one rocprofv3 --pmc pass over a legs_trace.py leg (per-kernel means)
@@ -61,7 +62,8 @@ for step in "$@"; do
             2> "$out.err" || { echo "bench failed rc=$?"; tail -30 "$out.err"; exit 14; }
         python tools/bench_summary.py "$out.json" ;;
     ab)
-        timeout -k 10 600 python -u tools/dip_ab.py "${a[@]:3}" --workload "${a[1]}" --rounds "${a[2]}" > "$out.jsonl" 2> "$out.err" \
+        EV=(); [[ "${a[2]}" == *e ]] && EV=(--events)          # rounds "4e": HIP-event scan timing
+        timeout -k 10 600 python -u tools/dip_ab.py "${a[@]:3}" --workload "${a[1]}" --rounds "${a[2]%e}" "${EV[@]}" > "$out.jsonl" 2> "$out.err" \
             || { echo "ab failed rc=$?"; tail -30 "$out.err"; exit 15; }
         python - "$out.jsonl" <<'PY'
 import json, sys
