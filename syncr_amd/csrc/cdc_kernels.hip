@@ -942,6 +942,18 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     uint32_t HA[16], HB[16];
     auto load_halo = [&](uint32_t st) {
         const int64_t sa = (int64_t)st * STB + (int64_t)lane * L - 64, sbb = sa + 64 * (int64_t)L;
+        if (st != 0u && (uint64_t)st * STB + STB <= (uint64_t)span) {
+            // (wave-uniform) every halo of the ST lies inside the batch: no per-load bounds
+            // (the checked form below is ~50 VALU per ST)
+            const uint4 *pa = (const uint4 *)(data + sa), *pb = (const uint4 *)(data + sbb);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const uint4 va = pa[m], vb = pb[m];
+                HA[4 * m] = va.x; HA[4 * m + 1] = va.y; HA[4 * m + 2] = va.z; HA[4 * m + 3] = va.w;
+                HB[4 * m] = vb.x; HB[4 * m + 1] = vb.y; HB[4 * m + 2] = vb.z; HB[4 * m + 3] = vb.w;
+            }
+            return;
+        }
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             uint4 va, vb;
@@ -977,7 +989,13 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             const bool first = g == 0u;
             if (first && lane < TILES) tcnt[lane] = 0u;
             uint32_t have = 0;                                       // dirty slots taken (wave-uniform)
-            wait_vmcnt<0>();                                         // segment g landed (and, at 0, the halo)
+            // Segment g landed (and, at 0, the halo; and the ST grab).  The builtin, not
+            // asm: hipcc's waitcnt tracking sees it, so it adds no wait of its own for
+            // loads it believes pending across the loop (the halo) -- it put a vmcnt(0)
+            // right behind the next ST's DMAs, a landing-time stall at every ST end.
+            // The empty statement after it is pend's definition for hipcc.
+            __builtin_amdgcn_s_waitcnt(0x0F70);                      // vmcnt(0)
+            asm volatile("" : "+v"(pend) : : "memory");
 #ifdef SYNCR_CDC_DEV
             if (stamp && first && nst_done == 0) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 1, wall_clock64());
             // every segment landing of the first DBG_TILE_W waves (unit switches vs. steady segments)
@@ -1019,11 +1037,6 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 // (grabbing at segment 0 before its landing wait put every wave of the grid on
                 // one address at launch: the first segment landed 18.7 us after entry, median,
                 // tools/scan_timeline.py)
-                if (g == (nth == 0u ? 4u + (blockIdx.x & 3u) : (uint32_t)SEGS - 2u) && nst > gridDim.x) {
-                    // (the compiler waits for the result at once -- its copy into the
-                    // loop-carried register -- but segment 1's DMAs are in flight by then)
-                    if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
-                }
             } else {
                 nextst = nst > gridDim.x ? gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nst;
                 more = nextst < nst;
@@ -1031,6 +1044,28 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                     issue_seg(nextst, 0);
                     load_halo(nextst);
                 }
+            }
+            {
+                // The grab: an asm atomic of lane 0 (exec set inside the statement), run in
+                // EVERY segment so that pend has one definition per segment -- exec 0 but
+                // at the grab segment.  Its result is read only at the ST's last segment,
+                // after that segment's top wait (the grab is at most segment 7 < SEGS - 1).
+                // hipcc's atomicAdd waited for it at once (the atomic optimizer reads the
+                // result to spread it over the lanes), and so for the next segment's DMAs
+                // issued just above: a landing-time stall once per ST.
+                const uint32_t gm = __builtin_amdgcn_readfirstlane(
+                    (g == (nth == 0u ? 4u + (blockIdx.x & 3u) : (uint32_t)SEGS - 2u) && nst > gridDim.x) ? 1u : 0u);
+                uint32_t keep_lo, keep_hi;
+                asm volatile("s_mov_b32 %1, exec_lo\n\t"
+                             "s_mov_b32 %2, exec_hi\n\t"
+                             "s_mov_b32 exec_lo, %3\n\t"
+                             "s_mov_b32 exec_hi, 0\n\t"
+                             "global_atomic_add %0, %4, %5, %6 offset:%7 sc0\n\t"
+                             "s_mov_b32 exec_lo, %1\n\t"
+                             "s_mov_b32 exec_hi, %2"
+                             : "+v"(pend), "=&s"(keep_lo), "=&s"(keep_hi)
+                             : "s"(gm), "v"(0u), "v"(1u), "s"(T.ctr), "i"(CTR_CANDS_HI * 4)
+                             : "memory");
             }
             // ---- roll segment g: positions 0..63 drop Pd, later ones this segment's own pairs
             const int64_t lim_rel = span - (int64_t)st * STB;         // ST-relative positions >= lim: not bytes
