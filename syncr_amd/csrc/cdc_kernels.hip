@@ -66,6 +66,36 @@ __device__ __forceinline__ void st_cut(DevCut *p, const DevCut &v, uint32_t nt) 
     }
 }
 
+// The scans' tile / segment wait and their work grab.  Their DMAs are inline asm
+// (LDS-DMA with M0), which hipcc's waitcnt tracking cannot see, so
+//  - the wait is the builtin (tracked: hipcc then adds no vmcnt(0) of its own for
+//    loads it believes pending across the loop -- a landing-time stall behind the
+//    DMAs just issued), and the empty statement after it is the definition of the
+//    grab's result `pend` for hipcc;
+//  - the grab is an asm atomic of lane 0, exec set inside the statement (`on` 0:
+//    no lane), run at every tile / segment so `pend` has one definition per
+//    iteration and no join copy reads its register before it returned.  hipcc's
+//    atomicAdd waited for the result at once (the atomic optimizer spreads it over
+//    the lanes), i.e. for the DMAs issued just before it.
+__device__ __forceinline__ void wait_all_pend(uint32_t &pend) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);                               // vmcnt(0)
+    asm volatile("" : "+v"(pend) : : "memory");
+}
+__device__ __forceinline__ void grab_async(uint32_t &pend, uint32_t *ctr_word0, uint32_t on) {
+    const uint32_t gm = __builtin_amdgcn_readfirstlane(on);
+    uint32_t keep_lo, keep_hi;
+    asm volatile("s_mov_b32 %1, exec_lo\n\t"
+                 "s_mov_b32 %2, exec_hi\n\t"
+                 "s_mov_b32 exec_lo, %3\n\t"
+                 "s_mov_b32 exec_hi, 0\n\t"
+                 "global_atomic_add %0, %4, %5, %6 offset:%7 sc0\n\t"
+                 "s_mov_b32 exec_lo, %1\n\t"
+                 "s_mov_b32 exec_hi, %2"
+                 : "+v"(pend), "=&s"(keep_lo), "=&s"(keep_hi)
+                 : "s"(gm), "v"(0u), "v"(1u), "s"(ctr_word0), "i"(CTR_CANDS_HI * 4)
+                 : "memory");
+}
+
 // ds_bpermute round trips through the LDS unit: lane l gets lane l-1's value
 // (up1; lane 0 gets 0) or lane l+1's (down1; lane 63 gets 0).  All lanes active.
 __device__ __forceinline__ uint32_t up1(uint32_t v) {
@@ -714,10 +744,10 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 gjn = gj + 1;
             } else {
                 if (gj == 0) {                                       // group ends at its first tile (last round)
-                    if (lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
+                    grab_async(pend, T.ctr, 1u);
                     grabbed = true;                                  // (no second grab below: it would drop a group)
                 }
-                wait_vmcnt<0>();                                     // the grab
+                wait_all_pend(pend);                                 // the grab
                 next = gbase(stride + (uint32_t)__builtin_amdgcn_readfirstlane(pend));
                 gjn = 0;
             }
@@ -726,7 +756,8 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         }
         const int64_t t0 = (int64_t)tile * TILE;
         if (lane == 0) { *wcount = 0u; *dcount = 0u; }
-        wait_vmcnt<0>();                                             // this tile has landed
+        if constexpr (DYN) wait_all_pend(pend);                      // this tile has landed (and the group grab)
+        else wait_vmcnt<0>();
         uint32_t nk = 0;
         if constexpr (CUS) {                                         // the CU's next tile (read after the runs)
             pf_store();
@@ -767,7 +798,7 @@ void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
         }
         if (next < T.ntiles && (MODE & 3) != 2) issue_tile<RUN, (MODE & 4) != 0>(data, T.span, next, lds0, lane);
         if constexpr (DYN) {
-            if (gj == 0 && !grabbed && lane == 0) pend = atomicAdd(&T.ctr[CTR_CANDS_HI], 1u);
+            grab_async(pend, T.ctr, (gj == 0 && !grabbed) ? 1u : 0u);  // read at the group's last tile
             gj = gjn;
         }
         if constexpr ((MODE & 3) == 1) {                                   // diagnostics: staging only
@@ -989,13 +1020,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             const bool first = g == 0u;
             if (first && lane < TILES) tcnt[lane] = 0u;
             uint32_t have = 0;                                       // dirty slots taken (wave-uniform)
-            // Segment g landed (and, at 0, the halo; and the ST grab).  The builtin, not
-            // asm: hipcc's waitcnt tracking sees it, so it adds no wait of its own for
-            // loads it believes pending across the loop (the halo) -- it put a vmcnt(0)
-            // right behind the next ST's DMAs, a landing-time stall at every ST end.
-            // The empty statement after it is pend's definition for hipcc.
-            __builtin_amdgcn_s_waitcnt(0x0F70);                      // vmcnt(0)
-            asm volatile("" : "+v"(pend) : : "memory");
+            wait_all_pend(pend);                                     // segment g landed (and, at 0, the halo)
 #ifdef SYNCR_CDC_DEV
             if (stamp && first && nst_done == 0) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 1, wall_clock64());
             // every segment landing of the first DBG_TILE_W waves (unit switches vs. steady segments)
@@ -1045,28 +1070,10 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                     load_halo(nextst);
                 }
             }
-            {
-                // The grab: an asm atomic of lane 0 (exec set inside the statement), run in
-                // EVERY segment so that pend has one definition per segment -- exec 0 but
-                // at the grab segment.  Its result is read only at the ST's last segment,
-                // after that segment's top wait (the grab is at most segment 7 < SEGS - 1).
-                // hipcc's atomicAdd waited for it at once (the atomic optimizer reads the
-                // result to spread it over the lanes), and so for the next segment's DMAs
-                // issued just above: a landing-time stall once per ST.
-                const uint32_t gm = __builtin_amdgcn_readfirstlane(
-                    (g == (nth == 0u ? 4u + (blockIdx.x & 3u) : (uint32_t)SEGS - 2u) && nst > gridDim.x) ? 1u : 0u);
-                uint32_t keep_lo, keep_hi;
-                asm volatile("s_mov_b32 %1, exec_lo\n\t"
-                             "s_mov_b32 %2, exec_hi\n\t"
-                             "s_mov_b32 exec_lo, %3\n\t"
-                             "s_mov_b32 exec_hi, 0\n\t"
-                             "global_atomic_add %0, %4, %5, %6 offset:%7 sc0\n\t"
-                             "s_mov_b32 exec_lo, %1\n\t"
-                             "s_mov_b32 exec_hi, %2"
-                             : "+v"(pend), "=&s"(keep_lo), "=&s"(keep_hi)
-                             : "s"(gm), "v"(0u), "v"(1u), "s"(T.ctr), "i"(CTR_CANDS_HI * 4)
-                             : "memory");
-            }
+            // the ST grab (grab_async): lane 0 at 4 + blockIdx % 4 in a wave's first ST,
+            // at SEGS - 2 in later ones; read at the ST's last segment after its wait
+            grab_async(pend, T.ctr, (g == (nth == 0u ? 4u + (blockIdx.x & 3u) : (uint32_t)SEGS - 2u) &&
+                                     nst > gridDim.x) ? 1u : 0u);
             // ---- roll segment g: positions 0..63 drop Pd, later ones this segment's own pairs
             const int64_t lim_rel = span - (int64_t)st * STB;         // ST-relative positions >= lim: not bytes
             const uint32_t relA0 = (uint32_t)lane * L + g * RUN;
