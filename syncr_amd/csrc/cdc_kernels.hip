@@ -2263,13 +2263,16 @@ __device__ __forceinline__ uint64_t word_prefix(const Tables &T, uint32_t w, int
 
 // A nonempty tile's candidate count for the compaction and its tile_meta (DENSE_BIT |
 // dense index, else 0 or the count).
-__device__ __forceinline__ uint32_t tile_cands(const Tables &T, uint32_t tile, uint32_t &meta) {
-    meta = T.tile_meta[tile];
+__device__ __forceinline__ uint32_t tile_cands_of(const Tables &T, uint32_t m, uint32_t &meta) {
+    meta = m;
     if (meta & DENSE_BIT) {
         const uint32_t idx = meta & ~DENSE_BIT;
         return (!T.dense_off && idx < T.dense_cap) ? T.dense_cnt[idx] & ~DENSE_FIXED : 0u;
     }
     return meta;
+}
+__device__ __forceinline__ uint32_t tile_cands(const Tables &T, uint32_t tile, uint32_t &meta) {
+    return tile_cands_of(T, T.tile_meta[tile], meta);
 }
 
 // Dense tiles are expanded by the blocks past the word blocks, one wave per
@@ -2351,14 +2354,17 @@ __global__ __launch_bounds__(256) void cdc_gather_kernel(Tables T) {
             if (total > T.cand_cap) T.ctr[CTR_FLAGS] |= FLAG_CAND_OVERFLOW;
         }
     }
+    // the word's bits and its tiles' metas are loaded with the prefix's counts (one round
+    // trip, not three: the super_off store kept them behind the prefix)
+    const uint32_t tile = w * 64 + lane;
+    const unsigned long long bits = T.nonempty[w];
+    const uint32_t m0 = T.tile_meta[tile < T.ntiles ? tile : 0u];
     const uint64_t pre = word_prefix(T, w, lane);
     if (lane == 0) T.super_off[w] = pre;
-    const unsigned long long bits = T.nonempty[w];
     if (!bits) return;
-    const uint32_t tile = w * 64 + lane;
     const bool has = (bits >> lane) & 1ull;
     uint32_t meta = 0, c = 0;
-    if (has) c = tile_cands(T, tile, meta);
+    if (has) c = tile_cands_of(T, m0, meta);
     const uint32_t incl = wave_incl_scan(c, lane);
     const uint64_t base = pre + (incl - c);
     const bool dense = has && (meta & DENSE_BIT) && c;
@@ -2421,14 +2427,15 @@ __global__ __launch_bounds__(256) void cdc_gather_fix_kernel(const uint8_t *__re
             if (total > T.cand_cap) T.ctr[CTR_FLAGS] |= FLAG_CAND_OVERFLOW;
         }
     }
+    const uint32_t tile = w * 64 + (uint32_t)lane;
+    const unsigned long long bits = T.nonempty[w];                 // (loaded with the prefix's counts)
+    const uint32_t m0 = T.tile_meta[tile < T.ntiles ? tile : 0u];
     const uint64_t pre = word_prefix(T, w, lane);
     if (lane == 0) T.super_off[w] = pre;
-    const unsigned long long bits = T.nonempty[w];
     if (!bits) return;
-    const uint32_t tile = w * 64 + (uint32_t)lane;
     const bool has = (bits >> lane) & 1ull;
     uint32_t meta = 0, c = 0;
-    if (has) c = tile_cands(T, tile, meta);                  // (dense_off: a dense tile counts 0; fetch re-runs)
+    if (has) c = tile_cands_of(T, m0, meta);                 // (dense_off: a dense tile counts 0; fetch re-runs)
     if (meta & DENSE_BIT) c = 0u;
     const uint32_t incl = wave_incl_scan(c, lane);
     const uint32_t ctot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
