@@ -565,8 +565,10 @@ def ingest_files_leg(host: np.ndarray, offs, lens, idx, device: int, gib: float 
     are written to local disk (a temporary directory), then every file goes
     through syncr_ingest_submit_file (pread straight into pinned staging ->
     H2D -> chunk + BLAKE3 -> per-file ChunkInfo callbacks); every file is
-    checked against the golden digests.  The files were just written, so they
-    are served from the page cache (this process cannot drop it)."""
+    checked against the golden digests.  The files were just written and
+    fsync'ed, so they are served from the page cache, clean (this process cannot
+    drop it; dirty pages under writeback during the timed passes once read at
+    10.7 GiB/s instead of ~37)."""
     import shutil
     import tempfile
     import syncr_amd
@@ -584,6 +586,8 @@ def ingest_files_leg(host: np.ndarray, offs, lens, idx, device: int, gib: float 
             pth = os.path.join(d, f"f{j:05d}.bin")
             with open(pth, "wb") as f:
                 f.write(host[int(offs[j]): int(offs[j] + lens[j])].tobytes())
+                f.flush()
+                os.fsync(f.fileno())       # clean pages: no writeback of them during the timed reads
             paths.append(pth)
         best = None
         with syncr_amd.Ingest(device=device, batch_bytes=256 << 20, depth=3, copy_threads=16,
@@ -602,7 +606,8 @@ def ingest_files_leg(host: np.ndarray, offs, lens, idx, device: int, gib: float 
     got = [res[k][1] for k in range(len(take))]
     return {"value": round(tot / best / 2**30, 3), "unit": "GiB/s", "seconds": round(best, 4), "bytes": tot,
             "files": len(take),
-            "path": "files on local disk (page-cache resident: just written) -> syncr_ingest_submit_file (open + "
+            "path": "files on local disk (page-cache resident and clean: just written, fsync'ed) -> "
+                    "syncr_ingest_submit_file (open + "
                     "fstat on the caller, pread into pinned staging on 16 pool threads, 2 MiB per task, the caller "
                     "goes on to the next file) -> H2D -> chunk + BLAKE3 -> per-file ChunkInfo; best of %d "
                     "passes" % reps,
