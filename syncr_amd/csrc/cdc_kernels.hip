@@ -1020,13 +1020,19 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             const bool first = g == 0u;
             if (first && lane < TILES) tcnt[lane] = 0u;
             uint32_t have = 0;                                       // dirty slots taken (wave-uniform)
+#ifdef SYNCR_CDC_DEV
+            // every segment of the first DBG_TILE_W waves: arrival at the wait (bit 55) and
+            // landing (unit switches vs. steady segments; processing vs. waiting)
+            if (blockIdx.x < (uint32_t)DBG_TILE_W && seg_done + 1 < (uint32_t)DBG_TILE_N)
+                SCAN_STAMP(T, DBG_TILE + DBG_TILE_N * blockIdx.x + seg_done,
+                           wall_clock64() | ((uint64_t)g << 56) | (1ull << 55));
+#endif
             wait_all_pend(pend);                                     // segment g landed (and, at 0, the halo)
 #ifdef SYNCR_CDC_DEV
             if (stamp && first && nst_done == 0) SCAN_STAMP(T, DBG_SCAN + 4 * blockIdx.x + 1, wall_clock64());
-            // every segment landing of the first DBG_TILE_W waves (unit switches vs. steady segments)
-            if (blockIdx.x < (uint32_t)DBG_TILE_W && seg_done < (uint32_t)DBG_TILE_N)
-                SCAN_STAMP(T, DBG_TILE + DBG_TILE_N * blockIdx.x + seg_done, wall_clock64() | ((uint64_t)g << 56));
-            ++seg_done;
+            if (blockIdx.x < (uint32_t)DBG_TILE_W && seg_done + 1 < (uint32_t)DBG_TILE_N)
+                SCAN_STAMP(T, DBG_TILE + DBG_TILE_N * blockIdx.x + seg_done + 1, wall_clock64() | ((uint64_t)g << 56));
+            seg_done += 2;
 #endif
             if (first) {                                             // warm-up from the halo (closed form)
                 uint32_t SA = 0, WA = 0, SB = 0, WB = 0;
@@ -1184,13 +1190,21 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 }
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll 1
-                for (uint32_t t = 0; t < (uint32_t)TILES; ++t) {
+                // the ST's tile counts in one LDS read (lane t: tile t), then only the tiles
+                // with candidates or a dense mark (random data: none) -- one LDS round trip
+                // per tile was ~0.6 us of every ST switch
+                static_assert(TILES <= 64, "one lane per tile");
+                const uint32_t cl = (uint32_t)lane < (uint32_t)TILES
+                                        ? __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)&tcnt[lane],
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)
+                                        : 0u;
+                uint64_t todo = __builtin_amdgcn_ballot_w64(cl != 0u);
+                while (todo) {
+                    const uint32_t t = (uint32_t)__builtin_ctzll(todo);
+                    todo &= todo - 1ull;
                     const uint32_t tile = st * TILES + t;
                     if (tile >= T.ntiles) break;
-                    const uint32_t c = __builtin_amdgcn_readfirstlane(
-                        __hip_atomic_load((__attribute__((address_space(3))) uint32_t *)&tcnt[t], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WAVEFRONT));
+                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, (int)t);
                     publish_list(T, tile, tlist + t * LC, c & 0x7fffffffu, lane, (c >> 31) != 0u,
                                  dslots_alloc, (uint32_t)LC);
                 }

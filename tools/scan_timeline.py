@@ -69,10 +69,20 @@ def summarize(d, grid):
     tiles = d[DBG_TILE:DBG_TILE + DBG_TILE_W * DBG_TILE_N].reshape(DBG_TILE_W, DBG_TILE_N).astype(np.uint64)
     per_tile = []
     seg_by_g = {}                                   # stream-tile scan: landing-to-landing time by segment index
+    wait_by_g, work_by_g = {}, {}                   # stream tiles: wait at the landing / work before it
     for w in range(DBG_TILE_W):
         raw = tiles[w][tiles[w] > 0]
+        arr = (raw >> np.uint64(55)) & np.uint64(1)
         g = (raw >> np.uint64(56)).astype(np.int64)
-        t = (raw & np.uint64((1 << 56) - 1)).astype(np.int64)
+        t = (raw & np.uint64((1 << 55) - 1)).astype(np.int64)
+        if arr.any():                               # stream-tile kernel: (arrive, landed) pairs
+            land = np.nonzero(arr == 0)[0]
+            for j, k in enumerate(land):
+                if k > 0 and arr[k - 1]:
+                    wait_by_g.setdefault(int(g[k]), []).append(float(t[k] - t[k - 1]) / 100.0)
+                    if j > 0:
+                        work_by_g.setdefault(int(g[k]), []).append(float(t[k - 1] - t[land[j - 1]]) / 100.0)
+            g, t = g[land], t[land]
         if t.size > 2:
             dt = np.diff(t)
             per_tile.extend(dt.tolist())
@@ -97,6 +107,10 @@ def summarize(d, grid):
         # unit's first segment, after the last segment of the previous one)
         "seg_landing_gap_us_by_g": {g: {"median": round(float(np.median(v)), 3), "n": len(v)}
                                     for g, v in sorted(seg_by_g.items())},
+        # of that gap: the wave's own work since the previous landing (roll, DMA issue, grab,
+        # publish) and its wait for segment g's DMA
+        "seg_work_us_by_g": {g: round(float(np.median(v)), 3) for g, v in sorted(work_by_g.items())},
+        "seg_wait_us_by_g": {g: round(float(np.median(v)), 3) for g, v in sorted(wait_by_g.items())},
     }
     # per-wave rate (tiles per us of the wave's life) by placement: which waves are slow?
     rate = sc[:, 3] / np.maximum((sc[:, 2] - sc[:, 0]) / 100.0, 1e-3)
