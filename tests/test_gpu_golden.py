@@ -105,6 +105,33 @@ def test_strong_shards_vs_golden(nshards):
     assert files == sizes.size
 
 
+def test_stream_tiles_back_to_back_launches_vs_golden():
+    """The stream-tile scan's asynchronous ST grab (cdc_kernels.hip grab_async:
+    an asm atomic whose result is read a segment later) across back-to-back
+    launches of one plan with no fetch between them (the bench's timed steps),
+    then a fetch: config 4's N = 8 rank-0 batch (35 tiles per scan wave, stream
+    tiles; the library's own report says so), every file's cuts and hashes
+    against the golden digests, twice."""
+    sizes = WL.zipf_sizes()
+    sh = WL.lpt_shard(sizes, 8)[0]
+    lens = sizes[sh]
+    offs = WL.offsets_of(lens)
+    with syncr_amd.Chunker() as ch:
+        buf = syncr_amd.DeviceBuffer(ch, int(lens.sum()))
+        try:
+            buf.gen_corpus(offs, lens, indices=sh.astype(np.uint64))
+            ch.plan(offs, lens, int(lens.sum()))
+            for rep in range(2):
+                for _ in range(4):
+                    ch.launch(buf.ptr, hashed=True)
+                got = ch.fetch(hashed=True)
+                assert ch.last_scan()["kind"] == "stream_tiles", ch.last_scan()
+                p = G.check_files("zipf10k", got, sh, hashed=True)
+                assert p["files"] == sh.size and p["mismatches"] == 0, (rep, p)
+        finally:
+            buf.free()
+
+
 def test_shard_leg_reports_every_shard():
     r = L.shard_leg(0, steps=2, warmup=1, nshards=8)
     assert len(r["shards"]) == 8 and r["parity"]["files"] == 10000 and r["parity"]["mismatches"] == 0, r
