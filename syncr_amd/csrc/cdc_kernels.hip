@@ -941,6 +941,11 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
     uint32_t *tcnt = tlist + TILES * LC;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
     const uint32_t nst = T.nst;
+    // the grid size in a register for the loop (read from the dispatch packet by a
+    // scalar load and an lgkmcnt(0) wait at every segment otherwise)
+    uint32_t grid = gridDim.x;
+    asm volatile("" : "+s"(grid));
+    const bool multi = nst > grid;                 // more STs than waves: the counter hands out the rest
     const int64_t span = (int64_t)T.span;
     // DMA instruction i, lane l fills slot 64 i + l = stream 8 i + l / 8, physical piece l % 8,
     // which holds logical piece (l % 8) ^ ((l / 8) & 7): a per-lane offset fixed for the kernel
@@ -1069,7 +1074,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
                 // one address at launch: the first segment landed 18.7 us after entry, median,
                 // tools/scan_timeline.py)
             } else {
-                nextst = nst > gridDim.x ? gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nst;
+                nextst = multi ? grid + (uint32_t)__builtin_amdgcn_readfirstlane(pend) : nst;
                 more = nextst < nst;
                 if (more) {
                     issue_seg(nextst, 0);
@@ -1079,7 +1084,7 @@ void cdc_scan_st_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
             // the ST grab (grab_async): lane 0 at 4 + blockIdx % 4 in a wave's first ST,
             // at SEGS - 2 in later ones; read at the ST's last segment after its wait
             grab_async(pend, T.ctr, (g == (nth == 0u ? 4u + (blockIdx.x & 3u) : (uint32_t)SEGS - 2u) &&
-                                     nst > gridDim.x) ? 1u : 0u);
+                                     multi) ? 1u : 0u);
             // ---- roll segment g: positions 0..63 drop Pd, later ones this segment's own pairs
             const int64_t lim_rel = span - (int64_t)st * STB;         // ST-relative positions >= lim: not bytes
             const uint32_t relA0 = (uint32_t)lane * L + g * RUN;
