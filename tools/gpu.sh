@@ -9,7 +9,7 @@
 #   tests[|<pytest -k expr>]            product library, pytest -m gpu
 #   devtests|<ENV=V,...>[|<-k expr>]    the GPU suite on libsyncr_cdc_dev.so with a variant forced
 #   smoke                               __graft_entry__.smoke()
-#   bench[|<extra bench.py flags>[|<checkout>]]  the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
+#   bench[|<extra bench.py flags>[|<checkout>[|<ENV=V,...>]]]  the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 #   ab|<workload>|<rounds>[e]|<V1>|<V2>... tools/dip_ab.py variants (dev library) in the driver's condition
 #                                       (rounds suffix e: scan timed by HIP events)
 #   trace|<workload>[|<shard>[|--no-events[|<checkout>]]]  kernel trace of one small-batch leg
@@ -58,7 +58,7 @@ for step in "$@"; do
         tail -c 300 "$out.log"; echo ;;
     bench)
         BROOT=$R/${a[2]:-.}                         # another checkout's bench (e.g. build/r04src: same-box A/B)
-        ( cd "$BROOT" && timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 ${a[1]} ) > "$out.json" \
+        ( cd "$BROOT" && envrun "${a[3]}" timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 ${a[1]} ) > "$out.json" \
             2> "$out.err" || { echo "bench failed rc=$?"; tail -30 "$out.err"; exit 14; }
         python tools/bench_summary.py "$out.json" ;;
     ab)
