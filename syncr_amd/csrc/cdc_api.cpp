@@ -181,6 +181,7 @@ KParams make_kparams(const syncr_cdc_params &p) {
     k.read_cap = p.read_cap;
     k.nt = 1;              // tile bytes are read once: non-temporal loads
     k.nt_out = 0;          // candidate words / cuts: plain stores (non-temporal: dev A/B, no faster)
+    k.dense_blocks = 0;
     // exact alternative resolves, for cross-checks (include/syncr_cdc.h)
     k.resolve_lane = (p.flags & SYNCR_CDC_FLAG_RESOLVE_LANE) ? 1u : 0u;
     k.resolve_noburst = (p.flags & SYNCR_CDC_FLAG_RESOLVE_NOBURST) ? 1u : 0u;
@@ -596,6 +597,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *a = getenv("SYNCR_CDC_DENSE_FUSE")) h->kp.dense_fuse = atoi(a) != 0;           // A/B only
     if (const char *a = getenv("SYNCR_CDC_ST_SEGS")) h->kp.st_segs = (uint32_t)atoi(a);          // A/B only
     if (const char *a = getenv("SYNCR_CDC_NT_OUT")) h->kp.nt_out = atoi(a) != 0;                 // A/B only
+    if (const char *a = getenv("SYNCR_CDC_DENSE_BLOCKS")) h->kp.dense_blocks = (uint32_t)atoi(a);  // A/B only
     if (const char *a = getenv("SYNCR_CDC_TRACE"))                                              // timeline
         if (atoi(a)) CHECK_HIP(h->dbg.ensure(DBG_WORDS * sizeof(uint64_t)));
     if (const char *a = getenv("SYNCR_CDC_SPLIT_SEGC")) h->split_segc = std::max(256, atoi(a));        // A/B only

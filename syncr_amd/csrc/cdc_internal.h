@@ -133,6 +133,7 @@ struct KParams {
     uint32_t st_segs;          // (dev A/B: SYNCR_CDC_ST_SEGS) 9 / 18 / 27 / 36 segments per stream forced; 0: st_segs()
     uint32_t nt_out;           // 1: candidate words and cuts are stored non-temporally (dev A/B:
                                //   SYNCR_CDC_NT_OUT=1; product 0); Tables::nt_out carries it to the kernels
+    uint32_t dense_blocks;     // (dev A/B: SYNCR_CDC_DENSE_BLOCKS) dense-pass grid forced; 0: the product's
 };
 constexpr int RESOLVE_PF = 8;  // product: candidate windows in the resolve walk's LDS ring (PF-1 ahead)
 
@@ -288,7 +289,9 @@ enum { DBG_RES_START = 0, DBG_RES_END = 1, DBG_W_ENTRY = 2, DBG_W_SETUP = 3, DBG
        DBG_NREC = 1024, DBG_FW = DBG_REC + 2 * DBG_NREC, DBG_NFW = 1024, DBG_SCAN = DBG_FW + DBG_NFW,
        DBG_SCAN_N = 4096, DBG_TILE = DBG_SCAN + 4 * DBG_SCAN_N, DBG_TILE_W = 16, DBG_TILE_N = 128,
        DBG_CW = DBG_TILE + DBG_TILE_W * DBG_TILE_N, DBG_NCW = 4096,   // split copy waves: end, start
-       DBG_WORDS = DBG_CW + 2 * DBG_NCW };
+       DBG_DW = DBG_CW + 2 * DBG_NCW, DBG_NDW = 2048,                  // dense-pass waves: entry, end | tiles << 56
+       DBG_DT = DBG_DW + 2 * DBG_NDW, DBG_DT_W = 16, DBG_DT_N = 16,    // their first tiles: issue, landed, rolled, fixed
+       DBG_WORDS = DBG_DT + 4 * DBG_DT_W * DBG_DT_N };
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------
 // A lane TASK is B3_LANE_LEAVES consecutive 1 KiB leaves of one chunk.  A chunk

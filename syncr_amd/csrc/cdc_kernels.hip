@@ -2172,6 +2172,7 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
     constexpr int TILE = tile_bytes(RUN), NQ = (HALO + RUN) / 16, NG = RUN / 16;
     constexpr int BUFD = dense_buf_bytes(RUN, FUSE);
     const int lane = threadIdx.x;
+    if (blockIdx.x < (uint32_t)DBG_NDW) SCAN_STAMP(T, DBG_DW + 2 * blockIdx.x, wall_clock64());
     const uint32_t nd = min(sload_u32(&T.ctr[CTR_DENSE]), T.dense_cap);
     // Block b takes the contiguous list range [b*per, (b+1)*per): the list is
     // in scan order, so a grid stride over it put the whole grid's coarse
@@ -2191,12 +2192,18 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
         tile = sload_u32(&T.dense_list[idx]);
     }
     uint32_t cur_c = tile >> 12, acc_c = 0, ndone = 0;
+    // (dev timeline: the first DBG_DT_N tiles of the first DBG_DT_W blocks)
+    const bool dstamp = blockIdx.x < (uint32_t)DBG_DT_W;
+#define DENSE_STAMP(k, j) do { if (dstamp && (k) < (uint32_t)DBG_DT_N) \
+        SCAN_STAMP(T, DBG_DT + 4 * (DBG_DT_N * blockIdx.x + (k)) + (j), wall_clock64()); } while (0)
+    DENSE_STAMP(0u, 0);
     issue_buf<BUFD, TILE, true>(data, T.span, tile, lds0, lane);
     for (uint32_t next; idx < iend; idx = next) {
         next = idx + 1;
         uint32_t ntile = DENSE_HOLE;
         while (next < iend && (ntile = sload_u32(&T.dense_list[next])) == DENSE_HOLE) ++next;
         wait_vmcnt<0>();                                          // this tile has landed
+        DENSE_STAMP(ndone, 1);
         uint32_t A[NQ * 4], B[NQ * 4];
         {
             const uint4 *la = (const uint4 *)(dbuf + lane * RUN);          // = run start - 64
@@ -2221,13 +2228,18 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
             rr[g] = r;
         });
         for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+        DENSE_STAMP(ndone, 2);
         bool fixed = false;
         if constexpr (FUSE) {
             // a tile whose fix-ups are stored gets its candidates as a position list
             // (dense_pos, 2 B per candidate) instead of the bitmap (TILE / 8 bytes)
             fixed = dense_fixups<RUN>(dbuf, P, T, rr, cnt, idx, t0, lane);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // the fix-ups' LDS reads are done
-            if (next < iend) issue_buf<BUFD, TILE, true>(data, T.span, ntile, lds0, lane);
+            DENSE_STAMP(ndone, 3);
+            if (next < iend) {
+                DENSE_STAMP(ndone + 1u, 0);
+                issue_buf<BUFD, TILE, true>(data, T.span, ntile, lds0, lane);
+            }
             if (!fixed) {
 #pragma unroll
                 for (int g = 0; g < NG; ++g) {
@@ -2251,6 +2263,8 @@ __global__ __launch_bounds__(64) void cdc_dense_packed_kernel(const uint8_t *__r
     }
     if (lane == 0 && acc_c) atomicAdd(&T.coarse[cur_c * COARSE_STRIDE], acc_c);
     if (lane == 0) atomicAdd(&T.split[SPL_DENSE_TILES], ndone);     // real tiles, for the stats
+    if (blockIdx.x < (uint32_t)DBG_NDW) SCAN_STAMP(T, DBG_DW + 2 * blockIdx.x + 1, wall_clock64() | ((uint64_t)ndone << 56));
+#undef DENSE_STAMP
 }
 
 // Compact every tile's candidates into T.cand in position order (one wave per
@@ -4119,7 +4133,8 @@ int scan_blocks_per_cu(ScanGeom g) {
 hipError_t launch_post(const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s, bool dense_inline,
                        uint32_t scan_grid) {
     if (!t.ntiles) return hipSuccess;
-    const uint32_t dblocks = t.dense_cap < 2048u ? (t.dense_cap ? t.dense_cap : 1u) : 2048u;
+    uint32_t dblocks = t.dense_cap < 2048u ? (t.dense_cap ? t.dense_cap : 1u) : 2048u;
+    if (p.dense_blocks) dblocks = p.dense_blocks;                  // (development A/B)
     if (dense_inline) {
         // (development A/B) the scan passed its dense tiles itself
     } else if (t.dense_off) {

@@ -2,7 +2,8 @@
 """Timeline of one resolve launch (development library, SYNCR_CDC_TRACE=1).
 
 The resolve kernel stamps wall_clock64 (Tables::dbg, cdc_internal.h DBG_*):
-the resolve kernel's block 0 start, the largest split file's walker (entry, after its split
+the dense pass's waves (entry, end, and issue / landing / roll end / fix-up end of
+the first tiles of 16 waves), the resolve kernel's block 0 start, the largest split file's walker (entry, after its split
 setup, each block of 64 adopted records, walk end), every split worker's walk
 (start, end) of records < DBG_NREC, and the copy launch's start.  Printed in us from
 the resolve kernel's first wave.
@@ -29,7 +30,43 @@ DBG_W_BLK, DBG_COPY_START, DBG_COPY_END, DBG_REC, DBG_NREC = 8, 248, 249, 256, 1
 DBG_FW, DBG_NFW = DBG_REC + 2 * DBG_NREC, 1024
 DBG_SCAN = DBG_FW + DBG_NFW
 DBG_CW, DBG_NCW = DBG_SCAN + 4 * 4096 + 16 * 128, 4096      # split copy waves: end, start
-WORDS = DBG_CW + 2 * DBG_NCW
+DBG_DW, DBG_NDW = DBG_CW + 2 * DBG_NCW, 2048                   # dense-pass waves: entry, end | tiles << 56
+DBG_DT, DBG_DT_W, DBG_DT_N = DBG_DW + 2 * DBG_NDW, 16, 16       # their first tiles: issue, landed, rolled, fixed
+WORDS = DBG_DT + 4 * DBG_DT_W * DBG_DT_N
+
+
+def dense_timeline(d):
+    """The dense pass's waves, in us from its first wave's entry."""
+    dw = d[DBG_DW:DBG_DW + 2 * DBG_NDW].reshape(-1, 2)
+    live = (dw[:, 0] > 0) & (dw[:, 1] > 0)
+    if not live.any():
+        return
+    mask = (1 << 56) - 1
+    ent = dw[live, 0].astype(np.int64)
+    end = (dw[live, 1] & np.uint64(mask)).astype(np.int64)
+    ntl = (dw[live, 1] >> np.uint64(56)).astype(np.int64)
+    t0 = ent.min()
+    us = lambda v: (v - t0) / 100.0                                    # noqa: E731
+    e, x = us(ent), us(end)
+    print(f"  dense waves ({live.sum()}): entry p50 {np.median(e):.1f} max {e.max():.1f}; end p10 "
+          f"{np.percentile(x, 10):.1f} p50 {np.median(x):.1f} p90 {np.percentile(x, 90):.1f} max {x.max():.1f}; "
+          f"tiles per wave p50 {np.median(ntl):.0f} max {ntl.max()}")
+    dt = d[DBG_DT:DBG_DT + 4 * DBG_DT_W * DBG_DT_N].reshape(DBG_DT_W, DBG_DT_N, 4).astype(np.int64)
+    lat, roll, fix, gap = [], [], [], []
+    for w in range(DBG_DT_W):
+        for k in range(DBG_DT_N):
+            iss, land, rl, fx = dt[w, k]
+            if not (iss and land and rl and fx):
+                continue
+            lat.append((land - iss) / 100.0)
+            roll.append((rl - land) / 100.0)
+            fix.append((fx - rl) / 100.0)
+            if k + 1 < DBG_DT_N and dt[w, k + 1, 1]:
+                gap.append((dt[w, k + 1, 1] - fx) / 100.0)
+    if lat:
+        q = lambda v: f"p50 {np.median(v):.2f} p90 {np.percentile(v, 90):.2f} max {max(v):.2f}"   # noqa: E731
+        print(f"  dense tiles ({len(lat)} of {DBG_DT_W} waves): issue->landed {q(lat)}; roll {q(roll)}; "
+              f"fix-ups {q(fix)}; fix-ups end->next landed {q(gap) if gap else '-'}")
 
 
 def main():
@@ -99,6 +136,7 @@ def main():
                   f"max {cs.max():.1f}; durations p50 {np.percentile(dur, 50):.1f} p90 {np.percentile(dur, 90):.1f} "
                   f"max {dur.max():.1f}; waves by wid/1024: "
                   + ", ".join(f"{np.median(dur[(np.nonzero(live)[0] // 1024) == b]):.1f}" for b in range(4)))
+        dense_timeline(d)
         fw = d[DBG_FW:DBG_FW + DBG_NFW]
         ends = sorted(((us(v), k) for k, v in enumerate(fw) if v), reverse=True)[:6]
         order = np.argsort(-sizes.astype(np.int64), kind="stable")
