@@ -381,7 +381,8 @@ __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
 // loads (LD_PLAIN, development A/B only), the cooperative LDS-DMA loader one
 // 64-byte block per task per issue round (LD_COOP64), or two blocks (one
 // 128-byte run) per task per round (LD_PAIR).
-constexpr int LD_PLAIN = 0, LD_COOP64 = 1, LD_PAIR = 2;
+constexpr int LD_PLAIN = 0, LD_PAIR = 2;
+[[maybe_unused]] constexpr int LD_COOP64 = 1;   // (development library only)
 
 // ---------------------------------------------------------------------------
 // Cooperative block loader (COOP): the wave steps through block index t in

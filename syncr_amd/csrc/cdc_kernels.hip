@@ -591,6 +591,9 @@ __host__ __device__ constexpr bool scan_stream_tiles(uint32_t ntiles, uint32_t g
 // cycles per tile and the group counter balances the CUs.
 constexpr uint32_t CU_GROUP = 32;            // tiles per group
 constexpr uint32_t CU_NSLOT = 8;             // group ring in LDS (local group j in slot j % CU_NSLOT)
+template <int RUN>                           // (below: the scan wave's own exact pass over a dense tile)
+__device__ __forceinline__ void scan_dense_tile(const uint8_t *__restrict__ data, const KParams &P,
+                                                const Tables &T, uint32_t tile, int64_t t0, int lane);
 template <int RUN, int MODE, int WPB = 1>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu((MODE & 32) ? 3 : 1)))
 void cdc_scan_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
