@@ -334,21 +334,28 @@ def run_legs(args, dev_id: int, dbuf, offs, lens, idx, rank_span: int, out: dict
         out["dense1"] = timed("dense1", L.dense1_leg, dev_id, k, w)
     out["h2d_probe"] = timed("h2d_probe", L.h2d_probe, dev_id)
     if host is not None:
-        out["ingest"] = timed("ingest", L.ingest_leg, host, offs, lens, idx, dev_id)
-        parity["ingest_multi_device"] = out["ingest"].get("multi_device", {}).get("parity")
-        out["ingest_files"] = timed("ingest_files", L.ingest_files_leg, host, offs, lens, idx, dev_id)
-        out["ingest_zero_copy"] = timed("ingest_zero_copy", L.ingest_zero_copy_leg, host, offs, lens, idx, dev_id)
+        # end to end from host memory / files, driven from C++ (benchlib/e2e_driver.cpp): the
+        # shim's per-file call site, the batched walk, and the ingest entry points
+        from benchlib import e2e as E
+        e2e = timed("e2e", E.legs, host, offs, lens, idx, dev_id)
+        for key in E.MODES:
+            out[key] = e2e.get(key, {"error": e2e.get("error", "not run")})
+        md = timed("ingest_multi_device", L.ingest_multi_device_leg, host, offs, lens, idx, dev_id)
+        parity["ingest_multi_device"] = md.get("parity", md)
         h2d = out["h2d_probe"].get("h2d", {}).get("best_gbs")
-        for key in ("ingest", "ingest_files", "ingest_zero_copy"):
+        cpu1 = (out.get("cpu_baseline") or {}).get("value")
+        for key in E.MODES:
             v = out[key].get("value")
             if h2d and v:          # the end-to-end rate on its link ceiling (GiB/s -> GB/s)
                 out[key]["frac_of_h2d"] = round(v * 2**30 / 1e9 / h2d, 4)
+            if cpu1 and v:         # next to the reference loop's one-thread rate (cpu_baseline.value)
+                out[key]["vs_cpu_one_thread"] = round(v / cpu1, 2)
     del host
     # one summary: every parity check of the line
     checks = []
     for name, p in list(parity.items()) + [(f"{s}.parity", out.get(s, {}).get("parity")) for s in
                                             ("shard8", "uniform1k", "dedup", "dense", "dense1", "ingest",
-                                             "ingest_files", "ingest_zero_copy")] + \
+                                             "ingest_files", "ingest_zero_copy", "shim_per_file", "shim_walk")] + \
             [(f"{s}.parity_hashed", out.get(s, {}).get("parity_hashed")) for s in ("dedup", "dense", "dense1")] + \
             [("dense1.parity_ideal", out.get("dense1", {}).get("parity_ideal"))]:
         if isinstance(p, dict) and "mismatches" in p:

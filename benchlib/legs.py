@@ -452,168 +452,23 @@ def ideal_leg(dbuf, offs, lens, idx, device: int) -> dict:
     return G.check_files("zipf10k", cuts, idx, semantics="ideal")
 
 
-def ingest_leg(host: np.ndarray, offs, lens, idx, device: int, reps: int = 2, multi_files: int = 2000) -> dict:
-    """End to end (north_star: the path starts and ends in host memory): the
-    zipf10k corpus's files in ordinary host memory -> syncr_ingest_submit
-    (copied into pinned staging) -> H2D -> scan + resolve + BLAKE3 -> one
-    ChunkInfo list per file back on the host, in submission order.  Every
-    file is checked against the golden digests (cuts and hashes).  Then the
-    multi-device front end (syncr_ingest_open_multi, devices {d, d}) on the
-    first `multi_files` files, checked the same way."""
+def ingest_multi_device_leg(host: np.ndarray, offs, lens, idx, device: int, multi_files: int = 2000) -> dict:
+    """The multi-device front end (syncr_ingest_open_multi, devices {d, d}) on
+    the first `multi_files` zipf10k files from host memory, every file's cuts and
+    hashes against the golden digests (a parity leg: the timed end-to-end legs
+    are driven from C++, benchlib/e2e.py)."""
     import syncr_amd
-    files = [host[int(o): int(o + n)] for o, n in zip(offs.tolist(), lens.tolist())]
-    span = int(lens.sum())
+    nm = min(multi_files, int(lens.size))
     res: dict = {}
-
-    def on_file(tag, status, a):
-        res[tag] = (status, a)
-
-    out = {}
-    with syncr_amd.Ingest(device=device, batch_bytes=256 << 20, depth=3, copy_threads=16, on_file=on_file) as g:
-        best = None
-        for _ in range(reps):
-            res.clear()
-            t0 = time.perf_counter()
-            for i, f in enumerate(files):
-                g.submit(f, i)
-            g.flush()
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
-        st = g.stats()
-        stages = g.timing()
-    got = [res[i][1] for i in range(len(files))]
-    out.update({"value": round(span / best / 2**30, 3), "unit": "GiB/s", "seconds": round(best, 4),
-                "bytes": span, "files": len(files), "batches_per_pass": st["batches"] // reps,
-                "path": "syncr_ingest_submit from pageable host memory (16 copy threads into pinned staging, "
-                        "256 MiB batches, depth 3) -> hipMemcpyAsync H2D -> chunk + BLAKE3 -> per-file "
-                        "ChunkInfo callbacks; best of %d passes" % reps,
-                "status_nonzero": int(sum(res[i][0] != 0 for i in range(len(files)))),
-                "host_stage_seconds": {k: round(v / reps, 4) for k, v in stages.items()},
-                "host_stage_note": ("syncr_ingest_timing per pass: copy (pageable -> pinned staging, %d threads), "
-                                    "seal (plan + H2D/kernel enqueue), wait (for a batch's results: H2D + kernels + "
-                                    "D2H still running), deliver; all on the caller's thread, so copy + seal + wait + "
-                                    "deliver ~= the pass: wait ~ 0 means the host side bounds the rate" % 16),
-                "parity": G.check_files("zipf10k", got, idx, hashed=True)})
-    nm = min(multi_files, len(files))
-    res.clear()
     with syncr_amd.Ingest(devices=[device, device], batch_bytes=64 << 20, depth=2, copy_threads=8,
-                          on_file=on_file) as g:
+                          on_file=lambda t, st, a: res.__setitem__(t, a)) as g:
         for i in range(nm):
-            g.submit(files[i], i)
+            g.submit(host[int(offs[i]): int(offs[i] + lens[i])], i)
         g.flush()
         ds = g.device_stats()
-    got = [res[i][1] for i in range(nm)]
-    out["multi_device"] = {"devices": [device, device], "per_device_files": [d["files"] for d in ds],
-                           "parity": G.check_files("zipf10k", got, idx[:nm], hashed=True)}
-    return out
-
-
-def ingest_zero_copy_leg(host: np.ndarray, offs, lens, idx, device: int, reps: int = 2) -> dict:
-    """End to end through the zero-copy entry points: for every zipf10k file the
-    caller reserves its bytes in pinned staging (syncr_ingest_reserve), writes
-    them there itself (here: from the same host bytes as the `ingest` leg, big
-    files split over 16 caller threads) and commits (syncr_ingest_commit); the
-    library copies nothing.  Every file is checked against the golden digests
-    (cuts and hashes).  `caller_fill_seconds` is the caller's own writing."""
-    from concurrent.futures import ThreadPoolExecutor
-    import syncr_amd
-    files = [host[int(o): int(o + n)] for o, n in zip(offs.tolist(), lens.tolist())]
-    span = int(lens.sum())
-    res: dict = {}
-    piece = 4 << 20
-
-    def fill(dst, src, ex):
-        if src.size <= piece:
-            np.copyto(dst, src)
-            return
-        list(ex.map(lambda a: np.copyto(dst[a:a + piece], src[a:a + piece]), range(0, src.size, piece)))
-
-    best, fill_s = None, 0.0
-    with ThreadPoolExecutor(16) as ex, syncr_amd.Ingest(device=device, batch_bytes=256 << 20, depth=3,
-                                                        copy_threads=16,
-                                                        on_file=lambda t, st, a: res.__setitem__(t, (st, a))) as g:
-        for _ in range(reps):
-            res.clear()
-            tf = 0.0
-            t0 = time.perf_counter()
-            for i, f in enumerate(files):
-                dst = g.reserve(f.size)
-                t1 = time.perf_counter()
-                fill(dst, f, ex)
-                tf += time.perf_counter() - t1
-                g.commit(i)
-            g.flush()
-            dt = time.perf_counter() - t0
-            if best is None or dt < best:
-                best, fill_s = dt, tf
-        stages = g.timing()
-    got = [res[i][1] for i in range(len(files))]
-    return {"value": round(span / best / 2**30, 3), "unit": "GiB/s", "seconds": round(best, 4), "bytes": span,
-            "files": len(files),
-            "path": "syncr_ingest_reserve -> the caller writes the file's bytes into pinned staging (16 caller "
-                    "threads for big files) -> syncr_ingest_commit -> H2D -> chunk + BLAKE3 -> per-file ChunkInfo; "
-                    "256 MiB batches, depth 3; best of %d passes" % reps,
-            "caller_fill_seconds": round(fill_s, 4),
-            "status_nonzero": int(sum(res[i][0] != 0 for i in range(len(files)))),
-            "host_stage_seconds": {k: round(v / reps, 4) for k, v in stages.items()},
-            "parity": G.check_files("zipf10k", got, idx, hashed=True)}
-
-
-def ingest_files_leg(host: np.ndarray, offs, lens, idx, device: int, gib: float = 2.0, reps: int = 2) -> dict:
-    """End to end FROM FILES, as the reference reads them (File::open + reads,
-    file_operations.rs:737-745,776): the first zipf10k files up to `gib` GiB
-    are written to local disk (a temporary directory), then every file goes
-    through syncr_ingest_submit_file (pread straight into pinned staging ->
-    H2D -> chunk + BLAKE3 -> per-file ChunkInfo callbacks); every file is
-    checked against the golden digests.  The files were just written and
-    fsync'ed, so they are served from the page cache, clean (this process cannot
-    drop it; dirty pages under writeback during the timed passes once read at
-    10.7 GiB/s instead of ~37)."""
-    import shutil
-    import tempfile
-    import syncr_amd
-    take, tot = [], 0
-    for j in range(lens.size):
-        if tot >= gib * 2**30:
-            break
-        take.append(j)
-        tot += int(lens[j])
-    d = tempfile.mkdtemp(prefix="syncr_ingest_files_")
-    res: dict = {}
-    try:
-        paths = []
-        for j in take:
-            pth = os.path.join(d, f"f{j:05d}.bin")
-            with open(pth, "wb") as f:
-                f.write(host[int(offs[j]): int(offs[j] + lens[j])].tobytes())
-                f.flush()
-                os.fsync(f.fileno())       # clean pages: no writeback of them during the timed reads
-            paths.append(pth)
-        best = None
-        with syncr_amd.Ingest(device=device, batch_bytes=256 << 20, depth=3, copy_threads=16,
-                              on_file=lambda t, st, a: res.__setitem__(t, (st, a))) as g:
-            for _ in range(reps):
-                res.clear()
-                t0 = time.perf_counter()
-                for k, pth in enumerate(paths):
-                    g.submit_file(pth, k)
-                g.flush()
-                dt = time.perf_counter() - t0
-                best = dt if best is None else min(best, dt)
-            stages = g.timing()
-    finally:
-        shutil.rmtree(d, ignore_errors=True)
-    got = [res[k][1] for k in range(len(take))]
-    return {"value": round(tot / best / 2**30, 3), "unit": "GiB/s", "seconds": round(best, 4), "bytes": tot,
-            "files": len(take),
-            "path": "files on local disk (page-cache resident and clean: just written, fsync'ed) -> "
-                    "syncr_ingest_submit_file (open + "
-                    "fstat on the caller, pread into pinned staging on 16 pool threads, 2 MiB per task, the caller "
-                    "goes on to the next file) -> H2D -> chunk + BLAKE3 -> per-file ChunkInfo; best of %d "
-                    "passes" % reps,
-            "status_nonzero": int(sum(res[k][0] != 0 for k in range(len(take)))),
-            "host_stage_seconds": {k: round(v / reps, 4) for k, v in stages.items()},
-            "parity": G.check_files("zipf10k", got, idx[np.array(take, np.int64)], hashed=True)}
+    got = [res[i] for i in range(nm)]
+    return {"devices": [device, device], "per_device_files": [d["files"] for d in ds],
+            "parity": G.check_files("zipf10k", got, idx[:nm], hashed=True)}
 
 
 def ingest_multi_leg(device: int = 0, max_file: int = 4 * M, nfiles: int = 1500) -> dict:

@@ -212,12 +212,18 @@ int32_t syncr_ingest_open_multi(const int32_t *devices, uint32_t ndevices, const
 int32_t syncr_ingest_submit(syncr_ingest *g, const uint8_t *data, uint64_t len, uint64_t tag);
 /* a file read with pread straight into pinned staging: opened and sized on the
  * calling thread, read by the copy_threads pool while the caller goes on (the
- * batch waits for its reads when it is sealed) */
+ * batch waits for its reads when it is sealed).  A file's descriptor stays open
+ * until its reads are done; at most 64 files per device are open at once (past
+ * that, submit_file runs queued reads on the calling thread, or waits, before it
+ * opens the next file), so a walk of many small files never exhausts the
+ * process's descriptors. */
 int32_t syncr_ingest_submit_file(syncr_ingest *g, const char *path, uint64_t tag);
 /* zero-copy: reserve `len` bytes of pinned staging, fill them, then commit */
 int32_t syncr_ingest_reserve(syncr_ingest *g, uint64_t len, uint8_t **dst);
 int32_t syncr_ingest_commit(syncr_ingest *g, uint64_t tag);
-/* seal the current batch and deliver every outstanding file */
+/* seal the current batch and deliver every outstanding file; staging grown
+ * past 4 x batch_bytes for an oversized file is released (an idle pipeline
+ * holds at most depth x 4 x batch_bytes of pinned and device memory) */
 int32_t syncr_ingest_flush(syncr_ingest *g);
 /* [files, bytes, batches, chunks] so far */
 int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4);

@@ -77,6 +77,11 @@ __device__ __forceinline__ void st_cut(DevCut *p, const DevCut &v, uint32_t nt) 
 //    iteration and no join copy reads its register before it returned.  hipcc's
 //    atomicAdd waited for the result at once (the atomic optimizer spreads it over
 //    the lanes), i.e. for the DMAs issued just before it.
+// Invariant (hipcc cannot see it): between the asm atomic and the next
+// vmcnt(0) no instruction may read, copy or spill `pend`'s register, or the
+// scan reads a stale work index.  tests/test_codeobj.py disassembles the product
+// code object and checks every path from each grab to its wait, and that the
+// scans spill no VGPRs; a compiler update that breaks it fails that test.
 __device__ __forceinline__ void wait_all_pend(uint32_t &pend) {
     __builtin_amdgcn_s_waitcnt(0x0F70);                               // vmcnt(0)
     asm volatile("" : "+v"(pend) : : "memory");

@@ -204,6 +204,13 @@ struct Slot {
 
 constexpr uint64_t PAR_COPY = 4ull << 20;   // copies above this are split over the pool
 constexpr uint64_t PIECE = 2ull << 20;
+// Files whose reads are still queued or running keep their descriptor open.
+// submit_file opens the next file only while fewer than this many are open
+// (it helps with the queued reads, or waits, otherwise), so a walk of many
+// small files on slow storage never runs the process out of descriptors --
+// the reference limits itself the same way, 8 files at a time through its
+// walk's semaphore (file_operations.rs:596-599, streaming.rs:91).
+constexpr uint32_t MAX_OPEN_READS = 64;
 
 typedef void (*deliver_fn)(void *owner, uint64_t tag, int32_t status, const syncr_chunk_info *chunks, uint64_t n);
 
@@ -232,9 +239,10 @@ struct Pipe {
     // pinned staging, file reads into it, seal (plan + H2D and kernel enqueue),
     // waiting for a batch's results (fetch), per-file delivery
     std::atomic<uint64_t> tns[5] = {{0}, {0}, {0}, {0}, {0}};
-    // completion of the pool's file reads (Slot::pending)
+    // completion of the pool's file reads (Slot::pending) and of open files
     std::mutex rmu;
     std::condition_variable rcv;
+    uint32_t open_reads = 0;            // files with reads outstanding (guarded by rmu)
 };
 
 enum { T_COPY = 0, T_READ = 1, T_SEAL = 2, T_WAIT = 3, T_DELIVER = 4 };
@@ -319,6 +327,7 @@ int32_t ensure_slot(Pipe *g, Slot &s, uint64_t bytes) {
 // (Shrinking right after each oversized file made a stream of them pay a
 // device-synchronising free and a fresh pin per file: ADVICE r4.)
 constexpr uint32_t SHRINK_AFTER = 4;
+constexpr uint64_t TRIM_ON_FLUSH = 4;       // flush shrinks slots larger than this many batches
 void shrink_slot(Pipe *g, Slot &s, bool oversized) {
     if (s.cap <= std::max<uint64_t>(g->batch, 64) || s.inflight || s.used) return;
     s.small_uses = oversized ? 0u : s.small_uses + 1u;
@@ -604,9 +613,25 @@ void read_piece(PendingRead &pr, unsigned i) {
     pr.got[i] = pos - a;
 }
 
+// Block until fewer than MAX_OPEN_READS files have reads outstanding, running
+// queued reads on this thread meanwhile.
+void wait_read_room(Pipe *g) {
+    StageTimer tr(g->tns[T_READ]);
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> l(g->rmu);
+            if (g->open_reads < MAX_OPEN_READS) return;
+        }
+        if (g->pool && g->pool->run_one()) continue;
+        std::unique_lock<std::mutex> l(g->rmu);
+        g->rcv.wait_for(l, std::chrono::microseconds(200), [&] { return g->open_reads < MAX_OPEN_READS; });
+    }
+}
+
 int32_t pipe_submit_file(Pipe *g, const char *path, uint64_t tag) {
     if (g->reserved) return SYNCR_CDC_ESTATE;
     if (g->error) return g->error;
+    wait_read_room(g);
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     struct stat st;
     int32_t status = 0;
@@ -679,13 +704,18 @@ int32_t pipe_submit_file(Pipe *g, const char *path, uint64_t tag) {
         std::lock_guard<std::mutex> l(g->rmu);
         pr.left = pieces;
         s.pending += pieces;
+        g->open_reads++;
     }
     for (unsigned i = 0; i < pieces; i++) {
         auto task = [g, &s, &pr, i] {
             read_piece(pr, i);
             std::lock_guard<std::mutex> l(g->rmu);            // (pr may be gone once pending drops)
-            if (--pr.left == 0) close(pr.fd);
-            if (--s.pending == 0) g->rcv.notify_all();
+            bool wake = false;
+            if (--pr.left == 0) {
+                close(pr.fd);
+                wake = g->open_reads-- == MAX_OPEN_READS;     // a submit_file may be waiting for room
+            }
+            if (--s.pending == 0 || wake) g->rcv.notify_all();
         };
         if (g->pool) g->pool->post(task);
         else task();
@@ -705,6 +735,15 @@ int32_t pipe_flush(Pipe *g) {
         if (rc) return rc;
     }
     g->cur = (g->cur + 1) % n;
+    // An idle pipeline keeps at most TRIM_ON_FLUSH x batch_bytes per slot: a
+    // slot grown past that for one huge file is shrunk now, not after
+    // SHRINK_AFTER more batches that may never come (a pooled per-file
+    // pipeline can sit idle for the rest of the process).
+    for (Slot &s : g->slots)
+        if (s.cap > TRIM_ON_FLUSH * std::max<uint64_t>(g->batch, 64)) {
+            s.small_uses = SHRINK_AFTER;
+            shrink_slot(g, s, false);
+        }
     return SYNCR_CDC_OK;
 }
 

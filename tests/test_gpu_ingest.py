@@ -381,3 +381,57 @@ def test_read_fault_keeps_reference_prefix(tmp_path, devices):
         assert np.array_equal(arr["len"].astype(np.uint64), e - starts), tag
         hs = O.blake3_batch(d, starts, e - starts, nthreads=8) if e.size else np.zeros((0, 32), np.uint8)
         assert np.array_equal(arr["hash"], hs), tag
+
+
+FD_CHILD = r'''
+import json, os, resource, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import syncr_amd
+from oracle import oracle as O
+paths = sys.argv[2:]
+res = {}
+with syncr_amd.Ingest(batch_bytes=64 << 20, depth=2, copy_threads=2,
+                      on_file=lambda t, st, a: res.__setitem__(t, (st, a))) as g:
+    open_now = len(os.listdir("/proc/self/fd"))
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    lim = open_now + 80                     # the pipeline's 64 open reads + headroom, far below len(paths)
+    resource.setrlimit(resource.RLIMIT_NOFILE, (lim, hard))
+    for i, p in enumerate(paths):
+        g.submit_file(p, i)
+    g.flush()
+bad = 0
+for i, p in enumerate(paths):
+    st, a = res[i]
+    data = np.fromfile(p, np.uint8)
+    ends = O.chunk_production(data)
+    got = (a["offset"].astype(np.uint64) + a["len"].astype(np.uint64))
+    bad += st != 0 or not np.array_equal(got, ends.astype(np.uint64))
+print(json.dumps({"files": len(paths), "bad": int(bad), "limit": lim,
+                  "statuses": sorted({int(res[i][0]) for i in range(len(paths))})}))
+'''
+
+
+def test_submit_file_bounded_open_files(tmp_path):
+    """ADVICE r5: submit_file keeps a file's descriptor until its reads finish;
+    with reads queued faster than one pool thread serves them, the open files
+    are capped (MAX_OPEN_READS = 64 per pipeline: submit_file helps with the
+    queued reads or waits), so 3000 files go through a process whose descriptor
+    limit is 80 above what it has open, each with status 0 and the oracle's
+    cuts -- the reference opens one file at a time (file_operations.rs:599-605)
+    and lists every file."""
+    import json
+    import os
+    import subprocess
+    import sys
+    rng = np.random.default_rng(11)
+    paths = []
+    for i in range(3000):
+        p = tmp_path / f"f{i:05d}"
+        p.write_bytes(O.xorshift_bytes(7000 + i, int(rng.integers(1, 24 << 10))).tobytes())
+        paths.append(str(p))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", FD_CHILD, root, *paths], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["files"] == 3000 and out["bad"] == 0 and out["statuses"] == [0], out

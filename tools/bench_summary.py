@@ -13,11 +13,14 @@ def main():
     print("value", d["value"], "ms", d["ms_per_step"], "frac", r["frac"], "kernel", r.get("kernel"),
           "traffic", r.get("traffic"), "hashed", (d.get("hashed") or {}).get("value"))
     print("parity", json.dumps(d["parity"].get("summary")))
-    for k in ("uniform1k", "dedup", "dense", "dense1", "ingest", "ingest_files", "ingest_zero_copy", "h2d_probe"):
+    for k in ("uniform1k", "dedup", "dense", "dense1", "ingest", "ingest_files", "ingest_zero_copy", "shim_per_file",
+              "shim_walk", "h2d_probe"):
         v = d.get(k) or {}
         if v:
             print(k, {x: v.get(x) for x in ("value", "ms_per_step", "scan_ms", "scan_frac", "step_frac", "dense_ms",
-                                            "resolve_ms", "frac_of_h2d", "host_stage_seconds", "error") if x in v})
+                                            "resolve_ms", "frac_of_h2d", "vs_cpu_one_thread", "latency_us", "in_walk_order",
+                                            "host_stage_seconds", "error") if x in v},
+                  "parity_mism", (v.get("parity") or {}).get("mismatches"))
     s8 = d.get("shard8") or {}
     print("shard8", {x: s8.get(x) for x in ("mean_step_frac", "mean_scan_frac", "max_ms_per_step", "projected_value",
                                             "error")})
