@@ -3,8 +3,9 @@
 //!
 //! Drop this file and `chunking_gpu_ffi.rs` into syncr's `src/`, apply
 //! `integration/file_operations.diff` (adds the `gpu` cargo feature, the
-//! `build.rs` link step and the call site) and build with `--features gpu`.
-//! Without the feature syncr is unchanged.
+//! `build.rs` link step and the two call sites: the batched walk in
+//! traverse_and_stream, `GpuWalk`, and compute_file_chunks per file) and build
+//! with `--features gpu`.  Without the feature syncr is unchanged.
 //!
 //! What it replaces: the rollsum loop of compute_file_chunks -- a fresh
 //! `Bup::new_with_chunk_bits(CHUNK_BITS)` per chunk (:748), `find_chunk_edge`
@@ -28,8 +29,10 @@
 
 use std::collections::VecDeque;
 use std::ffi::{CStr, CString};
+use std::fs;
 use std::os::raw::c_void;
 use std::os::unix::ffi::OsStrExt;
+use std::os::unix::fs::MetadataExt;
 use std::path::{Path, PathBuf};
 use std::sync::atomic::{AtomicUsize, Ordering};
 use std::sync::Mutex;
@@ -37,7 +40,7 @@ use std::sync::Mutex;
 use tracing::warn;
 
 use crate::chunking;
-use crate::protocol::types::ChunkInfo;
+use crate::protocol::types::{ChunkInfo, FileSystemEntry, FileSystemEntryType};
 use crate::serve::DumpState;
 use crate::util;
 
@@ -315,14 +318,233 @@ pub async fn compute_file_chunks_gpu(path: &Path, state: &DumpState) -> Option<V
         }
         Err(_) => return None,
     };
-    if res.status != 0 {
-        // open / first read failed (:727-744: no chunks) or a later read failed
-        // (:776-782: the chunks cut before it are kept)
-        let err = std::io::Error::from_raw_os_error(-res.status);
-        warn!("Error reading file {}: {}", path.display(), err);
-    }
+    warn_read_status(path, &res);
     for c in &res.chunks {
         state.add_chunk(util::hash_to_base64(&c.hash), path.to_path_buf(), c.offset, c.size as usize).await;
     }
     Some(res.chunks)
+}
+
+/// The reference's warning for a file the engine could not read completely
+/// (its status is -errno).  With no chunks the open (:730) or the first read
+/// (:741) failed: the two are told apart by opening the file again (only on
+/// this error path).  With chunks a later read failed (:780) and the chunks cut
+/// before it are kept, as the reference's loop keeps them (:776-782): a failed
+/// later read always follows a first read of >= 1 byte, which yields a chunk.
+fn warn_read_status(path: &Path, res: &FileResult) {
+    if res.status == 0 {
+        return;
+    }
+    let err = std::io::Error::from_raw_os_error(-res.status);
+    if !res.chunks.is_empty() {
+        warn!("Error reading file {}: {}", path.display(), err);
+    } else if fs::File::open(path).is_err() {
+        warn!("Cannot open file {}: {}", path.display(), err);
+    } else {
+        warn!("Cannot read file {}: {}", path.display(), err);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The walk's call site: traverse_and_stream (file_operations.rs:544-715), see
+// integration/file_operations.diff.  Instead of awaiting compute_file_chunks
+// per file (:599-605), every regular file goes to ONE batched pipeline over all
+// GPUs of the node, and the entries are sent (:707) in the walk's order as the
+// files' ChunkInfo lists come back.
+// ---------------------------------------------------------------------------
+
+/// The walk's pipeline: 256 MiB staging batches (~5 ms of H2D each), three in
+/// flight (reads of one, H2D + kernels of another, results of a third), 16
+/// threads for the reads into pinned staging.
+const WALK_BATCH_BYTES: u64 = 256 << 20;
+const WALK_DEPTH: u32 = 3;
+const WALK_COPY_THREADS: u32 = 16;
+
+/// The FileSystemEntry traverse_and_stream builds for a file, symlink or
+/// directory (:608-620, :668-680, :683-695), chunks still empty.
+pub fn walk_entry(path: &Path, relative_path: PathBuf, meta: &fs::Metadata) -> FileSystemEntry {
+    let (entry_type, size, target) = if meta.is_file() {
+        (FileSystemEntryType::File, meta.size(), None)
+    } else if meta.is_symlink() {
+        (FileSystemEntryType::SymLink, 0, fs::read_link(path).ok())
+    } else {
+        (FileSystemEntryType::Directory, 0, None)
+    };
+    FileSystemEntry {
+        entry_type,
+        path: relative_path,
+        mode: meta.mode(),
+        user_id: meta.uid(),
+        group_id: meta.gid(),
+        created_time: meta.ctime() as u32,
+        modified_time: meta.mtime() as u32,
+        size,
+        target,
+        needs_data_transfer: None,
+        chunks: Vec::new(),
+    }
+}
+
+/// What the walk sends next (pop_ready).
+pub enum WalkItem {
+    /// the entry, complete (a file's chunks filled in, each registered with
+    /// DumpState::add_chunk)
+    Ready(FileSystemEntry),
+    /// a file the engine could not chunk (it failed): the caller runs the
+    /// rollsum loop on the path and sends the entry with those chunks
+    Cpu(FileSystemEntry, PathBuf),
+}
+
+enum Slot {
+    Ready,
+    Waiting,
+    Done(FileResult),
+    Cpu,
+}
+
+struct Queued {
+    entry: FileSystemEntry,
+    path: PathBuf,
+    slot: Slot,
+}
+
+/// The batched walk.  Entries are queued in walk order; a file's entry is
+/// ready once its result is back, and pop_ready only ever hands out the head
+/// of the queue, so the listing's order is the reference's.  The pipeline's
+/// blocking calls run on tokio's blocking pool (spawn_blocking), moving the
+/// pipeline there and back: one thread uses it at a time.
+pub struct GpuWalk {
+    pipe: Option<GpuPipeline>,
+    queue: VecDeque<Queued>,
+    /// walk positions of the submitted files still without a result, in
+    /// submission order = the order the pipeline delivers them
+    waiting: VecDeque<u64>,
+    /// entries popped so far (walk position of the queue's head)
+    popped: u64,
+}
+
+impl GpuWalk {
+    /// A pipeline over every GPU of the node; None (the walk then awaits the
+    /// rollsum loop per file, as the reference does) when there is none.
+    pub async fn open() -> Option<GpuWalk> {
+        let opened = tokio::task::spawn_blocking(|| {
+            GpuPipeline::open_all_devices(WALK_BATCH_BYTES, WALK_DEPTH, WALK_COPY_THREADS)
+        })
+        .await;
+        match opened {
+            Ok(Ok(pipe)) => Some(GpuWalk { pipe: Some(pipe), queue: VecDeque::new(), waiting: VecDeque::new(), popped: 0 }),
+            Ok(Err(e)) => {
+                warn!("GPU chunking unavailable ({}); chunking on the CPU", e);
+                None
+            }
+            Err(_) => None,
+        }
+    }
+
+    /// A regular file met by the walk: submitted to the pipeline, which reads
+    /// it on its own threads (and may run a full batch and deliver earlier
+    /// files meanwhile).
+    pub async fn push_file(&mut self, path: PathBuf, entry: FileSystemEntry) {
+        let pos = self.popped + self.queue.len() as u64;
+        let mut pipe = match self.pipe.take() {
+            Some(p) => p,
+            None => {
+                self.queue.push_back(Queued { entry, path, slot: Slot::Cpu });
+                return;
+            }
+        };
+        self.queue.push_back(Queued { entry, path: path.clone(), slot: Slot::Waiting });
+        self.waiting.push_back(pos);
+        let done = tokio::task::spawn_blocking(move || {
+            let r = pipe.submit_file(&path, pos);
+            (pipe, r)
+        })
+        .await;
+        match done {
+            Ok((pipe, r)) => {
+                self.pipe = Some(pipe);
+                self.collect();
+                if let Err(e) = r {
+                    self.engine_failed(e);
+                }
+            }
+            Err(_) => self.engine_failed(GpuError(SYNCR_CDC_EIO)),   // the pipeline went down with the task
+        }
+    }
+
+    /// A directory or symlink entry: sent in its place in the walk's order.
+    pub fn push_entry(&mut self, entry: FileSystemEntry) {
+        self.queue.push_back(Queued { entry, path: PathBuf::new(), slot: Slot::Ready });
+    }
+
+    /// The head of the queue once it is ready, in walk order.
+    pub async fn pop_ready(&mut self, state: &DumpState) -> Option<WalkItem> {
+        match self.queue.front() {
+            Some(q) if !matches!(q.slot, Slot::Waiting) => {}
+            _ => return None,
+        }
+        let Queued { mut entry, path, slot } = self.queue.pop_front()?;
+        self.popped += 1;
+        match slot {
+            Slot::Done(res) => {
+                warn_read_status(&path, &res);
+                for c in &res.chunks {
+                    state.add_chunk(util::hash_to_base64(&c.hash), path.clone(), c.offset, c.size as usize).await;
+                }
+                entry.chunks = res.chunks;
+                Some(WalkItem::Ready(entry))
+            }
+            Slot::Cpu => Some(WalkItem::Cpu(entry, path)),
+            Slot::Ready | Slot::Waiting => Some(WalkItem::Ready(entry)),
+        }
+    }
+
+    /// The walk is over: flush the pipeline so that every entry becomes ready.
+    pub async fn finish(&mut self) {
+        let mut pipe = match self.pipe.take() {
+            Some(p) => p,
+            None => return,
+        };
+        let done = tokio::task::spawn_blocking(move || {
+            let r = pipe.flush();
+            (pipe, r)
+        })
+        .await;
+        match done {
+            Ok((pipe, r)) => {
+                self.pipe = Some(pipe);
+                self.collect();
+                if let Err(e) = r {
+                    self.engine_failed(e);
+                } else if !self.waiting.is_empty() {
+                    self.engine_failed(GpuError(SYNCR_CDC_EIO));   // flush delivers every file
+                }
+            }
+            Err(_) => self.engine_failed(GpuError(SYNCR_CDC_EIO)),
+        }
+    }
+
+    /// Results delivered by the last pipeline call, matched to their files.
+    fn collect(&mut self) {
+        if let Some(pipe) = self.pipe.as_mut() {
+            for r in pipe.take_done() {
+                if let Some(pos) = self.waiting.pop_front() {
+                    let i = (pos - self.popped) as usize;
+                    self.queue[i].slot = Slot::Done(r);
+                }
+            }
+        }
+    }
+
+    /// The engine failed: the pipeline is closed, and every file still without
+    /// a result (and every later one) goes to the rollsum loop -- the listing
+    /// never fails because of the GPU (file_operations.rs:622-643).
+    fn engine_failed(&mut self, e: GpuError) {
+        warn!("GPU chunking failed ({}); the rest of the walk is chunked on the CPU", e);
+        self.pipe = None;
+        for pos in self.waiting.drain(..) {
+            let i = (pos - self.popped) as usize;
+            self.queue[i].slot = Slot::Cpu;
+        }
+    }
 }

@@ -159,6 +159,12 @@ def test_rust_shim_sources_match_the_header():
     assert os.path.exists(os.path.join(root, "rust", "build.rs"))
     diff = open(os.path.join(root, "integration", "file_operations.diff")).read()
     assert "+++ b/src/protocol/file_operations.rs" in diff and "compute_file_chunks_gpu" in diff
+    # the batched walk is patched into traverse_and_stream, not prose
+    for needle in ("GpuWalk::open()", "walk.push_file(path, entry)", "walk.finish()", "send_ready_gpu_entries"):
+        assert needle in diff, needle
+    for fn in ("pub async fn open()", "pub async fn push_file(", "pub fn push_entry(", "pub async fn pop_ready(",
+               "pub async fn finish(", "pub fn walk_entry("):
+        assert fn in shim, fn
     r = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_integration_diff.py"), "--check"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr

@@ -6,10 +6,12 @@ compute_file_chunks (src/protocol/file_operations.rs:721-788).
 The patch is computed from syncr's own files (read as text) and the edits
 below, each anchored on text that must occur exactly once -- so a check run
 proves the patch still applies to the reference as it is.  It only adds: the
-`gpu` cargo feature and the build script, `mod chunking_gpu`, and a
-`compute_file_chunks` that tries the GPU first and otherwise runs the
-unchanged rollsum loop, renamed `compute_file_chunks_cpu`.  With the feature
-off the program is the reference's.  rust/src/chunking_gpu.rs,
+`gpu` cargo feature and the build script, `mod chunking_gpu`, the batched walk
+in traverse_and_stream (every regular file submitted to `GpuWalk`, entries sent
+in walk order as results return, a file the engine failed on chunked by the
+rollsum loop), and a `compute_file_chunks` that tries the GPU first and
+otherwise runs the unchanged rollsum loop, renamed `compute_file_chunks_cpu`.
+With the feature off the program is the reference's.  rust/src/chunking_gpu.rs,
 rust/src/chunking_gpu_ffi.rs and rust/build.rs are the new files it expects
 next to them.
 
@@ -40,6 +42,82 @@ EDITS = [
      "pub mod chunking;\n"
      "#[cfg(feature = \"gpu\")]\n"
      "pub mod chunking_gpu;\n"),
+    # the batched walk: traverse_and_stream (:544-715) hands every regular file
+    # to GpuWalk (one pipeline over all GPUs) instead of awaiting
+    # compute_file_chunks per file (:599-605); entries still leave in walk order
+    ("src/protocol/file_operations.rs",
+     "/// Traverses directory tree and streams entries through a channel\n",
+     "/// Sends the GPU walk's ready entries in walk order (feature `gpu`); a file the\n"
+     "/// engine could not chunk goes through the rollsum loop here.  false when the\n"
+     "/// receiver is gone.\n"
+     "#[cfg(feature = \"gpu\")]\n"
+     "async fn send_ready_gpu_entries(\n"
+     "\twalk: &mut crate::chunking_gpu::GpuWalk,\n"
+     "\tstate: &DumpState,\n"
+     "\tsender: &super::streaming::ListingSender,\n"
+     ") -> bool {\n"
+     "\twhile let Some(item) = walk.pop_ready(state).await {\n"
+     "\t\tlet entry = match item {\n"
+     "\t\t\tcrate::chunking_gpu::WalkItem::Ready(e) => e,\n"
+     "\t\t\tcrate::chunking_gpu::WalkItem::Cpu(mut e, path) => {\n"
+     "\t\t\t\te.chunks = compute_file_chunks_cpu(&path, state).await.unwrap_or_default();\n"
+     "\t\t\t\te\n"
+     "\t\t\t}\n"
+     "\t\t};\n"
+     "\t\tif sender.send(Ok(entry)).await.is_err() {\n"
+     "\t\t\tdebug!(\"Receiver dropped, terminating directory stream\");\n"
+     "\t\t\treturn false;\n"
+     "\t\t}\n"
+     "\t}\n"
+     "\ttrue\n"
+     "}\n"
+     "\n"
+     "/// Traverses directory tree and streams entries through a channel\n"),
+    ("src/protocol/file_operations.rs",
+     "\tlet mut stack = vec![base_path.clone()];\n",
+     "\tlet mut stack = vec![base_path.clone()];\n"
+     "\t// GPU chunking (feature `gpu`): every regular file goes to one batched\n"
+     "\t// pipeline; entries leave in walk order as their chunk lists come back\n"
+     "\t#[cfg(feature = \"gpu\")]\n"
+     "\tlet mut gpu_walk = crate::chunking_gpu::GpuWalk::open().await;\n"),
+    ("src/protocol/file_operations.rs",
+     "\t\t\t// Prepare entry based on type\n",
+     "\t\t\t#[cfg(feature = \"gpu\")]\n"
+     "\t\t\t{\n"
+     "\t\t\t\tif let Some(walk) = gpu_walk.as_mut() {\n"
+     "\t\t\t\t\tif !(meta.is_file() || meta.is_symlink() || meta.is_dir()) {\n"
+     "\t\t\t\t\t\tcontinue;\n"
+     "\t\t\t\t\t}\n"
+     "\t\t\t\t\tlet entry = crate::chunking_gpu::walk_entry(&path, relative_path, &meta);\n"
+     "\t\t\t\t\tif meta.is_file() {\n"
+     "\t\t\t\t\t\twalk.push_file(path, entry).await;\n"
+     "\t\t\t\t\t} else {\n"
+     "\t\t\t\t\t\tif meta.is_dir() {\n"
+     "\t\t\t\t\t\t\tstack.push(path);\n"
+     "\t\t\t\t\t\t}\n"
+     "\t\t\t\t\t\twalk.push_entry(entry);\n"
+     "\t\t\t\t\t}\n"
+     "\t\t\t\t\tif !send_ready_gpu_entries(walk, &state, &sender).await {\n"
+     "\t\t\t\t\t\treturn Ok(());\n"
+     "\t\t\t\t\t}\n"
+     "\t\t\t\t\tcontinue;\n"
+     "\t\t\t\t}\n"
+     "\t\t\t}\n"
+     "\n"
+     "\t\t\t// Prepare entry based on type\n"),
+    ("src/protocol/file_operations.rs",
+     "\t\t}\n\t}\n\n\tOk(())\n}\n\n/// Compute chunks for a file using rolling hash\n",
+     "\t\t}\n\t}\n\n"
+     "\t// the walk's last files: flush the pipeline, send the rest in walk order\n"
+     "\t#[cfg(feature = \"gpu\")]\n"
+     "\t{\n"
+     "\t\tif let Some(mut walk) = gpu_walk {\n"
+     "\t\t\twalk.finish().await;\n"
+     "\t\t\tsend_ready_gpu_entries(&mut walk, &state, &sender).await;\n"
+     "\t\t}\n"
+     "\t}\n"
+     "\n"
+     "\tOk(())\n}\n\n/// Compute chunks for a file using rolling hash\n"),
     ("src/protocol/file_operations.rs",
      "/// Compute chunks for a file using rolling hash\n"
      "///\n"
