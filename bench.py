@@ -596,7 +596,7 @@ def main(argv=None):
         "traffic": (int(tr["hbm_bytes_per_launch"]) if tr else None),
         "kernel": scan_kernel, "kernel_ms": round(scan_ms, 4), "scan_schedule": scan_info,
         "kernel_timing": "mean over the K timed launches by the device clock (the scan's waves stamp "
-                         "wall_clock64 at entry / exit, syncr_cdc_set_timing mode 2: no queue packets); "
+                         "wall_clock64 at entry / exit, syncr_cdc_set_timing mode 4: no queue packets); "
                          "kernel_ms_hip_events: the same K steps right after, HIP events bound to the scan "
                          "dispatch on its stream",
         "kernel_ms_hip_events": round(ems[0] / max(en, 1), 4) if en else None,

@@ -292,6 +292,7 @@ int32_t syncr_cdc_memcpy_d2h(syncr_cdc *h, void *dst, const void *d_src, uint64_
 /* Device-to-device copy on the handle's device (building device-resident
  * batches from shared pieces, e.g. the dedup corpus of SURVEY.md §8d config 5). */
 int32_t syncr_cdc_memcpy_d2d(syncr_cdc *h, void *d_dst, const void *d_src, uint64_t bytes, void *stream);
+/* wait for the handle's work: its own stream and its last launch's stream */
 int32_t syncr_cdc_synchronize(syncr_cdc *h);
 void *syncr_cdc_stream(syncr_cdc *h);
 /* Fill [d_bytes + file_off[i], +file_len[i]) with corpus file number
@@ -310,14 +311,17 @@ int32_t syncr_cdc_read_probe(syncr_cdc *h, const uint8_t *d_bytes, uint64_t byte
 /* Per-kernel timing (kernel_times: summed ms of [scan, dense + compaction,
  * resolve] since the last set_timing, and the number of launches):
  *   enable = 1  every phase of each launch bracketed by HIP events on the launch stream;
- *   enable = 2  the scan kernel only, by the device's own clock: its first waves
+ *   enable = 2  the scan kernel only, by HIP events bound to its dispatch (as in ABI v2);
+ *   enable = 3  the same as 2;
+ *   enable = 4  the scan kernel only, by the device's own clock: its first waves
  *               stamp their entry, every wave its exit (wall_clock64, the constant
  *               clock HIP events read), the launch's resolve adds last exit - first
  *               entry to device-side sums -- no packets in the queue, so the timed
  *               launches run exactly as untimed ones (an event pair costs a 1 GiB
  *               batch ~6 % of its step in queue idle);
- *   enable = 3  the scan kernel only, by HIP events bound to its dispatch;
- *   enable = 0  off. */
+ *   enable = 0  off.
+ * set_timing(4) and kernel_times wait for this handle's streams only (not the
+ * whole device). */
 int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable);
 int32_t syncr_cdc_kernel_times(syncr_cdc *h, double *ms3, uint64_t *launches);
 /* The same for up to 4 phases: [scan, dense+compaction, resolve, hash]. */

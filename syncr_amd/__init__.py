@@ -333,7 +333,7 @@ class Chunker:
         """Per-kernel timing (syncr_cdc_set_timing): HIP events around each launch's
         phases; scan_only: the scan kernel alone, by the device clock (no queue
         packets), or with events=True by HIP events bound to its dispatch."""
-        mode = ((3 if events else 2) if scan_only else 1) if on else 0
+        mode = ((2 if events else 4) if scan_only else 1) if on else 0
         _check(library().syncr_cdc_set_timing(self._h, mode), "syncr_cdc_set_timing")
 
     def kernel_times(self) -> tuple[list[float], int]:

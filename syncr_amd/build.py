@@ -18,6 +18,8 @@ SOURCES = [os.path.join(CSRC, "cdc_kernels.hip"), os.path.join(CSRC, "b3_kernels
            os.path.join(CSRC, "cache.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, "cdc_internal.h"), os.path.join(CSRC, "lds_dma.h"),
                   os.path.join(CSRC, "ingest_logic.h"), os.path.join(ROOT, "include", "syncr_cdc.h")]
+# development-only kernels and launchers, #included under SYNCR_CDC_DEV (the product build never reads them)
+DEV_DEPS = [os.path.join(CSRC, "dev", f) for f in ("scan_mfma.inc", "dense_generic.inc", "scan_launch_dev.inc")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SYNCR_CDC_ARCH", "gfx950")
 
@@ -26,7 +28,7 @@ def needs_build(lib: str = LIB) -> bool:
     if not os.path.exists(lib):
         return True
     t = os.path.getmtime(lib)
-    return any(os.path.getmtime(p) > t for p in DEPS)
+    return any(os.path.getmtime(p) > t for p in DEPS + (DEV_DEPS if lib == DEV_LIB else []))
 
 
 def build(force: bool = False, verbose: bool = False, dev: bool = False) -> str:

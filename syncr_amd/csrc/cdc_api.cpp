@@ -130,8 +130,8 @@ struct syncr_cdc {
 
     // timing
     bool timing = false;
-    bool timing_scan_only = false;            // set_timing(h, 2 or 3): the scan only
-    bool timing_clock = false;                // set_timing(h, 2): by the device clock (no events)
+    bool timing_scan_only = false;            // set_timing(h, 2, 3 or 4): the scan only
+    bool timing_clock = false;                // set_timing(h, 4): by the device clock (no events)
     DevBuf tacc;                              // [sum of scan ticks, launches] (timing_clock)
     uint64_t wall_khz = 100000;               // the device clock's rate
     std::vector<PendingTiming> pending;
@@ -466,9 +466,9 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
 #ifdef SYNCR_CDC_DEV
     if (t.dbg) CHECK_HIP(hipMemsetAsync(t.dbg, 0, DBG_WORDS * sizeof(uint64_t), s));
 #endif
-    // HIP events (timing modes 1 and 3) are marker packets around the kernels: each
+    // HIP events (timing modes 1, 2 and 3) are marker packets around the kernels: each
     // costs queue idle (an event pair ~18 us of a 1 GiB batch's ~0.3 ms step,
-    // profiles/r05c_*_trace_shard8); mode 2 times the scan by the device clock instead
+    // profiles/r05c_*_trace_shard8); mode 4 times the scan by the device clock instead
     const bool events = h->timing && !h->timing_clock;
     const bool bound = events && t.ntiles;           // the pair around the scan: launch_scan records it
     if (events && !bound) CHECK_HIP(hipEventRecord(pt.ev[0], s));
@@ -1073,10 +1073,21 @@ int32_t syncr_cdc_memcpy_d2d(syncr_cdc *h, void *d_dst, const void *d_src, uint6
     return SYNCR_CDC_OK;
 }
 
+namespace {
+// Wait for this handle's work only (its own stream and the stream of its last
+// launch): other handles and ingest pipelines on the device keep running.
+hipError_t sync_handle(syncr_cdc *h) {
+    hipError_t e = hipSuccess;
+    if (h->last_stream && h->last_stream != h->stream) e = hipStreamSynchronize(h->last_stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return e;
+}
+}  // namespace
+
 int32_t syncr_cdc_synchronize(syncr_cdc *h) {
     if (!h) return SYNCR_CDC_EINVAL;
     CHECK_HIP(hipSetDevice(h->device));
-    CHECK_HIP(hipDeviceSynchronize());
+    CHECK_HIP(sync_handle(h));
     return SYNCR_CDC_OK;
 }
 
@@ -1176,27 +1187,27 @@ int32_t syncr_cdc_read_probe(syncr_cdc *h, const uint8_t *d_bytes, uint64_t byte
 }
 
 int32_t syncr_cdc_set_timing(syncr_cdc *h, int32_t enable) {
-    if (!h || enable < 0 || enable > 3) return SYNCR_CDC_EINVAL;
+    if (!h || enable < 0 || enable > 4) return SYNCR_CDC_EINVAL;
     CHECK_HIP(hipSetDevice(h->device));
     drain_timing(h);
-    if (enable == 2) {
+    if (enable == 4) {
         CHECK_HIP(h->tacc.ensure(16));
-        CHECK_HIP(hipDeviceSynchronize());            // no earlier launch may still add to the sums
+        CHECK_HIP(sync_handle(h));                    // no earlier launch may still add to the sums
         CHECK_HIP(hipMemset(h->tacc.p, 0, 16));
     }
     h->timing = enable != 0;
-    h->timing_scan_only = enable == 2 || enable == 3;
-    h->timing_clock = enable == 2;
+    h->timing_scan_only = enable >= 2;
+    h->timing_clock = enable == 4;
     for (double &m : h->ms) m = 0;
     h->timed_launches = 0;
     return SYNCR_CDC_OK;
 }
 
 namespace {
-// the device-clock sums into ms[0] / timed_launches (timing mode 2)
+// the device-clock sums into ms[0] / timed_launches (timing mode 4)
 int32_t read_clock_times(syncr_cdc *h) {
     if (!h->timing_clock || !h->tacc.p) return SYNCR_CDC_OK;
-    CHECK_HIP(hipDeviceSynchronize());
+    CHECK_HIP(sync_handle(h));
     uint64_t v[2] = {0, 0};
     CHECK_HIP(hipMemcpy(v, h->tacc.p, 16, hipMemcpyDeviceToHost));
     h->ms[0] = (double)v[0] / (double)h->wall_khz;

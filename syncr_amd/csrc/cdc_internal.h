@@ -271,7 +271,7 @@ struct Tables {
     uint32_t nst;                  // stream-tile scan: STs of the batch (launch geometry)
     uint32_t nt_out;               // KParams::nt_out: non-temporal stores of candidate words and cuts
     uint64_t gapmax;               // chain links: the next candidate at most min(MAX, read_cap) past
-    // scan timing by the device clock (syncr_cdc_set_timing mode 2; null: off): the scan's
+    // scan timing by the device clock (syncr_cdc_set_timing mode 4; null: off): the scan's
     // waves stamp wall_clock64 -- tscan[0] = ~0 - the earliest entry, tscan[1] = the
     // latest exit (atomic max, zeroed per launch) -- and the resolve adds exit - entry
     // to tacc[0] and 1 to tacc[1] (the handle's running sums).  No queue packets.

@@ -1475,201 +1475,7 @@ void cdc_scan3_kernel(const uint8_t *__restrict__ data, KParams P, Tables T) {
 }
 
 #ifdef SYNCR_CDC_DEV
-// ---------------------------------------------------------------------------
-// MFMA scan (development library only: north_star asks for integer VALU work,
-// and it measured slightly below the VALU scan).
-// W at position n is a 64-tap FIR of the bytes:
-//     W(n) = sum_{a=0..63} (a+1) * x[n-a],    S(n) = sum_{a=0..63} x[n-a]
-// (the closed form of Bup's s2 / s1 recurrences).  For a block of 32
-// positions [32b, 32b+32) of one stream it is a product with three constant
-// 32x32 Toeplitz matrices:  W_b = M0 X_b + M1 X_{b-1} + M2 X_{b-2}, where
-// X_b is the block's bytes and Mq[i][k] = w(32q + i - k), w(a) = a+1 on
-// [0, 63].  v_mfma_i32_32x32x32_i8 evaluates it for 32 streams at once: the
-// stream is the MFMA column, lane (c, h) holds 16 bytes of block b of stream
-// c, so the two predecessor blocks are the same lane's previous registers.
-// Bytes enter as signed i8 (x ^ 0x80 = x - 128); the 128*2080 bias and the
-// hit target are folded into the accumulator's initial value.
-//
-// The filter tests only the s2 half of the digest (W + 124993 == 0 mod 2^bw,
-// bw = min(bits, 16)), a superset of the edges.  A wave that sees a filter
-// hit anywhere in its tile redoes the tile exactly (W and S by MFMA, then the
-// full digest test) and records the true edges.  Expected filter hits per
-// 8 KiB tile at bits = 20: 0.125.
-// ---------------------------------------------------------------------------
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
-
-constexpr int FIR_SUM_W = 2080;          // sum of the weights 1..64
-constexpr int S2_BIAS = 124993;          // s2 + 1 = 124993 + W (Bup's CHAR_OFFSET terms)
-
-// Lane fragment of Mq (A operand): lane (i = l&31, h = l>>5) byte j holds
-// Mq[i][16h + j] (verified on gfx950 by tools/mfma_i8_check.hip).
-__device__ __forceinline__ v4i fir_matrix(int q, int lane, bool ones) {
-    const int i = lane & 31, h = lane >> 5;
-    int d[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int a = 32 * q + i - (16 * h + 4 * m + b);
-            const uint32_t w = (a >= 0 && a <= 63) ? (ones ? 1u : (uint32_t)(a + 1)) : 0u;
-            v |= w << (8 * b);
-        }
-        d[m] = (int)v;
-    }
-    return v4i{d[0], d[1], d[2], d[3]};
-}
-
-// output row of accumulator register v on lane half h (gfx950 32x32 C/D map)
-__device__ __forceinline__ int mf_row(int v, int h) { return (v & 3) + 8 * (v >> 2) + 4 * h; }
-
-__device__ __forceinline__ v16i splat16(int x) {
-    v16i c;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) c[v] = x;
-    return c;
-}
-
-// MODE bits as cdc_scan_kernel (0 product, 1 staging only, 2 no DMA; 4 nt),
-// plus 8: one landing buffer, 16: no software pipelining of the MFMA chains.
-// LOW16: bits >= 16 (the filter tests whole low halves, no scaling).
-template <int NB, int MODE, bool LOW16>
-__global__ __launch_bounds__(64) void cdc_scan_mfma_kernel(const uint8_t *__restrict__ data, KParams P,
-                                                           Tables T) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int BUF = mf_buf_bytes(NB);
-    constexpr int TILE = mf_tile_bytes(NB);
-    constexpr int L = 32 * NB;                        // bytes per stream
-    constexpr bool NT = (MODE & 4) != 0;
-    const int lane = threadIdx.x, c = lane & 31, h = lane >> 5;
-    constexpr int NDMA = (BUF + 1023) / 1024;         // DMA instructions per tile
-    constexpr bool DB = (MODE & 8) == 0;              // double-buffered landing
-    constexpr bool PIPE = (MODE & 16) == 0;
-    uint8_t *wl = smem;                               // landing buffers wl[0..BUF), wl[BUF..2BUF)
-    uint32_t *wlist = (uint32_t *)(smem + (DB ? 2 : 1) * BUF);
-    uint32_t *wcount = wlist + LISTCAP;
-    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(wl));
-    const uint32_t stride = gridDim.x;
-    uint32_t tile = blockIdx.x;
-    if (tile >= T.ntiles) return;
-    const int64_t span = (int64_t)T.span;
-    const v4i M0 = fir_matrix(0, lane, false), M1 = fir_matrix(1, lane, false),
-              M2 = fir_matrix(2, lane, false);
-    const int cinit = 128 * FIR_SUM_W + S2_BIAS;      // D = W + 124993
-    const u16x2 kk = as_u16x2(P.kk);
-    issue_buf<BUF, TILE, NT>(data, T.span, tile, lds0, lane);
-    if (DB && tile + stride < T.ntiles && (MODE & 3) != 2)
-        issue_buf<BUF, TILE, NT>(data, T.span, tile + stride, lds0 + BUF, lane);
-    DenseSlots dslots_alloc;
-    uint32_t cur = 0;                                 // buffer of this tile
-    for (; tile < T.ntiles; tile += stride, cur ^= (DB ? 1u : 0u)) {
-        const uint32_t after = tile + (DB ? 2 : 1) * stride;   // lands in this tile's buffer
-        const int64_t t0 = (int64_t)tile * TILE;
-        if (lane == 0) *wcount = 0u;
-        // this tile has landed (vm ops complete in order: at most the next
-        // tile's NDMA loads, or anything younger, may still be in flight)
-        if (DB && tile + stride < T.ntiles && (MODE & 3) != 2) wait_vmcnt<NDMA>(); else wait_vmcnt<0>();
-        v4i X[NB + 2];                                // X[b] = block b-2 of stream c, half h
-        {
-            const uint8_t *lp = wl + cur * BUF + HALO + c * L + 16 * h - 64;
-#pragma unroll
-            for (int b = 0; b < NB + 2; ++b) X[b] = *(const v4i *)(lp + 32 * b);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (after < T.ntiles && (MODE & 3) != 2)
-            issue_buf<BUF, TILE, NT>(data, T.span, after, lds0 + cur * BUF, lane);
-        if constexpr ((MODE & 3) == 1) {
-#pragma unroll
-            for (int b = 0; b < NB + 2; ++b) asm volatile("" ::"v"(X[b]));
-            continue;
-        }
-#pragma unroll
-        for (int b = 0; b < NB + 2; ++b) X[b] ^= (int)0x80808080;
-        // filter, software-pipelined: block b+1's MFMA chain is issued before
-        // block b's test so the matrix pipe runs under the VALU work
-        auto chain = [&](const v4i &x0, const v4i &x1, const v4i &x2) -> v16i {
-            v16i d = splat16(cinit);
-            d = __builtin_amdgcn_mfma_i32_32x32x32_i8(M0, x0, d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_i32_32x32x32_i8(M1, x1, d, 0, 0, 0);
-            return __builtin_amdgcn_mfma_i32_32x32x32_i8(M2, x2, d, 0, 0, 0);
-        };
-        uint32_t acc = 0xffffffffu;
-        v16i dn = chain(X[2], X[1], X[0]);
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            v16i d = dn;
-            if constexpr (PIPE) {
-                if (b + 1 < NB) dn = chain(X[b + 3], X[b + 2], X[b + 1]);
-            } else if (b > 0) {
-                d = chain(X[b + 2], X[b + 1], X[b]);
-            }
-            if constexpr (LOW16) {
-#pragma unroll
-                for (int v = 0; v < 16; v += 2) acc = min3_lo16(acc, (uint32_t)d[v], (uint32_t)d[v + 1]);
-            } else {
-#pragma unroll
-                for (int v = 0; v < 16; v += 2) {
-                    u16x2 q = as_u16x2(__builtin_amdgcn_perm((uint32_t)d[v + 1], (uint32_t)d[v], 0x05040100u));
-                    q = q * kk;                       // keep the low bw bits only
-                    acc = as_u32(__builtin_elementwise_min(as_u16x2(acc), q));
-                }
-            }
-            // bound the live accumulators to two blocks (the scheduler would
-            // otherwise hoist every block's MFMAs and spill)
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        const bool z = LOW16 ? (acc & 0xffffu) == 0u : ((acc & 0xffffu) == 0u || (acc >> 16) == 0u);
-        if constexpr ((MODE & 3) == 2) {              // diagnostics: filter only (stale LDS bytes)
-            if (z) record(wcount, wlist, 0u);
-            continue;
-        }
-        if (__builtin_expect(__ballot(z) != 0ull, 0)) {
-            // exact pass over the tile: W and S for every position, full digest
-            // test.  W and S are taken one after the other (16 accumulator
-            // registers live).
-            auto ones = [](v4i m) {                   // byte != 0 -> 1 (bytes <= 64)
-                asm volatile("" : "+v"(m));           // opaque: not hoisted into the hot loop
-                v4i o;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    o[q] = (int)((((uint32_t)m[q] + 0x7f7f7f7fu) >> 7) & 0x01010101u);
-                return o;
-            };
-            const int64_t lim_rel = span - t0;
-            const uint32_t bw = P.bits < 16 ? P.bits : 16u;
-            const uint32_t wmask = (1u << bw) - 1u;
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                const v16i w = chain(X[b + 2], X[b + 1], X[b]);
-                uint32_t hm = 0;                      // s2 half of the digest
-#pragma unroll
-                for (int v = 0; v < 16; ++v) hm |= (((uint32_t)w[v] & wmask) == 0u ? 1u : 0u) << v;
-                __builtin_amdgcn_sched_barrier(0);
-                // s1 half: (1984 + S) & m1 == m1.  Wave-uniform branch: an MFMA
-                // reads operands from every lane, so none may be masked off.
-                if (P.m1 && __ballot(hm != 0u) != 0ull) {
-                    v16i sm = __builtin_amdgcn_mfma_i32_32x32x32_i8(ones(M0), X[b + 2], splat16(0), 0, 0, 0);
-                    sm = __builtin_amdgcn_mfma_i32_32x32x32_i8(ones(M1), X[b + 1], sm, 0, 0, 0);
-                    sm = __builtin_amdgcn_mfma_i32_32x32x32_i8(ones(M2), X[b], sm, 0, 0, 0);
-                    uint32_t sh = 0;                  // S = sm + 128 * 64
-#pragma unroll
-                    for (int v = 0; v < 16; ++v)
-                        sh |= (((1984u + 8192u + (uint32_t)sm[v]) & P.m1) == P.m1 ? 1u : 0u) << v;
-                    hm &= sh;
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                while (hm) {
-                    const int v = __builtin_ctz(hm);
-                    hm &= hm - 1u;
-                    const uint32_t rel = (uint32_t)(c * L + 32 * b + mf_row(v, h));
-                    if ((int64_t)rel < lim_rel) record(wcount, wlist, rel);
-                }
-            }
-        }
-        publish_tile(data, P, T, tile, t0, wlist, wcount, lane, false, dslots_alloc);
-    }
-}
+#include "dev/scan_mfma.inc"
 #endif  // SYNCR_CDC_DEV
 
 // File starts: the scan treats the batch as ONE byte stream, so its G is exact
@@ -1863,85 +1669,7 @@ __global__ __launch_bounds__(256) void cdc_fix_kernel(const uint8_t *__restrict_
 }
 
 #ifdef SYNCR_CDC_DEV
-// (development library: the dense pass of scan geometries other than the product's)
-// ---------------------------------------------------------------------------
-// Dense tiles (more than LISTCAP candidates: low-entropy / periodic /
-// adversarial data): recompute G for every position of the tile into a bitmap
-// and count it.  One wave per dense tile: the tile and its 64-byte halo are
-// staged in LDS with coalesced 16-byte loads; lane l rolls the 2*RUN positions
-// [t0 + l*2*RUN, +2*RUN) exactly (S, W and the full digest test) from its 64
-// warm-up bytes (closed form, v_dot4), reading 32 new + 32 dropped bytes per
-// bitmap word as four ds_read_b128.  Stream semantics like the scan: no resets
-// at file starts (file heads are the resolve's head scan).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void cdc_dense_kernel(const uint8_t *__restrict__ data, KParams P,
-                                                       Tables T) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t dbuf[];   // [HALO + tile]
-    const int lane = threadIdx.x;
-    const uint32_t nd = min(T.ctr[CTR_DENSE], T.dense_cap);
-    const uint32_t TB = T.tile, BUFB = HALO + TB;
-    const uint32_t per_lane = TB / 64;                   // 2 * RUN: a multiple of 32
-    const uint32_t words_lane = per_lane / 32;
-    const int64_t span = (int64_t)T.span;
-    for (uint32_t idx = blockIdx.x; idx < nd; idx += gridDim.x) {
-        const uint32_t tile = T.dense_list[idx];
-        if (tile == DENSE_HOLE) continue;
-        const int64_t base = (int64_t)tile * TB - HALO;
-        __syncthreads();                                 // the previous tile's LDS reads are done
-        for (uint32_t o = (uint32_t)lane * 16u; o < BUFB; o += 1024u) {
-            const int64_t g = base + o;
-            uint4 v;
-            if (g >= 0 && g + 16 <= span) {
-                v = *(const uint4 *)(data + g);          // d_bytes and the tile size are 16-byte aligned
-            } else {                                     // batch edges: zeros outside [0, span)
-                uint32_t w4[4] = {0u, 0u, 0u, 0u};
-                for (int b = 0; b < 16; ++b)
-                    if (g + b >= 0 && g + b < span) w4[b >> 2] |= (uint32_t)data[g + b] << (8 * (b & 3));
-                v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-            }
-            *(uint4 *)(dbuf + o) = v;
-        }
-        __syncthreads();
-        const uint8_t *lb = dbuf + (size_t)lane * per_lane;        // run start - 64
-        uint32_t S = 0, W = 0;
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {                   // window before the run (weights 64..1)
-            const uint32_t wd = *(const uint32_t *)(lb + 4 * m);
-            S = __builtin_amdgcn_udot4(wd, 0x01010101u, S, false);
-            W = __builtin_amdgcn_udot4(wd, 0x3D3E3F40u - 0x04040404u * (uint32_t)m, W, false);
-        }
-        const int64_t rs = (int64_t)tile * TB + (int64_t)lane * per_lane;
-        const int64_t lim = span - rs;                   // positions >= span are not bytes
-        uint32_t *out = T.dense_bits + (size_t)idx * (TB / 32) + (size_t)lane * words_lane;
-        uint32_t cnt = 0;
-        for (uint32_t wi = 0; wi < words_lane; ++wi) {
-            const uint4 x0 = *(const uint4 *)(lb + HALO + 32 * wi), x1 = *(const uint4 *)(lb + HALO + 32 * wi + 16);
-            const uint4 d0 = *(const uint4 *)(lb + 32 * wi), d1 = *(const uint4 *)(lb + 32 * wi + 16);
-            const uint32_t xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-            const uint32_t ds[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-            uint32_t bits = 0;
-#pragma unroll
-            for (int b = 0; b < 32; ++b) {
-                const uint32_t x = (xs[b >> 2] >> (8 * (b & 3))) & 0xffu;
-                const uint32_t d = (ds[b >> 2] >> (8 * (b & 3))) & 0xffu;
-                S += x - d;
-                W += S - 64u * d;
-                bits |= (hit_exact(S, W, P.mask) ? 1u : 0u) << b;
-            }
-            const int64_t k0 = 32 * (int64_t)wi;
-            if (k0 + 32 > lim) bits &= k0 >= lim ? 0u : ((1u << (uint32_t)(lim - k0)) - 1u);
-            out[wi] = bits;
-            cnt += __builtin_popcount(bits);
-        }
-        for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
-        if (lane == 0) {
-            T.dense_cnt[idx] = cnt;
-            atomicAdd(&T.super_cnt[tile >> 6], cnt);
-            atomicAdd(&T.coarse[(tile >> 12) * COARSE_STRIDE], cnt);
-            atomicAdd(&T.split[SPL_DENSE_TILES], 1u);
-        }
-    }
-}
+#include "dev/dense_generic.inc"
 #endif  // SYNCR_CDC_DEV
 
 // Exact packed roll of one dense tile-lane (runs lane and lane+64 in the two
@@ -3904,168 +3632,7 @@ static hipError_t launch_scan_cu(uint32_t wave_grid, const uint8_t *d, const KPa
 }
 
 #ifdef SYNCR_CDC_DEV
-static bool valu_run_ok(int run) {
-    return run == 48 || run == 80 || run == W3_RUN || run == 112 || run == 144 || run == 176;
-}
-static bool mfma_nb_ok(int nb) { return nb == 4 || nb == 6 || nb == 8 || nb == 10 || nb == 12; }
-
-bool scan_supported(ScanGeom g) {
-    return g.kind == SCAN_VALU ? valu_run_ok(g.param) : (g.kind == SCAN_MFMA && mfma_nb_ok(g.param));
-}
-int scan_tile_bytes(ScanGeom g) { return g.kind == SCAN_VALU ? tile_bytes(g.param) : mf_tile_bytes(g.param); }
-int scan_lds_bytes(ScanGeom g) {
-    return g.kind == SCAN_VALU ? scan_lds_for_run(g.param) : mf_lds_bytes(g.param, (g.var & MFV_SINGLE) ? 1 : 2);
-}
-
-template <int RUN> static const void *scan_fn() { return (const void *)&cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>; }
-template <int NB> static const void *mfma_fn(int var) {
-    switch (var & 3) {
-        case 0: return (const void *)&cdc_scan_mfma_kernel<NB, 4, true>;
-        case 1: return (const void *)&cdc_scan_mfma_kernel<NB, 4 | 8, true>;
-        case 2: return (const void *)&cdc_scan_mfma_kernel<NB, 4 | 16, true>;
-        default: return (const void *)&cdc_scan_mfma_kernel<NB, 4 | 8 | 16, true>;
-    }
-}
-
-static const void *scan_kernel_ptr(ScanGeom g) {
-    if (g.kind == SCAN_MFMA) {
-        switch (g.param) {
-            case 4: return mfma_fn<4>(g.var);
-            case 6: return mfma_fn<6>(g.var);
-            case 8: return mfma_fn<8>(g.var);
-            case 10: return mfma_fn<10>(g.var);
-            case 12: return mfma_fn<12>(g.var);
-            default: return nullptr;
-        }
-    }
-    switch (g.param) {
-        case 48: return scan_fn<48>();
-        case 80: return scan_fn<80>();
-        case W3_RUN: return (const void *)&cdc_scan3_kernel<W3_RUN, 4 | 8>;
-        case 112: return scan_fn<112>();
-        case 144: return scan_fn<144>();
-        case 176: return scan_fn<176>();
-        default: return nullptr;
-    }
-}
-
-template <int RUN>
-static void launch_scan_t(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    const size_t lds = lds_wave_bytes(RUN);
-    if (p.ablate == 1u)                                              // timing only: staging, no roll
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 1>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 2u)                                         // timing only: roll, no DMA
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 3u)                                         // timing only: staging, nt
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 5>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 4u)                                         // A/B: static stride always (exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_STATIC_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 8u)                                         // A/B: dynamic groups always (exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 5u)                                         // A/B: round-1 roll (two dependent mads, exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 12>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 11u)                                        // A/B: dense tiles passed by the scan wave
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 128>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 6u)                                         // timing only: roll, no DMA
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, 2 | 16>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 10u)                                        // A/B: round-2 roll, a branch per group (exact)
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 64>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 17u)                                        // A/B: stream-tile scan (exact)
-        launch_st(grid, d, p, t, s);
-    else if (p.ablate == 15u) {                                      // A/B: CU schedule (exact)
-        (void)launch_scan_cu<RUN, 4 | 16>(grid, d, p, t, s);
-    } else if (p.ablate == 16u) {                                    // timing only: CU schedule, no warm-up/halo
-        (void)launch_scan_cu<RUN, 4 | 16 | 256 | 512>(grid, d, p, t, s);
-    }
-    else if (p.ablate == 12u)                                        // timing only: no closed-form warm-up
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 13u)                                        // timing only: no warm-up, no halo bytes
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 256 | 512>), dim3(grid), dim3(64), lds, s, d,
-                           p, t);
-    else if (p.ablate == 7u)                                         // A/B: product + 3 waves per SIMD hint
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE | 32>), dim3(grid), dim3(64), lds, s, d, p,
-                           t);
-    else if (p.nt && p.scan_tiles && scan_dynamic(t.ntiles, grid))   // product, dense-heavy data: tiles
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.nt && !p.scan_tiles && scan_stream_tiles(t.ntiles, grid) && RUN == DEFAULT_RUN)   // product: stream tiles
-        launch_st(grid, d, p, t, s);
-    else if (p.nt && scan_dynamic(t.ntiles, grid))                   // other geometries: nt + dynamic groups + ROLL2
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.nt)                                                   // product, small batch: CU schedule
-        (void)launch_scan_cu<RUN, SCAN_STATIC_MODE>(grid, d, p, t, s);
-    else
-        hipLaunchKernelGGL((cdc_scan_kernel<RUN, SCAN_PRODUCT_MODE & ~4>), dim3(grid), dim3(64), lds, s, d, p, t);
-}
-
-static void launch_scan3(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    const size_t lds = lds3_wave_bytes(W3_RUN);
-    if (p.ablate == 6u)                                              // timing only: roll, no DMA
-        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8 | 2>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (scan_dynamic(t.ntiles, grid))
-        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4 | 8>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else
-        hipLaunchKernelGGL((cdc_scan3_kernel<W3_RUN, 4>), dim3(grid), dim3(64), lds, s, d, p, t);
-}
-
-template <int NB, int V>
-static void launch_mfma_v(uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t, hipStream_t s) {
-    constexpr int VM = ((V & MFV_SINGLE) ? 8 : 0) | ((V & MFV_NOPIPE) ? 16 : 0);
-    const size_t lds = mf_lds_bytes(NB, (V & MFV_SINGLE) ? 1 : 2);
-    const bool low16 = p.bits >= 16;
-    if (p.ablate == 1u || p.ablate == 3u)
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 5, true>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.ablate == 2u)
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 2, true>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (low16 && p.nt)
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, true>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (low16)
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, true>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else if (p.nt)
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM | 4, false>), dim3(grid), dim3(64), lds, s, d, p, t);
-    else
-        hipLaunchKernelGGL((cdc_scan_mfma_kernel<NB, VM, false>), dim3(grid), dim3(64), lds, s, d, p, t);
-}
-
-template <int NB>
-static void launch_mfma_t(int var, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
-                          hipStream_t s) {
-    switch (var & 3) {
-        case 0: launch_mfma_v<NB, 0>(grid, d, p, t, s); break;
-        case 1: launch_mfma_v<NB, 1>(grid, d, p, t, s); break;
-        case 2: launch_mfma_v<NB, 2>(grid, d, p, t, s); break;
-        default: launch_mfma_v<NB, 3>(grid, d, p, t, s); break;
-    }
-}
-
-bool scan_dense_inline(ScanGeom g, const KParams &p) {
-    return g.kind == SCAN_VALU && g.param != W3_RUN && p.ablate == 11u;     // the mode-128 instance
-}
-
-static hipError_t launch_scan_kernel(ScanGeom g, uint32_t grid, const uint8_t *d, const KParams &p, const Tables &t,
-                                     hipStream_t s) {
-    grid = grid < t.ntiles ? grid : t.ntiles;
-    if (g.kind == SCAN_MFMA) {
-        switch (g.param) {
-            case 4: launch_mfma_t<4>(g.var, grid, d, p, t, s); break;
-            case 6: launch_mfma_t<6>(g.var, grid, d, p, t, s); break;
-            case 8: launch_mfma_t<8>(g.var, grid, d, p, t, s); break;
-            case 10: launch_mfma_t<10>(g.var, grid, d, p, t, s); break;
-            case 12: launch_mfma_t<12>(g.var, grid, d, p, t, s); break;
-            default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
-    switch (g.param) {
-        case 48: launch_scan_t<48>(grid, d, p, t, s); break;
-        case 80: launch_scan_t<80>(grid, d, p, t, s); break;
-        case W3_RUN: launch_scan3(grid, d, p, t, s); break;
-        case 112: launch_scan_t<112>(grid, d, p, t, s); break;
-        case 144: launch_scan_t<144>(grid, d, p, t, s); break;
-        case 176: launch_scan_t<176>(grid, d, p, t, s); break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
+#include "dev/scan_launch_dev.inc"
 #else   // product: one exact scan instance
 bool scan_supported(ScanGeom g) { return g.kind == SCAN_VALU && g.param == DEFAULT_RUN; }
 int scan_tile_bytes(ScanGeom) { return tile_bytes(DEFAULT_RUN); }

@@ -343,6 +343,16 @@ def test_kernel_timing_api(chunkers):
         # the two measure the same kernel: the same order of magnitude (on a 64 MiB batch the
         # scan is ~20-40 us and its dispatch start-up is part of both)
         assert 0.5 * ms3[0] <= ms2[0] <= 2.0 * ms3[0], (ms2[0], ms3[0])
+        # the raw modes keep their ABI-v2 meaning (2 = the scan by HIP events);
+        # the device clock is mode 4; anything else is refused
+        lib = syncr_amd.library()
+        for mode, clock in ((2, False), (3, False), (4, True)):
+            assert lib.syncr_cdc_set_timing(ch.handle, mode) == 0
+            ch.launch(buf.ptr)
+            m, k = ch.kernel_times()
+            assert k == 1 and m[0] > 0 and m[1] == m[2] == 0, (mode, m, k)
+        assert lib.syncr_cdc_set_timing(ch.handle, 5) == -22
+        ch.set_timing(False)
         ch.fetch()
         st = ch.last_stats()
         assert st["tiles"] >= data_len // (144 * 128) and st["flags"] == 0

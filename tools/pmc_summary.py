@@ -69,7 +69,7 @@ def dispatches(trace_csv, line, k="cdc::cdc_scan_kernel"):
         "leaf_ms_per_dispatch": [round(x, 4) for x in leaf], "leaf_ms_mean": mean(leaf),
         "bench_line_scan_ms_hip_events": (line or {}).get("roofline", {}).get("kernel_ms_hip_events"),
         "note": "rocprofv3 kernel-trace durations; the bench line's kernel_ms is the device-clock mean over the "
-                "same timed window (syncr_cdc_set_timing mode 2), kernel_ms_hip_events its event-pair cross-check "
+                "same timed window (syncr_cdc_set_timing mode 4), kernel_ms_hip_events its event-pair cross-check "
                 "on the K steps after it (profiling adds a few % per dispatch)",
     }
 
