@@ -144,7 +144,7 @@ def legs(host: np.ndarray, offs, lens, idx, device: int, names=tuple(MODES)) -> 
     out = {}
     try:
         for name in names:
-            r = run(MODES[name], root, device)
+            r = run(MODES[name], root, device, reps=2 if name == "shim_per_file" else 3)
             r["path"] = PATHS[name]
             r["tree"] = (f"{nfiles} zipf10k files in {(nfiles + FILES_PER_DIR - 1) // FILES_PER_DIR} directories "
                          f"on local disk, written and fsync'ed before the passes (page cache, clean); "

@@ -74,6 +74,7 @@ struct Result {
 
 struct Pass {
     double seconds = 0;
+    double fill_seconds = 0;          // zero_copy: the caller's own copies into staging
     std::vector<double> latency_us;
     std::vector<Result> results;
     double stage[5] = {0, 0, 0, 0, 0};
@@ -309,6 +310,7 @@ Pass run_ingest(const Corpus &c, const std::string &mode, syncr_ingest *g, Fill 
             syncr::cdc_check(syncr_ingest_reserve(g, c.len[i], &dst), "reserve");
             const uint8_t *src = c.host + c.off[i];
             const uint64_t n = c.len[i];
+            const auto f0 = Clock::now();
             if (n <= PAR) {
                 memcpy(dst, src, n);
             } else {
@@ -317,6 +319,7 @@ Pass run_ingest(const Corpus &c, const std::string &mode, syncr_ingest *g, Fill 
                     memcpy(dst + a, src + a, b - a);
                 });
             }
+            p.fill_seconds += secs(f0, Clock::now());
             syncr::cdc_check(syncr_ingest_commit(g, i), "commit");
         }
     }
@@ -429,14 +432,14 @@ int main(int argc, char **argv) {
         printf("], \"bytes\": %llu, \"files\": %llu, \"entries\": %llu, \"delivered\": %zu, \"status_nonzero\": %llu, "
                "\"in_walk_order\": %s, \"latency_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"max\": %.1f, \"mean\": %.1f}, "
                "\"host_stage_seconds\": {\"copy\": %.4f, \"read\": %.4f, \"seal\": %.4f, \"wait\": %.4f, "
-               "\"deliver\": %.4f}}\n",
+               "\"deliver\": %.4f}, \"caller_fill_seconds\": %.4f}\n",
                (unsigned long long)bytes, (unsigned long long)files, (unsigned long long)best.entries,
                best.results.size(), (unsigned long long)nonzero, in_order ? "true" : "false", pct(best.latency_us, 0.5),
                pct(best.latency_us, 0.9), pct(best.latency_us, 0.99), pct(best.latency_us, 1.0),
                best.latency_us.empty() ? 0.0
                                        : std::accumulate(best.latency_us.begin(), best.latency_us.end(), 0.0) /
                                              (double)best.latency_us.size(),
-               best.stage[0], best.stage[1], best.stage[2], best.stage[3], best.stage[4]);
+               best.stage[0], best.stage[1], best.stage[2], best.stage[3], best.stage[4], best.fill_seconds);
         free(c.host);
     } catch (const std::exception &e) {
         fprintf(stderr, "e2e_driver: %s\n", e.what());

@@ -680,17 +680,35 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
     uint32_t *stage_ptr = stage_mem + (COOP ? (threadIdx.x >> 6) * SLOT : 0);
     const uint32_t stage = (uint32_t)__builtin_amdgcn_readfirstlane(lds_addr(stage_ptr));
     const uint64_t nbig = min(H.ctr[B3C_ITEMS], H.items_cap);
+    // Wave items are dealt by B3_SHARDS counters 4 KiB apart (shard k: items
+    // k, k + S, k + 2S, ...; a block starts on shard blockIdx % S and moves on
+    // when it is spent).  One counter made it the limit on many tiny chunks: one
+    // address takes ~70 M atomics/s, and a wave item of class 0 or 1 (64 or 32
+    // chunks of <= 4 KiB) can be one compression per lane (dense1: 2.1 M 64-byte
+    // chunks = 33 K wave items = 0.45 ms of grabs on one counter).
     uint64_t npk[B3_CLASSES], total = nbig;
 #pragma unroll
     for (int c = 0; c < B3_CLASSES; ++c) {
         npk[c] = min(H.ctr[B3C_PK0 + c], H.packed_cap);
         total += (npk[c] + (64u >> c) - 1) >> (6 - c);          // waves of class c
     }
+    uint32_t shard = blockIdx.x % B3_SHARDS, spent = 0;
     for (;;) {
-        uint64_t w = 0;
-        if (lane == 0) w = atomicAdd((unsigned long long *)&H.ctr[B3C_NEXT], 1ull);
-        w = bcast64(w);
-        if (w >= total) break;
+        unsigned long long *const sc = (unsigned long long *)&H.ctr[(shard + 1) * B3_SHARD_STRIDE];
+        uint64_t j = 0;
+        if (lane == 0) {
+            // a shard other than the block's own is looked at first (a load: no
+            // atomic on a counter that is already past its last item)
+            j = spent ? __hip_atomic_load(sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+            if (shard + j * B3_SHARDS < total) j = atomicAdd(sc, 1ull);
+        }
+        j = bcast64(j);
+        const uint64_t w = shard + j * B3_SHARDS;
+        if (w >= total) {                                        // this shard is spent: the next one
+            if (++spent == B3_SHARDS) break;
+            shard = (shard + 1) % B3_SHARDS;
+            continue;
+        }
         // per-lane geometry
         bool valid;
         uint64_t slot = 0;
@@ -955,7 +973,7 @@ static hipError_t launch_leaf_v(int device, const uint8_t *d, const Tables &t, c
 
 hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
     hipError_t e = hipSuccess;
-    if (!t.hzero) e = hipMemsetAsync(ht.ctr, 0, B3C_WORDS * sizeof(uint64_t), s);   // else: the resolve zeroed them
+    if (!t.hzero) e = hipMemsetAsync(ht.ctr, 0, B3_CTR_BYTES, s);   // else: the resolve zeroed them
     if (e != hipSuccess) return e;
     if (!t.nfiles) return hipSuccess;
     hipLaunchKernelGGL(b3_items_kernel, dim3(ht.n_iblocks), dim3(256), 0, s, t, ht);

@@ -298,7 +298,7 @@ int32_t upload_cut_tables(syncr_cdc *h) {
     for (uint32_t i = 0; i < h->nfiles; i++) icap += (h->h_flen[i] + gbytes - 1) / gbytes + h->h_cut_cap[i];
     h->items_cap = std::max<uint64_t>(icap, 1);
     h->trees_cap = std::max<uint64_t>(acc, 1);
-    CHECK_HIP(h->hctr.ensure(B3C_WORDS * 8));
+    CHECK_HIP(h->hctr.ensure(B3_CTR_BYTES));
     CHECK_HIP(h->items.ensure(h->items_cap * 8));
     CHECK_HIP(h->trees.ensure(h->trees_cap * 16));
     CHECK_HIP(h->gcv.ensure(h->items_cap * 32));

@@ -265,7 +265,7 @@ struct Tables {
     // so a step needs no memset packet (cdc_api.cpp do_launch).
     uint4 *znext;                  // [znext_vec] the next launch's block (nullptr: none)
     uint32_t znext_vec;
-    uint64_t *hzero;               // [B3C_WORDS] hash counters of this launch (hashed launches), or nullptr
+    uint64_t *hzero;               // [B3C_WORDS] + shards: hash counters of this launch (hashed launches), or nullptr
     uint64_t *dbg;                 // development library only (SYNCR_CDC_TRACE=1): [DBG_WORDS] resolve
                                    //   timeline (wall_clock64 stamps, DBG_*), else nullptr
     uint32_t nst;                  // stream-tile scan: STs of the batch (launch geometry)
@@ -310,12 +310,17 @@ constexpr int B3_CLASSES = 7;                               // packed classes: <
 constexpr uint64_t B3_TAIL = 1ull << 63;                  // packed entry: tail unit
 constexpr uint64_t B3_PIECE = 1ull << 62;                 // packed entry: piece (index into pieces[])
 constexpr uint32_t B3_MAX_PIECES = 7;                     // popcount of a task count <= 127
-constexpr uint64_t B3_ITEMS_CUTS = 16384;                 // output slots per b3_items_kernel block
+constexpr uint64_t B3_ITEMS_CUTS = 2048;                  // output slots per b3_items_kernel block (dense1: 1024 blocks)
 enum { B3C_ITEMS = 0, B3C_TREES = 1, B3C_NEXT = 2, B3C_FLAGS = 3, B3C_PK0 = 4, B3C_PIECES = 4 + B3_CLASSES,
        B3C_WORDS = 5 + B3_CLASSES };
+// The leaf kernel's work counters: B3_SHARDS of them, 4 KiB apart (different
+// memory channels: each takes its own atomics), after the B3C_WORDS counters in
+// the same buffer: shard k at ctr[(k + 1) * B3_SHARD_STRIDE].  Zeroed with them.
+constexpr uint32_t B3_SHARDS = 8, B3_SHARD_STRIDE = 512;
+constexpr uint64_t B3_CTR_BYTES = (uint64_t)(B3_SHARDS + 1) * B3_SHARD_STRIDE * 8;
 
 struct HashTables {
-    uint64_t *ctr;                 // [B3C_WORDS] (zeroed per hashed launch)
+    uint64_t *ctr;                 // [B3C_WORDS] + the leaf's shard counters (zeroed per hashed launch)
     uint64_t *items;               // [items_cap] slot << 24 | group (| B3_TAIL: tail placeholder)
     uint64_t items_cap;
     uint64_t *packed;              // [B3_CLASSES * packed_cap] by packed class: a chunk slot, or

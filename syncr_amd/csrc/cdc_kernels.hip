@@ -2279,6 +2279,7 @@ __device__ __forceinline__ void zero_next(const Tables &T) {
     if (T.znext)
         for (uint32_t k = tid; k < T.znext_vec; k += nthr) T.znext[k] = make_uint4(0u, 0u, 0u, 0u);
     if (T.hzero && tid < (uint32_t)B3C_WORDS) T.hzero[tid] = 0ull;
+    if (T.hzero && tid < B3_SHARDS) T.hzero[(tid + 1) * B3_SHARD_STRIDE] = 0ull;
 }
 
 __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restrict__ data, KParams P,

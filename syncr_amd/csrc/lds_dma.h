@@ -64,6 +64,10 @@ __device__ __forceinline__ void dma4(const void *gsrc, uint32_t lds) {
 template <bool NT>
 __device__ __forceinline__ void dma16_s(uint32_t voff, uint64_t sbase, uint32_t lds) {
     lds = (uint32_t)__builtin_amdgcn_readfirstlane(lds);     // M0 takes an SGPR (wave-uniform by contract)
+    // the base too (wave-uniform by contract): the "s" operand must be an SGPR pair
+    // even where the compiler cannot prove the value uniform
+    sbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sbase >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
     uint32_t keep;
     if constexpr (NT)
         asm volatile(

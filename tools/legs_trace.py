@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--shard", type=int, default=0)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--hashed", action="store_true", help="chunk + BLAKE3 (launch_hashed) instead of boundaries only")
     ap.add_argument("--no-events", action="store_true",
                     help="time the K steps with no HIP events at all (what the events cost a small step)")
     args = ap.parse_args()
@@ -67,10 +68,10 @@ def main():
                 dt = (time.perf_counter() - t0) / args.steps
                 r = {"ms_per_step": round(dt * 1e3, 4), "value": round(span / dt / 2**30, 3), "events": False}
             else:
-                r = L.time_steps(ch, b.ptr, span, args.steps, args.warmup)
+                r = L.time_steps(ch, b.ptr, span, args.steps, args.warmup, hashed=args.hashed)
         finally:
             b.free()
-    r.update({"workload": args.workload, "shard": args.shard, "bytes": span, "files": int(lens.size),
+    r.update({"workload": args.workload, "shard": args.shard, "bytes": span, "files": int(lens.size), "hashed": args.hashed,
               "steps": args.steps, "warmup": args.warmup})
     print(json.dumps(r), flush=True)
 
