@@ -80,7 +80,7 @@ struct syncr_cdc {
     uint64_t total_cut_cap = 0;
     std::vector<uint64_t> h_foff, h_flen, h_cut_base;
     std::vector<uint32_t> h_cut_cap;
-    DevBuf fstart, foff, flen, order, cut_base, cut_cap, tile_meta, slots, zeroed,
+    DevBuf fstart, foff, flen, order, ofile, cut_base, cut_cap, tile_meta, slots, zeroed,
         dense_list, dense_cnt, dense_bits, dense_fix, dense_pos, super_off, cand, linkw, cuts, counts;
     // BLAKE3 of every chunk (launch_hashed)
     bool hash_on = false;
@@ -223,6 +223,7 @@ Tables make_tables(syncr_cdc *h) {
     t.foff = h->foff.as<uint64_t>();
     t.flen = h->flen.as<uint64_t>();
     t.order = h->order.as<uint32_t>();
+    t.ofile = h->ofile.as<ulonglong2>();
     t.cut_base = h->cut_base.as<uint64_t>();
     t.cut_cap = h->cut_cap.as<uint32_t>();
     t.tile_meta = h->tile_meta.as<uint32_t>();
@@ -724,6 +725,7 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         CHECK_HIP(h->foff.ensure(std::max<size_t>(nfiles, 1) * 8));
         CHECK_HIP(h->flen.ensure(std::max<size_t>(nfiles, 1) * 8));
         CHECK_HIP(h->order.ensure(std::max<size_t>(nfiles, 1) * 4));
+        CHECK_HIP(h->ofile.ensure(std::max<size_t>(nfiles, 1) * 16));
         CHECK_HIP(h->counts.ensure(std::max<size_t>(nfiles, 1) * 8));
         CHECK_HIP(h->tile_meta.ensure(std::max<size_t>(h->ntiles, 1) * 4));
         CHECK_HIP(h->slots.ensure(std::max<size_t>(h->ntiles, 1) * LISTCAP * sizeof(uint2)));
@@ -745,6 +747,12 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
             CHECK_HIP(hipMemcpy(h->foff.p, file_off, nfiles * 8ull, hipMemcpyHostToDevice));
             CHECK_HIP(hipMemcpy(h->flen.p, file_len, nfiles * 8ull, hipMemcpyHostToDevice));
             CHECK_HIP(hipMemcpy(h->order.p, order.data(), nfiles * 4ull, hipMemcpyHostToDevice));
+            std::vector<uint64_t> of(2ull * nfiles);
+            for (uint32_t k = 0; k < nfiles; k++) {
+                of[2 * k] = file_off[order[k]];
+                of[2 * k + 1] = file_len[order[k]];
+            }
+            CHECK_HIP(hipMemcpy(h->ofile.p, of.data(), nfiles * 16ull, hipMemcpyHostToDevice));
         }
         rc = upload_cut_tables(h);
         if (rc) return rc;

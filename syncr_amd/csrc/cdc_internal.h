@@ -213,6 +213,8 @@ struct Tables {
     uint32_t nfiles;
     const uint64_t *foff, *flen;   // [nfiles] file table (caller order)
     const uint32_t *order;         // [nfiles] resolve order (largest first)
+    const ulonglong2 *ofile;       // [nfiles] {foff, flen} of order[k], in resolve order (read beside
+                                   //   order[k]: one dependent load less at every file walker's start)
     const uint64_t *cut_base;      // [nfiles] first output slot per file
     const uint32_t *cut_cap;       // [nfiles] output slots per file
     uint32_t *tile_meta;           // [ntiles] count or DENSE_BIT|pool index (valid iff nonempty bit)

@@ -2289,7 +2289,8 @@ __global__ __launch_bounds__(64) void cdc_resolve_kernel(const uint8_t *__restri
     const uint32_t kf = blockIdx.x * 64 + threadIdx.x;
     if (kf >= T.nfiles) return;
     const uint32_t i = T.order[kf];
-    const uint64_t F = T.flen[i], g0 = T.foff[i];
+    const ulonglong2 fr = T.ofile[kf];                          // {foff, flen} of file i
+    const uint64_t F = fr.y, g0 = fr.x;
     DevCut *out = T.cuts + T.cut_base[i];
     const uint32_t cap = T.cut_cap[i];
     const uint64_t MAX = P.max_chunk;
@@ -3461,7 +3462,8 @@ __global__ __launch_bounds__(256) void cdc_resolve_wave_kernel(const uint8_t *__
     const uint32_t kf = __builtin_amdgcn_readfirstlane(b * 4 + (threadIdx.x >> 6));
     if (kf >= T.nfiles) return;
     const uint32_t i = T.order[kf];
-    const uint64_t F = T.flen[i], g0 = T.foff[i];
+    const ulonglong2 fr = T.ofile[kf];                          // {foff, flen} of file i
+    const uint64_t F = fr.y, g0 = fr.x;
     const bool elig = kf < T.n_elig;
     if (kf == 0) DBG_STAMP(T, 7);
     if (F <= 0xFFFFFF00ull) {

@@ -19,6 +19,7 @@
 #   restl|<workload>                    resolve timeline (tools/resolve_timeline.py, dev library)
 #   prof|<PROFTAG>[|<extra flags>[|<ENV=V,...>]]  tools/prof.sh: trace + traffic + SQ passes of the driver's
 #                                       command (e.g. "prof|r05_st18|--dev-lib|SYNCR_CDC_ST_SEGS=18")
+#   rehearse|<N>                        torch.distributed.run with N ranks, all on device 0 (a flow check)
 #   build                               python -m syncr_amd.build (+ --dev) on the box (normally built here)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -101,6 +102,13 @@ PY
         cat "$out.txt" ;;
     prof)
         envrun "${a[3]}" bash tools/prof.sh "${a[1]}" ${a[2]} || { echo "prof failed rc=$?"; exit 18; } ;;
+    rehearse)                                  # rehearse|N: the driver's N-rank launcher, every rank on device 0
+        N=${a[1]:-2}
+        DM=$(python3 -c "print(','.join(['0']*$N))")
+        timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" --master-addr 127.0.0.1 \
+            --master-port $((29500 + N)) bench.py --gpus "$N" --steps 20 --warmup 5 --device-map "$DM" > "$out.json" \
+            2> "$out.err" || { echo "rehearse failed rc=$?"; tail -30 "$out.err"; exit 22; }
+        python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print('n_gpus', d['n_gpus'], 'value', d['value'], d.get('load_balance'), d['parity'].get('headline'))" "$out.json" ;;
     build)
         timeout -k 10 900 python -m syncr_amd.build --force > "$out.log" 2>&1 && \
         timeout -k 10 900 python -m syncr_amd.build --force --dev >> "$out.log" 2>&1 || { echo "build failed"; exit 19; } ;;
