@@ -318,11 +318,23 @@ pub async fn compute_file_chunks_gpu(path: &Path, state: &DumpState) -> Option<V
         }
         Err(_) => return None,
     };
+    if needs_cpu(&res) {
+        return None;
+    }
     warn_read_status(path, &res);
     for c in &res.chunks {
         state.add_chunk(util::hash_to_base64(&c.hash), path.to_path_buf(), c.offset, c.size as usize).await;
     }
     Some(res.chunks)
+}
+
+/// A file the engine could not take for lack of memory (its pinned staging and
+/// device buffer are sized to the file: a file larger than what can be pinned
+/// or allocated on the GPU gets SYNCR_CDC_ENOMEM and no chunks).  That is not a
+/// read error of the reference's loop, which streams the file through 16 MiB,
+/// so the file goes to the rollsum loop.
+fn needs_cpu(res: &FileResult) -> bool {
+    res.status == SYNCR_CDC_ENOMEM && res.chunks.is_empty()
 }
 
 /// The reference's warning for a file the engine could not read completely
@@ -390,8 +402,9 @@ pub enum WalkItem {
     /// the entry, complete (a file's chunks filled in, each registered with
     /// DumpState::add_chunk)
     Ready(FileSystemEntry),
-    /// a file the engine could not chunk (it failed): the caller runs the
-    /// rollsum loop on the path and sends the entry with those chunks
+    /// a file the engine could not chunk (it failed, or the file does not fit
+    /// its memory): the caller runs the rollsum loop on the path and sends the
+    /// entry with those chunks
     Cpu(FileSystemEntry, PathBuf),
 }
 
@@ -486,6 +499,7 @@ impl GpuWalk {
         let Queued { mut entry, path, slot } = self.queue.pop_front()?;
         self.popped += 1;
         match slot {
+            Slot::Done(res) if needs_cpu(&res) => Some(WalkItem::Cpu(entry, path)),
             Slot::Done(res) => {
                 warn_read_status(&path, &res);
                 for c in &res.chunks {
