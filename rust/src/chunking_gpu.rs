@@ -477,8 +477,18 @@ impl GpuWalk {
             Ok((pipe, r)) => {
                 self.pipe = Some(pipe);
                 self.collect();
-                if let Err(e) = r {
-                    self.engine_failed(e);
+                match r {
+                    Ok(()) => {}
+                    // this file alone could not be staged (its buffers, sized to the
+                    // file, did not fit): the call returned without queueing it, so no
+                    // result will come for it -- it goes to the rollsum loop, the walk
+                    // goes on on the GPU
+                    Err(GpuError(SYNCR_CDC_ENOMEM)) if self.waiting.back() == Some(&pos) => {
+                        self.waiting.pop_back();
+                        let i = (pos - self.popped) as usize;
+                        self.queue[i].slot = Slot::Cpu;
+                    }
+                    Err(e) => self.engine_failed(e),
                 }
             }
             Err(_) => self.engine_failed(GpuError(SYNCR_CDC_EIO)),   // the pipeline went down with the task
