@@ -942,16 +942,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
     b3_leaf_body<NT, ABLATE, LD, MQ>(data, T, H);
 }
 
-template <bool NT, int AB, int CO, bool MQ = false>
-static void launch_leaf(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
+// The persistent grid: every resident slot, but no more blocks (4 waves each)
+// than the launch can have wave items.  That bound is known on the host before
+// the item planner runs -- group items <= items_cap, and every packed class
+// list holds at most packed_cap entries, a chunk giving at most 7 (a whole unit,
+// or the binary pieces of its task count) -- and on a small batch it keeps the
+// 4096 waves of a full grid from each probing the work counters on their way
+// out (~0.1 ms for a one-file batch: the per-file call site, round 6).
+static uint32_t leaf_blocks(int device, const void *kernel, const HashTables &ht) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
         cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)&b3_leaf_kernel<NT, AB, CO, MQ>, 256, 0) !=
-            hipSuccess ||
-        per <= 0)
-        per = 1;
-    hipLaunchKernelGGL((b3_leaf_kernel<NT, AB, CO, MQ>), dim3((uint32_t)(cus * per)), dim3(256), 0, s, d, t, ht);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per <= 0) per = 1;
+    const uint64_t max_items = ht.items_cap + 7ull * ht.packed_cap + (uint64_t)B3_CLASSES;
+    return (uint32_t)std::max<uint64_t>(1ull, std::min<uint64_t>((uint64_t)cus * (uint64_t)per, (max_items + 3) / 4));
+}
+
+template <bool NT, int AB, int CO, bool MQ = false>
+static void launch_leaf(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
+    const uint32_t blocks = leaf_blocks(device, (const void *)&b3_leaf_kernel<NT, AB, CO, MQ>, ht);
+    hipLaunchKernelGGL((b3_leaf_kernel<NT, AB, CO, MQ>), dim3(blocks), dim3(256), 0, s, d, t, ht);
 }
 
 #ifdef SYNCR_CDC_DEV

@@ -49,6 +49,54 @@ struct DevBuf {
     template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+// Pinned host staging for a handle's small table uploads and result
+// downloads.  A synchronous hipMemcpy from pageable memory costs ~20 us; a
+// one-file batch made ~20 of them (plan's tables, fetch's counters, counts,
+// cuts and hashes): ~0.45 ms of a ~0.5 ms per-file round trip (rocprofv3 HIP
+// trace of the per-file call site, round 6).  A CopyGroup goes out as
+// hipMemcpyAsync through this buffer on the handle's stream and is waited for
+// once; groups above STAGE_MAX use plain hipMemcpy (large tables and results:
+// the runtime stages those itself, and the buffer stays small).
+struct HostStage {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    HostStage() = default;
+    HostStage(const HostStage &) = delete;
+    HostStage &operator=(const HostStage &) = delete;
+    ~HostStage() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t ensure(size_t n) {
+        if (n <= cap && p) return hipSuccess;
+        const size_t want = std::max<size_t>(n, std::max<size_t>(64u << 10, 2 * cap));
+        uint8_t *q = nullptr;
+        const hipError_t e = hipHostMalloc((void **)&q, want, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        if (p) (void)hipHostFree(p);
+        p = q;
+        cap = want;
+        return hipSuccess;
+    }
+};
+constexpr size_t STAGE_MAX = 4u << 20;
+
+// copies of one group: (device, host, bytes); host buffers stay valid until
+// upload() / download() returns
+struct CopyGroup {
+    struct Item {
+        void *dev;
+        void *host;
+        size_t n, off;
+    };
+    std::vector<Item> items;
+    size_t total = 0;
+    void add(void *dev, const void *host, size_t n) {
+        if (!n) return;
+        items.push_back({dev, const_cast<void *>(host), n, total});
+        total += (n + 15) & ~size_t(15);
+    }
+};
+
 constexpr int NPHASE = 4;            // scan, dense+compaction, resolve, hash
 
 struct PendingTiming {
@@ -127,6 +175,8 @@ struct syncr_cdc {
 
     // host-path staging
     DevBuf stage;
+    HostStage hstage;                   // pinned: CopyGroup uploads / downloads
+    std::vector<uint64_t> h_iblocks;    // b3_items_kernel block table (kept for its upload)
 
     // timing
     bool timing = false;
@@ -191,6 +241,41 @@ KParams make_kparams(const syncr_cdc_params &p) {
 
 // Output slots reserved per file: 16x the expected chunk count plus slack; a
 // file that needs more is re-resolved with its exact count (fetch()).
+// host -> device, complete on return
+hipError_t upload(syncr_cdc *h, const CopyGroup &g) {
+    if (g.items.empty()) return hipSuccess;
+    hipError_t e = hipSuccess;
+    if (g.total > STAGE_MAX || (e = h->hstage.ensure(g.total)) != hipSuccess) {
+        for (const auto &it : g.items)
+            if ((e = hipMemcpy(it.dev, it.host, it.n, hipMemcpyHostToDevice)) != hipSuccess) return e;
+        return hipSuccess;
+    }
+    for (const auto &it : g.items) {
+        memcpy(h->hstage.p + it.off, it.host, it.n);
+        if ((e = hipMemcpyAsync(it.dev, h->hstage.p + it.off, it.n, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
+            return e;
+    }
+    return hipStreamSynchronize(h->stream);
+}
+
+// device -> host, complete on return (the caller has waited for the kernels
+// that wrote the device side)
+hipError_t download(syncr_cdc *h, const CopyGroup &g) {
+    if (g.items.empty()) return hipSuccess;
+    hipError_t e = hipSuccess;
+    if (g.total > STAGE_MAX || (e = h->hstage.ensure(g.total)) != hipSuccess) {
+        for (const auto &it : g.items)
+            if ((e = hipMemcpy(it.host, it.dev, it.n, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+        return hipSuccess;
+    }
+    for (const auto &it : g.items)
+        if ((e = hipMemcpyAsync(h->hstage.p + it.off, it.dev, it.n, hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
+            return e;
+    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return e;
+    for (const auto &it : g.items) memcpy(it.host, h->hstage.p + it.off, it.n);
+    return hipSuccess;
+}
+
 uint32_t default_cut_cap(uint64_t len, uint32_t bits) {
     const uint32_t sh = bits > 4 ? bits - 4 : 0;
     uint64_t c = (len >> sh) + 8;
@@ -283,7 +368,7 @@ Tables make_tables(syncr_cdc *h) {
     return t;
 }
 
-int32_t upload_cut_tables(syncr_cdc *h) {
+int32_t upload_cut_tables(syncr_cdc *h, CopyGroup *into = nullptr) {
     h->h_cut_base.resize(h->nfiles);
     uint64_t acc = 0;
     for (uint32_t i = 0; i < h->nfiles; i++) {
@@ -313,7 +398,8 @@ int32_t upload_cut_tables(syncr_cdc *h) {
     // b3_items_kernel blocks: each group of 256 files is split into parts of
     // ~B3_ITEMS_CUTS of its output slots, so one file with millions of chunks
     // (periodic data) is planned by many blocks, not one
-    std::vector<uint64_t> ib;
+    std::vector<uint64_t> &ib = h->h_iblocks;
+    ib.clear();
     for (uint32_t g = 0; g * 256u < h->nfiles; g++) {
         uint64_t caps = 0;
         for (uint32_t i = g * 256u; i < std::min<uint32_t>(h->nfiles, g * 256u + 256u); i++) caps += h->h_cut_cap[i];
@@ -322,14 +408,15 @@ int32_t upload_cut_tables(syncr_cdc *h) {
     }
     h->n_iblocks = (uint32_t)ib.size();
     CHECK_HIP(h->iblocks.ensure(std::max<size_t>(ib.size(), 1) * 8));
-    if (!ib.empty()) CHECK_HIP(hipMemcpy(h->iblocks.p, ib.data(), ib.size() * 8, hipMemcpyHostToDevice));
     CHECK_HIP(h->cut_base.ensure(std::max<size_t>(h->nfiles, 1) * 8));
     CHECK_HIP(h->cut_cap.ensure(std::max<size_t>(h->nfiles, 1) * 4));
     CHECK_HIP(h->cuts.ensure(std::max<uint64_t>(acc, 1) * sizeof(DevCut)));
-    if (h->nfiles) {
-        CHECK_HIP(hipMemcpy(h->cut_base.p, h->h_cut_base.data(), h->nfiles * 8ull, hipMemcpyHostToDevice));
-        CHECK_HIP(hipMemcpy(h->cut_cap.p, h->h_cut_cap.data(), h->nfiles * 4ull, hipMemcpyHostToDevice));
-    }
+    CopyGroup own;
+    CopyGroup &g = into ? *into : own;
+    g.add(h->iblocks.p, ib.data(), ib.size() * 8);
+    g.add(h->cut_base.p, h->h_cut_base.data(), h->nfiles * 8ull);
+    g.add(h->cut_cap.p, h->h_cut_cap.data(), h->nfiles * 4ull);
+    if (!into) CHECK_HIP(upload(h, own));
     return SYNCR_CDC_OK;
 }
 
@@ -741,26 +828,25 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         if (rc) return rc;
         rc = ensure_cand(h, std::max<uint64_t>(4096, 2ull * h->ntiles));
         if (rc) return rc;
-        if (!starts.empty())
-            CHECK_HIP(hipMemcpy(h->fstart.p, starts.data(), starts.size() * 8, hipMemcpyHostToDevice));
-        if (nfiles) {
-            CHECK_HIP(hipMemcpy(h->foff.p, file_off, nfiles * 8ull, hipMemcpyHostToDevice));
-            CHECK_HIP(hipMemcpy(h->flen.p, file_len, nfiles * 8ull, hipMemcpyHostToDevice));
-            CHECK_HIP(hipMemcpy(h->order.p, order.data(), nfiles * 4ull, hipMemcpyHostToDevice));
-            std::vector<uint64_t> of(2ull * nfiles);
-            for (uint32_t k = 0; k < nfiles; k++) {
-                of[2 * k] = file_off[order[k]];
-                of[2 * k + 1] = file_len[order[k]];
-            }
-            CHECK_HIP(hipMemcpy(h->ofile.p, of.data(), nfiles * 16ull, hipMemcpyHostToDevice));
+        // every table of the plan goes up as one copy group (one wait)
+        CopyGroup up;
+        up.add(h->fstart.p, starts.data(), starts.size() * 8);
+        std::vector<uint64_t> of(2ull * nfiles);
+        for (uint32_t k = 0; k < nfiles; k++) {
+            of[2 * k] = file_off[order[k]];
+            of[2 * k + 1] = file_len[order[k]];
         }
-        rc = upload_cut_tables(h);
+        up.add(h->foff.p, file_off, nfiles * 8ull);
+        up.add(h->flen.p, file_len, nfiles * 8ull);
+        up.add(h->order.p, order.data(), nfiles * 4ull);
+        up.add(h->ofile.p, of.data(), nfiles * 16ull);
+        rc = upload_cut_tables(h, &up);
         if (rc) return rc;
         // read-boundary grid points k * read_cap of every file (production only)
         h->ngrid = 0;
+        std::vector<uint64_t> gbase(nfiles), gpos, gend;
         if (h->params.read_cap && nfiles) {
             const uint64_t cap = h->params.read_cap;
-            std::vector<uint64_t> gbase(nfiles), gpos, gend;
             uint64_t acc = 0;
             for (uint32_t i = 0; i < nfiles; i++) {
                 gbase[i] = acc;
@@ -777,12 +863,11 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
             CHECK_HIP(h->gpos.ensure(std::max<uint64_t>(acc, 1) * 8));
             CHECK_HIP(h->gend.ensure(std::max<uint64_t>(acc, 1) * 8));
             CHECK_HIP(h->gfix.ensure(std::max<uint64_t>(acc, 1)));
-            CHECK_HIP(hipMemcpy(h->gbase.p, gbase.data(), nfiles * 8ull, hipMemcpyHostToDevice));
-            if (acc) {
-                CHECK_HIP(hipMemcpy(h->gpos.p, gpos.data(), acc * 8, hipMemcpyHostToDevice));
-                CHECK_HIP(hipMemcpy(h->gend.p, gend.data(), acc * 8, hipMemcpyHostToDevice));
-            }
+            up.add(h->gbase.p, gbase.data(), nfiles * 8ull);
+            up.add(h->gpos.p, gpos.data(), acc * 8);
+            up.add(h->gend.p, gend.data(), acc * 8);
         }
+        CHECK_HIP(upload(h, up));
         h->planned = true;
         return SYNCR_CDC_OK;
     } catch (const std::bad_alloc &) {
@@ -825,8 +910,17 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
         CHECK_HIP(hipSetDevice(h->device));
         for (int attempt = 0; attempt < 8; attempt++) {
             if (h->last_stream) CHECK_HIP(hipStreamSynchronize(h->last_stream));
+            // the launch's counters, per-file counts and split counters in one copy group
             uint32_t ctr[4];
-            CHECK_HIP(hipMemcpy(ctr, zblock(h, h->zlast), 16, hipMemcpyDeviceToHost));
+            std::vector<uint64_t> counts(h->nfiles);
+            uint32_t sp[SPL_WORDS];
+            {
+                CopyGroup dn;
+                dn.add(zblock(h, h->zlast), ctr, 16);
+                dn.add(h->counts.p, counts.data(), h->nfiles * 8ull);
+                dn.add(zblock(h, h->zlast) + split_ctr_offset(h), sp, sizeof sp);
+                CHECK_HIP(download(h, dn));
+            }
             const uint64_t ncand = (uint64_t)ctr[CTR_CANDS_LO] | ((uint64_t)ctr[CTR_CANDS_HI] << 32);
             // for the next launch (also a re-run below): >= 64 Ki candidates at >= 1
             // per 16 KiB (random data: ~1 per MiB at chunk_bits 20)
@@ -836,13 +930,8 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
                 int32_t rc = ensure_split(h);
                 if (rc) return rc;
             }
-            std::vector<uint64_t> counts(h->nfiles);
-            if (h->nfiles)
-                CHECK_HIP(hipMemcpy(counts.data(), h->counts.p, h->nfiles * 8ull, hipMemcpyDeviceToHost));
 #ifdef SYNCR_CDC_DEV
             if (getenv("SYNCR_CDC_DEBUG_FETCH")) {
-                uint32_t sp[SPL_WORDS];
-                CHECK_HIP(hipMemcpy(sp, zblock(h, h->zlast) + split_ctr_offset(h), sizeof sp, hipMemcpyDeviceToHost));
                 fprintf(stderr, "fetch attempt %d: flags %u ncand %llu dense %u cand_cap %llu dense_cap %u seg_cap %u | "
                         "pub %u split %u reserved %u head %u done %u | counts",
                         attempt, ctr[CTR_FLAGS], (unsigned long long)ncand, ctr[CTR_DENSE],
@@ -903,9 +992,6 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
             h->stats[2] = h->ntiles;
             h->stats[3] = ctr[CTR_FLAGS];
             {
-                uint32_t sp[SPL_WORDS];
-                CHECK_HIP(hipMemcpy(sp, zblock(h, h->zlast) + split_ctr_offset(h), sizeof sp,
-                                    hipMemcpyDeviceToHost));
                 // dense tiles the dense pass rolled (in the development library's
                 // DenseSlots scans the list counter also counts unused 8-slot padding)
                 h->stats[1] = ctr[CTR_DENSE] ? sp[SPL_DENSE_TILES] : 0u;
@@ -926,18 +1012,21 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
             if (n_out) *n_out = total;
             if (total > cap || (total && !(hashed ? (void *)hout : (void *)out))) return SYNCR_CDC_ERANGE;
             if (total) {
+                // the cut slots (and hash counters and hashes) in one copy group
                 std::vector<DevCut> all(h->total_cut_cap);
-                CHECK_HIP(hipMemcpy(all.data(), h->cuts.p, h->total_cut_cap * sizeof(DevCut), hipMemcpyDeviceToHost));
                 std::vector<uint8_t> hs;
+                uint64_t hc[B3C_WORDS];
+                CopyGroup dn;
+                dn.add(h->cuts.p, all.data(), h->total_cut_cap * sizeof(DevCut));
                 if (hashed) {
-                    uint64_t hc[B3C_WORDS];
-                    CHECK_HIP(hipMemcpy(hc, h->hctr.p, sizeof hc, hipMemcpyDeviceToHost));
-                    if (hc[B3C_FLAGS] || hc[B3C_ITEMS] > h->items_cap || hc[B3C_TREES] > h->trees_cap ||
-                        hc[B3C_PIECES] > h->pieces_cap)
-                        return SYNCR_CDC_EIO;          // capacities are exact bounds: cannot happen
                     hs.resize(h->total_cut_cap * 32);
-                    CHECK_HIP(hipMemcpy(hs.data(), h->hashes.p, hs.size(), hipMemcpyDeviceToHost));
+                    dn.add(h->hctr.p, hc, sizeof hc);
+                    dn.add(h->hashes.p, hs.data(), hs.size());
                 }
+                CHECK_HIP(download(h, dn));
+                if (hashed && (hc[B3C_FLAGS] || hc[B3C_ITEMS] > h->items_cap || hc[B3C_TREES] > h->trees_cap ||
+                               hc[B3C_PIECES] > h->pieces_cap))
+                    return SYNCR_CDC_EIO;              // capacities are exact bounds: cannot happen
                 uint64_t o = 0;
                 for (uint32_t i = 0; i < h->nfiles; i++) {
                     const uint64_t b = h->h_cut_base[i];

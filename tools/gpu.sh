@@ -20,6 +20,8 @@
 #   prof|<PROFTAG>[|<extra flags>[|<ENV=V,...>]]  tools/prof.sh: trace + traffic + SQ passes of the driver's
 #                                       command (e.g. "prof|r05_st18|--dev-lib|SYNCR_CDC_ST_SEGS=18")
 #   rehearse|<N>                        torch.distributed.run with N ranks, all on device 0 (a flow check)
+#   e2etrace|<mode>|<files>             benchlib/e2e_driver.cpp <mode> over the first <files> zipf10k files,
+#                                       under rocprofv3 --kernel-trace --hip-trace --stats
 #   build                               python -m syncr_amd.build (+ --dev) on the box (normally built here)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -109,6 +111,16 @@ PY
             --master-port $((29500 + N)) bench.py --gpus "$N" --steps 20 --warmup 5 --device-map "$DM" > "$out.json" \
             2> "$out.err" || { echo "rehearse failed rc=$?"; tail -30 "$out.err"; exit 22; }
         python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print('n_gpus', d['n_gpus'], 'value', d['value'], d.get('load_balance'), d['parity'].get('headline'))" "$out.json" ;;
+    e2etrace)                                  # e2etrace|<mode>|<files>: one e2e_driver mode under the kernel + HIP API trace
+        P=$O/${TAG}_${n}_e2etrace_${a[1]}
+        mkdir -p "$P"
+        timeout -k 10 300 python3 tools/e2e_tree.py /tmp/syncr_e2e_tree --files "${a[2]:-500}" > "$P/tree.log" 2>&1 || { echo "tree failed"; exit 23; }
+        python3 -c "from benchlib import e2e; e2e.driver()" || exit 23
+        ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d "$P" -o run -- \
+            "$R/build/e2e_driver" "${a[1]}" /tmp/syncr_e2e_tree "$P/results.bin" --reps 1 > "$P/driver.json" 2> "$P/driver.err" ) \
+            || { echo "e2etrace failed rc=$?"; tail -20 "$P/driver.err"; exit 24; }
+        rm -rf /tmp/syncr_e2e_tree "$P/results.bin"
+        cat "$P/driver.json"; head -12 "$P"/*kernel_stats.csv; head -15 "$P"/*hip_api_stats.csv 2>/dev/null ;;
     build)
         timeout -k 10 900 python -m syncr_amd.build --force > "$out.log" 2>&1 && \
         timeout -k 10 900 python -m syncr_amd.build --force --dev >> "$out.log" 2>&1 || { echo "build failed"; exit 19; } ;;
