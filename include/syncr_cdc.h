@@ -222,8 +222,8 @@ int32_t syncr_ingest_submit_file(syncr_ingest *g, const char *path, uint64_t tag
 int32_t syncr_ingest_reserve(syncr_ingest *g, uint64_t len, uint8_t **dst);
 int32_t syncr_ingest_commit(syncr_ingest *g, uint64_t tag);
 /* seal the current batch and deliver every outstanding file; staging grown
- * past 4 x batch_bytes for an oversized file is released (an idle pipeline
- * holds at most depth x 4 x batch_bytes of pinned and device memory) */
+ * past 2 x batch_bytes for an oversized file is released (an idle pipeline
+ * holds at most depth x 2 x batch_bytes of pinned and device memory) */
 int32_t syncr_ingest_flush(syncr_ingest *g);
 /* [files, bytes, batches, chunks] so far */
 int32_t syncr_ingest_stats(const syncr_ingest *g, uint64_t *stats4);

@@ -326,10 +326,16 @@ int32_t ensure_slot(Pipe *g, Slot &s, uint64_t bytes) {
 // device memory returns to depth x batch_bytes between runs of oversized files.
 // (Shrinking right after each oversized file made a stream of them pay a
 // device-synchronising free and a fresh pin per file: ADVICE r4.)
+// A slot of up to KEEP_GROWN batches is kept as it is (the memory stays
+// bounded, and a one-file-per-batch caller -- the per-file call site's depth-1
+// pipelines -- met a file between 1 and 2 batches every ~100 files of zipf10k:
+// a fresh pin and a device-synchronising free each time cost ~0.1 s per 10 000
+// files); a bigger one shrinks after SHRINK_AFTER batch-sized batches, or at
+// the next flush.
 constexpr uint32_t SHRINK_AFTER = 4;
-constexpr uint64_t TRIM_ON_FLUSH = 4;       // flush shrinks slots larger than this many batches
+constexpr uint64_t KEEP_GROWN = 2;
 void shrink_slot(Pipe *g, Slot &s, bool oversized) {
-    if (s.cap <= std::max<uint64_t>(g->batch, 64) || s.inflight || s.used) return;
+    if (s.cap <= KEEP_GROWN * std::max<uint64_t>(g->batch, 64) || s.inflight || s.used) return;
     s.small_uses = oversized ? 0u : s.small_uses + 1u;
     if (s.small_uses < SHRINK_AFTER) return;
     s.small_uses = 0;
@@ -735,12 +741,12 @@ int32_t pipe_flush(Pipe *g) {
         if (rc) return rc;
     }
     g->cur = (g->cur + 1) % n;
-    // An idle pipeline keeps at most TRIM_ON_FLUSH x batch_bytes per slot: a
-    // slot grown past that for one huge file is shrunk now, not after
-    // SHRINK_AFTER more batches that may never come (a pooled per-file
-    // pipeline can sit idle for the rest of the process).
+    // An idle pipeline keeps at most KEEP_GROWN x batch_bytes per slot: a slot
+    // grown past that for one huge file is shrunk now, not after SHRINK_AFTER
+    // more batches that may never come (a pooled per-file pipeline can sit idle
+    // for the rest of the process).
     for (Slot &s : g->slots)
-        if (s.cap > TRIM_ON_FLUSH * std::max<uint64_t>(g->batch, 64)) {
+        if (s.cap > KEEP_GROWN * std::max<uint64_t>(g->batch, 64)) {
             s.small_uses = SHRINK_AFTER;
             shrink_slot(g, s, false);
         }
