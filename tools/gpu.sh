@@ -22,6 +22,8 @@
 #   rehearse|<N>                        torch.distributed.run with N ranks, all on device 0 (a flow check)
 #   e2etrace|<mode>|<files>             benchlib/e2e_driver.cpp <mode> over the first <files> zipf10k files,
 #                                       under rocprofv3 --kernel-trace --hip-trace --stats
+#   e2eab|<libdirs,>[|<modes,>[|<rounds>]]  tools/e2e_ab.py: e2e_driver legs against several library builds,
+#                                       interleaved (e.g. "e2eab|syncr_amd,build/ab_pre/syncr_amd")
 #   build                               python -m syncr_amd.build (+ --dev) on the box (normally built here)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -121,6 +123,10 @@ PY
             || { echo "e2etrace failed rc=$?"; tail -20 "$P/driver.err"; exit 24; }
         rm -rf /tmp/syncr_e2e_tree "$P/results.bin"
         cat "$P/driver.json"; head -12 "$P"/*kernel_stats.csv; head -15 "$P"/*hip_api_stats.csv 2>/dev/null ;;
+    e2eab)
+        timeout -k 10 900 python -u tools/e2e_ab.py --libs "${a[1]}" --modes "${a[2]:-files,mem,zero_copy,walk}" \
+            --rounds "${a[3]:-3}" > "$out.jsonl" 2> "$out.err" || { echo "e2eab failed rc=$?"; tail -20 "$out.err"; exit 25; }
+        tail -1 "$out.jsonl" ;;
     build)
         timeout -k 10 900 python -m syncr_amd.build --force > "$out.log" 2>&1 && \
         timeout -k 10 900 python -m syncr_amd.build --force --dev >> "$out.log" 2>&1 || { echo "build failed"; exit 19; } ;;
