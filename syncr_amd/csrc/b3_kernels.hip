@@ -9,7 +9,8 @@
 // compressed in sequence) whose chaining values (CVs) are merged in a
 // left-balanced binary tree of PARENT compressions; the last compression of
 // the root gets the ROOT flag.  Leaves are independent; a lane TASK is
-// LPL = B3_LANE_LEAVES consecutive leaves (contiguous bytes):
+// LPL consecutive leaves (contiguous bytes; LPL = B3_LANE_LEAVES, or 1 on a
+// launch of at most B3_SMALL_SPAN bytes: HashTables::lpl_log):
 //   b3_items_kernel  one block per 256 files (per part of their cut list): a chunk of T <= 64 tasks goes to packed
 //                    class c = ceil(log2 T) (64 >> c chunks share a wave, each
 //                    in an aligned run of 2^c lanes); a bigger chunk becomes
@@ -205,8 +206,8 @@ __device__ __forceinline__ uint32_t agg_inc(uint32_t *cnt, uint32_t key) {
 }
 
 __device__ __forceinline__ uint32_t chunk_leaves(uint32_t len) { return len ? (len + 1023u) >> 10 : 1u; }
-__device__ __forceinline__ uint32_t chunk_tasks(uint32_t len) {
-    return (chunk_leaves(len) + B3_LANE_LEAVES - 1) / B3_LANE_LEAVES;
+__device__ __forceinline__ uint32_t chunk_tasks(uint32_t len, uint32_t lpl_log) {
+    return (chunk_leaves(len) + (1u << lpl_log) - 1u) >> lpl_log;
 }
 __device__ __forceinline__ uint32_t ceil_log2(uint32_t t) { return t <= 1 ? 0u : 32u - __builtin_clz(t - 1); }
 
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(256) void b3_items_kernel(Tables T, HashTables H) {
     };
     auto one = [&](bool place, uint64_t slot, uint32_t len) {
         {
-            const uint32_t tk = chunk_tasks(len);
+            const uint32_t tk = chunk_tasks(len, H.lpl_log);
             if (tk <= 64) {
                 if ((tk & (tk - 1)) == 0 || H.nosplit) {  // one unit: the whole chunk
                     const uint32_t c = ceil_log2(tk);
@@ -410,7 +411,7 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // lines (profiles/r02_fetch_calibration.json: 1.34x the input bytes).
 // The next pair is issued once block t+1 is in registers, so it lands under
 // block t+1's compression, as the single-block round lands under block t's.
-template <bool NT, int ABLATE, int LD>
+template <bool NT, int ABLATE, int LD, uint32_t LPL>
 __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ data, uint64_t span, uint32_t stage,
                                                  uint32_t *stage_ptr, int lane, bool act, uint64_t tp,
                                                  uint32_t nbytes, uint32_t nblk, uint32_t nl, uint32_t nleaves,
@@ -418,6 +419,8 @@ __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ dat
                                                  uint32_t x[8]) {
     // leaf CVs are folded as they complete (left-balanced pairing of <= 4
     // leaves): x = leaf 0, then node(0,1); y = leaf 2, then node(2,3)
+    static_assert(LPL == 1 || LPL == 4, "lane tasks of 1 or 4 leaves");
+    constexpr uint32_t TASK = 1024u * LPL;                    // bytes per lane task
     uint32_t y[8];
     // piece at task byte ps (multiple of 16) is DMA'd iff ps < plim: inside the
     // chunk's task and 16 bytes inside the batch
@@ -434,17 +437,17 @@ __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ dat
         if constexpr (PAIR) {
             if (uni) {
                 // a group item inside the batch (wave-uniform): task q starts at
-                // tp0 + 4096 q, so instruction i's source is the SGPR base
-                // tp0 + 64 t + 32768 i plus a per-lane offset fixed for the item
+                // tp0 + TASK q, so instruction i's source is the SGPR base
+                // tp0 + 64 t + 8 TASK i plus a per-lane offset fixed for the item
                 // ((q >> 1) & 3 == (lane >> 4) & 3 for every i) -- no shuffles, no
                 // per-piece branch; pieces past a partial last task are fetched
                 // from inside the batch and overwritten by the owner's fix-up
                 const uint32_t pos = (uint32_t)lane & 7u;
                 const uint32_t pc = (pos & 4u) | ((pos & 3u) ^ (((uint32_t)lane >> 4) & 3u));
-                const uint32_t voff = ((uint32_t)lane >> 3) * 4096u + pc * 16u;
+                const uint32_t voff = ((uint32_t)lane >> 3) * TASK + pc * 16u;
                 const uint64_t b = (uint64_t)(data + tp0) + (uint64_t)t * 64u;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) dma16_s<NT>(voff, b + 32768ull * (uint64_t)i, stage + (uint32_t)i * 1024u);
+                for (int i = 0; i < 8; ++i) dma16_s<NT>(voff, b + 8ull * TASK * (uint64_t)i, stage + (uint32_t)i * 1024u);
                 return;
             }
         }
@@ -478,7 +481,7 @@ __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ dat
     uint8_t *const mine0 = (uint8_t *)stage_ptr + lane * (PAIR ? 128 : 64);
     if (ABLATE != 2 && tmax) issue(0);
 #pragma unroll
-    for (uint32_t jj = 0; jj < B3_LANE_LEAVES; ++jj) {
+    for (uint32_t jj = 0; jj < LPL; ++jj) {
         if (16 * jj < tmax) {                                    // uniform
             uint32_t cv[8];
             set_iv(cv);
@@ -545,7 +548,7 @@ __device__ __forceinline__ void leaf_blocks_coop(const uint8_t *__restrict__ dat
             }
         }
     }
-    if (nl > 2) parent(x, y, task_root ? B3_ROOT : 0u);
+    if (LPL > 2 && nl > 2) parent(x, y, task_root ? B3_ROOT : 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -669,10 +672,10 @@ __device__ __forceinline__ void merge_quads(uint32_t *slot_ptr, int lane, uint32
 // the packed classes 6..0.  Per lane: a chunk slot, its task k (leaves
 // LPL*k .. LPL*k+LPL-1) and the merge geometry of that chunk within the wave.
 // ---------------------------------------------------------------------------
-template <bool NT, int ABLATE, int LD, bool MQ>
+template <bool NT, int ABLATE, int LD, bool MQ, uint32_t LPL>
 __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, const Tables &T,
                                              const HashTables &H) {
-    constexpr uint32_t LPL = B3_LANE_LEAVES;
+    constexpr uint32_t LG = LPL == 1 ? 0u : 2u;                 // == H.lpl_log (the host launches this instance)
     const int lane = threadIdx.x & 63;
     constexpr bool COOP = LD != LD_PLAIN;
     constexpr uint32_t SLOT = LD == LD_PAIR ? 2048 : 1024;       // words: per-wave staging slot (8 / 4 KiB)
@@ -774,7 +777,7 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
             cstart = T.foff[cu.file] + cu.offset;                // batch offset of the chunk
             if (!group) {
                 k += k0;
-                mm = min(dmax, chunk_tasks(len) - k0);           // a piece before the last one is full
+                mm = min(dmax, chunk_tasks(len, LG) - k0);       // a piece before the last one is full
             }
         }
         // where the unit's CV goes, fixed before the block loop (slot and
@@ -790,10 +793,10 @@ __device__ __forceinline__ void b3_leaf_body(const uint8_t *__restrict__ data, c
         const bool task_root = root && mm == 1;                  // the task is the whole chunk
         uint32_t x[8];
         if constexpr (COOP) {
-            // uniform fast loader: a group item whose 64 tasks (256 KiB) lie inside the batch
-            const uint64_t tp0 = group ? bcast64(cstart + ((uint64_t)k0 << 12)) : 0ull;
-            const bool uni = group && tp0 + (64ull << 12) + 16u <= T.span && !H.nouni;
-            leaf_blocks_coop<NT, ABLATE, LD>(data, T.span, stage, stage_ptr, lane, act, cstart + lane_off, nbytes,
+            // uniform fast loader: a group item whose 64 tasks (64 LPL KiB) lie inside the batch
+            const uint64_t tp0 = group ? bcast64(cstart + (uint64_t)k0 * (1024u * LPL)) : 0ull;
+            const bool uni = group && tp0 + 64ull * 1024u * LPL + 16u <= T.span && !H.nouni;
+            leaf_blocks_coop<NT, ABLATE, LD, LPL>(data, T.span, stage, stage_ptr, lane, act, cstart + lane_off, nbytes,
                                          nblk, nl, nleaves, j0, task_root, uni, tp0, x);
         } else {
             uint32_t lc[LPL][8];                                 // leaf CVs
@@ -884,7 +887,7 @@ __global__ __launch_bounds__(256) void b3_tree_kernel(Tables T, HashTables H) {
         const ulonglong2 e = H.trees[w];
         const uint64_t slot = e.x;
         const bool small = e.y == ~0ull;                 // a split packed chunk: pieces only
-        uint32_t n = small ? 1u : (chunk_tasks(T.cuts[slot].len) + 63) / 64;
+        uint32_t n = small ? 1u : (chunk_tasks(T.cuts[slot].len, H.lpl_log) + 63) / 64;
         const uint64_t tp = H.tpieces[w];
         const uint32_t np = (uint32_t)(tp & 0xffu);
         if (np) {
@@ -937,9 +940,9 @@ __global__ __launch_bounds__(256) void b3_tree_kernel(Tables T, HashTables H) {
     }
 }
 
-template <bool NT, int ABLATE, int LD, bool MQ>
+template <bool NT, int ABLATE, int LD, bool MQ, uint32_t LPL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b3_leaf_kernel(const uint8_t *__restrict__ data, Tables T, HashTables H) {
-    b3_leaf_body<NT, ABLATE, LD, MQ>(data, T, H);
+    b3_leaf_body<NT, ABLATE, LD, MQ, LPL>(data, T, H);
 }
 
 // The persistent grid: every resident slot, but no more blocks (4 waves each)
@@ -958,17 +961,19 @@ static uint32_t leaf_blocks(int device, const void *kernel, const HashTables &ht
     return (uint32_t)std::max<uint64_t>(1ull, std::min<uint64_t>((uint64_t)cus * (uint64_t)per, (max_items + 3) / 4));
 }
 
-template <bool NT, int AB, int CO, bool MQ = false>
+template <bool NT, int AB, int CO, bool MQ = false, uint32_t LPL = B3_LANE_LEAVES>
 static void launch_leaf(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
-    const uint32_t blocks = leaf_blocks(device, (const void *)&b3_leaf_kernel<NT, AB, CO, MQ>, ht);
-    hipLaunchKernelGGL((b3_leaf_kernel<NT, AB, CO, MQ>), dim3(blocks), dim3(256), 0, s, d, t, ht);
+    const uint32_t blocks = leaf_blocks(device, (const void *)&b3_leaf_kernel<NT, AB, CO, MQ, LPL>, ht);
+    hipLaunchKernelGGL((b3_leaf_kernel<NT, AB, CO, MQ, LPL>), dim3(blocks), dim3(256), 0, s, d, t, ht);
 }
 
 #ifdef SYNCR_CDC_DEV
 // development library only: per-lane loads, non-temporal loads and the
 // timing-only ablations (loads only / no loads), selected by SYNCR_B3_* variables
+// (with 4-leaf lane tasks: the host plans those variants with lpl_log 2)
 template <int CO, bool MQ = false>
 static hipError_t launch_leaf_v(int device, const uint8_t *d, const Tables &t, const HashTables &ht, hipStream_t s) {
+    if (ht.lpl_log != 2) return hipErrorInvalidValue;
     switch (ht.ablate * 2 + (ht.nt ? 1 : 0)) {
         case 0: launch_leaf<false, 0, CO, MQ>(device, d, t, ht, s); break;
         case 1: launch_leaf<true, 0, CO, MQ>(device, d, t, ht, s); break;
@@ -988,7 +993,8 @@ hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const Hash
     if (!t.nfiles) return hipSuccess;
     hipLaunchKernelGGL(b3_items_kernel, dim3(ht.n_iblocks), dim3(256), 0, s, t, ht);
 #ifdef SYNCR_CDC_DEV
-    e = ht.coop == 3   ? launch_leaf_v<LD_PAIR, true>(device, d, t, ht, s)
+    if (ht.coop == 3 && !ht.ablate && !ht.nt && ht.lpl_log == 0) launch_leaf<false, 0, LD_PAIR, true, 1>(device, d, t, ht, s);
+    else e = ht.coop == 3   ? launch_leaf_v<LD_PAIR, true>(device, d, t, ht, s)
         : ht.coop == 2 ? launch_leaf_v<LD_PAIR>(device, d, t, ht, s)
         : ht.coop == 1 ? launch_leaf_v<LD_COOP64>(device, d, t, ht, s)
                        : launch_leaf_v<LD_PLAIN>(device, d, t, ht, s);
@@ -996,8 +1002,10 @@ hipError_t launch_hash(int device, const uint8_t *d, const Tables &t, const Hash
 #else
     // the one exact product instance: two blocks per loader round (zipf10k, same
     // process: leaf HBM reads 1.34x -> 1.255x of the input, time within 0.5 %)
-    // and quad-parallel cross-lane merges (leaf 4.157 -> 4.068 ms, same process)
-    launch_leaf<false, 0, LD_PAIR, true>(device, d, t, ht, s);
+    // and quad-parallel cross-lane merges (leaf 4.157 -> 4.068 ms, same process);
+    // 1-leaf lane tasks on a small launch (cdc_internal.h, B3_SMALL_SPAN)
+    if (ht.lpl_log == 0) launch_leaf<false, 0, LD_PAIR, true, 1>(device, d, t, ht, s);
+    else launch_leaf<false, 0, LD_PAIR, true, B3_LANE_LEAVES>(device, d, t, ht, s);
 #endif
     const uint64_t want = (ht.trees_cap + 3) / 4;
     const uint32_t blocks = (uint32_t)(want < 4096 ? (want ? want : 1) : 4096);

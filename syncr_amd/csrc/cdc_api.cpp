@@ -53,12 +53,16 @@ struct DevBuf {
 // downloads.  A synchronous hipMemcpy from pageable memory costs ~20 us; a
 // one-file batch made ~20 of them (plan's tables, fetch's counters, counts,
 // cuts and hashes): ~0.45 ms of a ~0.5 ms per-file round trip (rocprofv3 HIP
-// trace of the per-file call site, round 6).  A CopyGroup goes out as
-// hipMemcpyAsync through this buffer on the handle's stream and is waited for
-// once; groups above STAGE_MAX use plain hipMemcpy (large tables and results:
-// the runtime stages those itself, and the buffer stays small).
+// trace of the per-file call site, round 6).  A CopyGroup goes through this
+// buffer on the handle's stream and is waited for once: up to KCOPY_MAX bytes as
+// one cdc_copy_kernel dispatch that reads (upload) or writes (download) the
+// buffer across PCIe -- coherent memory, so nothing of it is cached on the
+// device -- else one hipMemcpyAsync per table; groups above STAGE_MAX use plain
+// hipMemcpy (large tables and results: the runtime stages those itself, and the
+// buffer stays small).
 struct HostStage {
     uint8_t *p = nullptr;
+    uint8_t *d = nullptr;               // the same memory, as the device addresses it
     size_t cap = 0;
     HostStage() = default;
     HostStage(const HostStage &) = delete;
@@ -69,16 +73,22 @@ struct HostStage {
     hipError_t ensure(size_t n) {
         if (n <= cap && p) return hipSuccess;
         const size_t want = std::max<size_t>(n, std::max<size_t>(64u << 10, 2 * cap));
-        uint8_t *q = nullptr;
-        const hipError_t e = hipHostMalloc((void **)&q, want, hipHostMallocDefault);
+        uint8_t *q = nullptr, *qd = nullptr;
+        hipError_t e = hipHostMalloc((void **)&q, want, hipHostMallocCoherent);
         if (e != hipSuccess) return e;
+        if ((e = hipHostGetDevicePointer((void **)&qd, q, 0)) != hipSuccess) {
+            (void)hipHostFree(q);
+            return e;
+        }
         if (p) (void)hipHostFree(p);
         p = q;
+        d = qd;
         cap = want;
         return hipSuccess;
     }
 };
 constexpr size_t STAGE_MAX = 4u << 20;
+constexpr size_t KCOPY_MAX = 256u << 10;
 
 // copies of one group: (device, host, bytes); host buffers stay valid until
 // upload() / download() returns
@@ -132,6 +142,8 @@ struct syncr_cdc {
         dense_list, dense_cnt, dense_bits, dense_fix, dense_pos, super_off, cand, linkw, cuts, counts;
     // BLAKE3 of every chunk (launch_hashed)
     bool hash_on = false;
+    uint32_t b3_lpl_log = 2;           // leaves per lane task of the planned launch (log2; upload_cut_tables)
+    uint32_t b3_lpl = 0;               // dev A/B only (SYNCR_B3_LPL=1|4): force it; 0 = by span
     uint32_t b3_ablate = 0, b3_nt = 0, b3_coop = 3, b3_nosplit = 0, b3_nouni = 0;     // dev A/B knobs; coop 3 = the product (LD_PAIR + quad merges)
     uint64_t items_cap = 0, trees_cap = 0;
     DevBuf hctr, items, trees, gcv, hashes, packed, tpieces, pieces, pcv, iblocks;
@@ -161,6 +173,21 @@ struct syncr_cdc {
     // resolve of launch k zeroes the other one for launch k+1
     uint32_t zpar = 0, zlast = 0;
     bool zclean[2] = {false, false};
+
+    // the fetched launch's results on the host: valid from its first fetch until
+    // the next plan or launch, so the count-then-fetch pattern (cap 0 for the
+    // total, then the caller's buffer: syncr_ingest's complete()) waits for the
+    // device once; a small launch's cut slots and hashes come down with its
+    // counters in that same wait
+    struct FetchCache {
+        bool valid = false, cuts = false;
+        uint32_t ctr[4];
+        std::vector<uint64_t> counts;
+        uint32_t sp[SPL_WORDS];
+        std::vector<DevCut> all;
+        uint64_t hc[B3C_WORDS];
+        std::vector<uint8_t> hs;
+    } fc;
 
     // launch
     bool launched = false;
@@ -242,6 +269,14 @@ KParams make_kparams(const syncr_cdc_params &p) {
 // Output slots reserved per file: 16x the expected chunk count plus slack; a
 // file that needs more is re-resolved with its exact count (fetch()).
 // host -> device, complete on return
+// the group as one copy dispatch: small, few tables, whole 4-byte words
+bool one_dispatch(const CopyGroup &g) {
+    if (g.total > KCOPY_MAX || g.items.size() > (size_t)COPY_MAX) return false;
+    for (const auto &it : g.items)
+        if (it.n & 3u) return false;
+    return true;
+}
+
 hipError_t upload(syncr_cdc *h, const CopyGroup &g) {
     if (g.items.empty()) return hipSuccess;
     hipError_t e = hipSuccess;
@@ -250,10 +285,16 @@ hipError_t upload(syncr_cdc *h, const CopyGroup &g) {
             if ((e = hipMemcpy(it.dev, it.host, it.n, hipMemcpyHostToDevice)) != hipSuccess) return e;
         return hipSuccess;
     }
-    for (const auto &it : g.items) {
-        memcpy(h->hstage.p + it.off, it.host, it.n);
-        if ((e = hipMemcpyAsync(it.dev, h->hstage.p + it.off, it.n, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
-            return e;
+    for (const auto &it : g.items) memcpy(h->hstage.p + it.off, it.host, it.n);
+    if (one_dispatch(g)) {
+        CopyList l{};
+        for (const auto &it : g.items) l.seg[l.n++] = CopySeg{h->hstage.d + it.off, it.dev, it.n};
+        if ((e = launch_copy(l, g.total, h->stream)) != hipSuccess) return e;
+    } else {
+        for (const auto &it : g.items)
+            if ((e = hipMemcpyAsync(it.dev, h->hstage.p + it.off, it.n, hipMemcpyHostToDevice, h->stream)) !=
+                hipSuccess)
+                return e;
     }
     return hipStreamSynchronize(h->stream);
 }
@@ -268,9 +309,16 @@ hipError_t download(syncr_cdc *h, const CopyGroup &g) {
             if ((e = hipMemcpy(it.host, it.dev, it.n, hipMemcpyDeviceToHost)) != hipSuccess) return e;
         return hipSuccess;
     }
-    for (const auto &it : g.items)
-        if ((e = hipMemcpyAsync(h->hstage.p + it.off, it.dev, it.n, hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
-            return e;
+    if (one_dispatch(g)) {
+        CopyList l{};
+        for (const auto &it : g.items) l.seg[l.n++] = CopySeg{it.dev, h->hstage.d + it.off, it.n};
+        if ((e = launch_copy(l, g.total, h->stream)) != hipSuccess) return e;
+    } else {
+        for (const auto &it : g.items)
+            if ((e = hipMemcpyAsync(h->hstage.p + it.off, it.dev, it.n, hipMemcpyDeviceToHost, h->stream)) !=
+                hipSuccess)
+                return e;
+    }
     if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return e;
     for (const auto &it : g.items) memcpy(it.host, h->hstage.p + it.off, it.n);
     return hipSuccess;
@@ -376,10 +424,13 @@ int32_t upload_cut_tables(syncr_cdc *h, CopyGroup *into = nullptr) {
         acc += h->h_cut_cap[i];
     }
     h->total_cut_cap = acc;
-    // BLAKE3 items: a chunk of len bytes is ceil(leaves / B3_GROUP_LEAVES) items
-    // (the last may be a tail placeholder), so a file needs at most
+    // BLAKE3 lane tasks: 1 leaf on a small launch, B3_LANE_LEAVES otherwise
+    // (cdc_internal.h).  A chunk of len bytes is ceil(leaves / (64 LPL)) group
+    // items (the last may be a tail placeholder), so a file needs at most
     // ceil(F / group bytes) + (its cuts) of them
-    const uint64_t gbytes = 1024ull * B3_GROUP_LEAVES;
+    const bool variant = h->b3_coop != 3 || h->b3_ablate || h->b3_nt;    // dev loaders: 4-leaf instances only
+    h->b3_lpl_log = (h->b3_lpl ? h->b3_lpl == 1 : h->span <= B3_SMALL_SPAN) && !variant ? 0u : 2u;
+    const uint64_t gbytes = (1024ull * 64ull) << h->b3_lpl_log;
     uint64_t icap = 0;
     for (uint32_t i = 0; i < h->nfiles; i++) icap += (h->h_flen[i] + gbytes - 1) / gbytes + h->h_cut_cap[i];
     h->items_cap = std::max<uint64_t>(icap, 1);
@@ -440,6 +491,7 @@ HashTables make_hash_tables(syncr_cdc *h) {
     t.coop = h->b3_coop;
     t.iblocks = h->iblocks.as<uint64_t>();
     t.n_iblocks = h->n_iblocks;
+    t.lpl_log = h->b3_lpl_log;
     t.nosplit = h->b3_nosplit;
     t.nouni = h->b3_nouni;
     return t;
@@ -518,6 +570,7 @@ ScanOrder &scan_order(int device) {
 
 int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
     CHECK_HIP(hipSetDevice(h->device));
+    h->fc.valid = false;
     KParams kp = h->kp;
     kp.scan_tiles = h->dense_heavy ? 1u : 0u;
     Tables t = make_tables(h);
@@ -694,6 +747,7 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
     if (const char *nt = getenv("SYNCR_B3_NT")) h->b3_nt = (uint32_t)atoi(nt) != 0;
     if (const char *sp = getenv("SYNCR_B3_SPLIT")) h->b3_nosplit = atoi(sp) == 0;          // A/B only
     if (const char *un = getenv("SYNCR_B3_UNI")) h->b3_nouni = atoi(un) == 0;              // A/B only
+    if (const char *lp = getenv("SYNCR_B3_LPL")) h->b3_lpl = atoi(lp) == 1 ? 1u : (atoi(lp) == 4 ? 4u : 0u);  // A/B only
     if (const char *ld = getenv("SYNCR_B3_LOAD"))                                         // A/B only
         h->b3_coop = strcmp(ld, "plain") == 0  ? 0u
                      : strcmp(ld, "coop") == 0 ? 1u
@@ -774,6 +828,7 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
         if (h->last_stream) CHECK_HIP(hipStreamSynchronize(h->last_stream));
         h->planned = false;
         h->launched = false;
+        h->fc.valid = false;
         // validate: inside span, non-empty files must not overlap
         std::vector<uint32_t> ne;
         ne.reserve(nfiles);
@@ -900,6 +955,23 @@ int32_t syncr_cdc_launch_hashed(syncr_cdc *h, const uint8_t *d_bytes, void *stre
 }
 
 namespace {
+// the launch's cut slots (and, after a hashed launch, its hash counters and
+// hashes) into the fetch cache by `dn`; with small_only, only when the group
+// stays within one copy dispatch
+bool add_results(syncr_cdc *h, CopyGroup &dn, bool small_only) {
+    auto &fc = h->fc;
+    const uint64_t bytes = h->total_cut_cap * (sizeof(DevCut) + (h->hash_on ? 32u : 0u)) + sizeof fc.hc;
+    if (small_only && (dn.total + bytes > KCOPY_MAX || dn.items.size() + 3 > (size_t)COPY_MAX)) return false;
+    fc.all.resize(h->total_cut_cap);
+    dn.add(h->cuts.p, fc.all.data(), h->total_cut_cap * sizeof(DevCut));
+    if (h->hash_on) {
+        fc.hs.resize(h->total_cut_cap * 32);
+        dn.add(h->hctr.p, fc.hc, sizeof fc.hc);
+        dn.add(h->hashes.p, fc.hs.data(), fc.hs.size());
+    }
+    return true;
+}
+
 // fetch / fetch_hashed: exactly one of out / hout is used (the other may be null)
 int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool hashed, uint64_t cap,
                    uint64_t *per_file_count, uint64_t *n_out) {
@@ -910,17 +982,22 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
         CHECK_HIP(hipSetDevice(h->device));
         for (int attempt = 0; attempt < 8; attempt++) {
             if (h->last_stream) CHECK_HIP(hipStreamSynchronize(h->last_stream));
-            // the launch's counters, per-file counts and split counters in one copy group
-            uint32_t ctr[4];
-            std::vector<uint64_t> counts(h->nfiles);
-            uint32_t sp[SPL_WORDS];
-            {
+            auto &fc = h->fc;
+            if (!fc.valid) {
+                // the launch's counters, per-file counts and split counters in one
+                // copy group (with a small launch's results)
+                fc.counts.assign(h->nfiles, 0);
                 CopyGroup dn;
-                dn.add(zblock(h, h->zlast), ctr, 16);
-                dn.add(h->counts.p, counts.data(), h->nfiles * 8ull);
-                dn.add(zblock(h, h->zlast) + split_ctr_offset(h), sp, sizeof sp);
+                dn.add(zblock(h, h->zlast), fc.ctr, 16);
+                dn.add(h->counts.p, fc.counts.data(), h->nfiles * 8ull);
+                dn.add(zblock(h, h->zlast) + split_ctr_offset(h), fc.sp, sizeof fc.sp);
+                fc.cuts = add_results(h, dn, true);
                 CHECK_HIP(download(h, dn));
+                fc.valid = true;
             }
+            const uint32_t *ctr = fc.ctr;
+            const std::vector<uint64_t> &counts = fc.counts;
+            const uint32_t *sp = fc.sp;
             const uint64_t ncand = (uint64_t)ctr[CTR_CANDS_LO] | ((uint64_t)ctr[CTR_CANDS_HI] << 32);
             // for the next launch (also a re-run below): >= 64 Ki candidates at >= 1
             // per 16 KiB (random data: ~1 per MiB at chunk_bits 20)
@@ -1013,17 +1090,15 @@ int32_t fetch_impl(syncr_cdc *h, syncr_cut *out, syncr_chunk_info *hout, bool ha
             if (total > cap || (total && !(hashed ? (void *)hout : (void *)out))) return SYNCR_CDC_ERANGE;
             if (total) {
                 // the cut slots (and hash counters and hashes) in one copy group
-                std::vector<DevCut> all(h->total_cut_cap);
-                std::vector<uint8_t> hs;
-                uint64_t hc[B3C_WORDS];
-                CopyGroup dn;
-                dn.add(h->cuts.p, all.data(), h->total_cut_cap * sizeof(DevCut));
-                if (hashed) {
-                    hs.resize(h->total_cut_cap * 32);
-                    dn.add(h->hctr.p, hc, sizeof hc);
-                    dn.add(h->hashes.p, hs.data(), hs.size());
+                if (!fc.cuts) {
+                    CopyGroup dn;
+                    add_results(h, dn, false);
+                    CHECK_HIP(download(h, dn));
+                    fc.cuts = true;
                 }
-                CHECK_HIP(download(h, dn));
+                const std::vector<DevCut> &all = fc.all;
+                const std::vector<uint8_t> &hs = fc.hs;
+                const uint64_t *hc = fc.hc;
                 if (hashed && (hc[B3C_FLAGS] || hc[B3C_ITEMS] > h->items_cap || hc[B3C_TREES] > h->trees_cap ||
                                hc[B3C_PIECES] > h->pieces_cap))
                     return SYNCR_CDC_EIO;              // capacities are exact bounds: cannot happen

@@ -296,7 +296,13 @@ enum { DBG_RES_START = 0, DBG_RES_END = 1, DBG_W_ENTRY = 2, DBG_W_SETUP = 3, DBG
        DBG_WORDS = DBG_DT + 4 * DBG_DT_W * DBG_DT_N };
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------
-// A lane TASK is B3_LANE_LEAVES consecutive 1 KiB leaves of one chunk.  A chunk
+// A lane TASK is LPL consecutive 1 KiB leaves of one chunk: LPL = B3_LANE_LEAVES
+// on a big launch, 1 on a launch of at most B3_SMALL_SPAN bytes (a lane's leaves
+// are compressed in sequence, 16 blocks each: a 4-leaf task is ~80 us of one
+// wave, so on a small batch -- one file of the per-file call site, an 8 KiB
+// file included -- the leaf kernel's time is that one task; 1-leaf tasks cut it
+// ~4x, and give a small batch 4x the group items to spread over the waves; a
+// big launch keeps 4 leaves per lane: a quarter of the cross-lane merges).  A chunk
 // of T <= 64 tasks is PACKED: class c = ceil(log2 T), 64 >> c such units per
 // wave, each in an aligned run of 2^c lanes.  A chunk of T > 64 tasks (a BIG
 // chunk) is floor(T / 64) GROUP items of 64 tasks (one wave each) plus, when
@@ -306,8 +312,8 @@ enum { DBG_RES_START = 0, DBG_RES_END = 1, DBG_W_ENTRY = 2, DBG_W_SETUP = 3, DBG
 // PIECES by the binary digits of r, largest first -- exactly the subtrees of
 // BLAKE3's left-balanced tree -- so each piece fills its 2^c lanes; the tree
 // kernel folds the piece CVs right to left.
-constexpr uint32_t B3_LANE_LEAVES = 4;                      // 1 KiB leaves per lane task
-constexpr uint32_t B3_GROUP_LEAVES = 64 * B3_LANE_LEAVES;   // leaves per group item (one wave)
+constexpr uint32_t B3_LANE_LEAVES = 4;                      // 1 KiB leaves per lane task (big launches)
+constexpr uint64_t B3_SMALL_SPAN = 1ull << 30;              // launches up to this many bytes: 1 leaf per task
 constexpr int B3_CLASSES = 7;                               // packed classes: <= 1, 2, 4, ..., 64 tasks
 constexpr uint64_t B3_TAIL = 1ull << 63;                  // packed entry: tail unit
 constexpr uint64_t B3_PIECE = 1ull << 62;                 // packed entry: piece (index into pieces[])
@@ -333,6 +339,7 @@ struct HashTables {
     ulonglong2 *pieces;            // [pieces_cap] {slot, first task}: a piece's chunk and position
     uint32_t *pcv;                 // [pieces_cap * 8] CV of each piece
     uint64_t pieces_cap;
+    uint32_t lpl_log;              // log2 of the leaves per lane task: 2 (B3_LANE_LEAVES) or 0 (small launch)
     uint32_t nosplit;              // dev A/B only (SYNCR_B3_SPLIT=0): one unit per power-of-two class, no pieces
     uint32_t nouni;                // dev A/B only (SYNCR_B3_UNI=0): group items use the per-task loader
     uint32_t *gcv;                 // [items_cap * 8] subtree CV of each item (or tail placeholder)
@@ -363,6 +370,22 @@ hipError_t launch_post(const uint8_t *d_bytes, const KParams &p, const Tables &t
                        uint32_t scan_grid);
 hipError_t launch_resolve(const uint8_t *d_bytes, const KParams &p, const Tables &t, hipStream_t s);
 bool resolve_splits(const KParams &p, const Tables &t);   // launch_resolve starts split workers
+// A small copy group (cdc_api.cpp upload / download) as one dispatch: each
+// segment's bytes (a multiple of 4) from src to dst, either side device memory
+// or the handle's pinned, device-visible staging.  A hipMemcpyAsync per table is
+// one blit dispatch each (~2 us of GPU and ~5 us of API time): a one-file batch
+// moved ~20 tables that way per round trip.
+constexpr int COPY_MAX = 12;
+struct CopySeg {
+    const void *src;
+    void *dst;
+    uint64_t bytes;
+};
+struct CopyList {
+    CopySeg seg[COPY_MAX];
+    uint32_t n;
+};
+hipError_t launch_copy(const CopyList &l, uint64_t total_bytes, hipStream_t s);
 hipError_t launch_gen(uint8_t *d_base, const uint64_t *d_foff, const uint64_t *d_flen,
                       const uint64_t *d_findex, const uint64_t *d_seg_prefix, uint32_t nfiles,
                       uint64_t nseg, uint64_t first_index, const uint64_t *d_jump, hipStream_t s);

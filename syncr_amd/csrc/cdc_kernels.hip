@@ -3531,6 +3531,34 @@ __global__ __launch_bounds__(256) void cdc_gen_kernel(uint8_t *__restrict__ base
 }
 
 // ---------------------------------------------------------------------------
+// A small copy group in one dispatch (cdc_internal.h CopyList): the grid strides
+// over each segment in turn, 16-byte words where both sides are 16-aligned.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cdc_copy_kernel(CopyList L) {
+    const uint64_t tid = (uint64_t)blockIdx.x * 256u + threadIdx.x, nthr = (uint64_t)gridDim.x * 256u;
+    for (uint32_t k = 0; k < L.n; ++k) {
+        const uint32_t *src = (const uint32_t *)L.seg[k].src;
+        uint32_t *dst = (uint32_t *)L.seg[k].dst;
+        const uint64_t nw = L.seg[k].bytes >> 2;
+        uint64_t head = 0;                                    // words done as 16-byte vectors
+        if ((((uintptr_t)src | (uintptr_t)dst) & 15u) == 0) {
+            const uint64_t nv = nw >> 2;
+            for (uint64_t i = tid; i < nv; i += nthr) ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
+            head = 4 * nv;
+        }
+        for (uint64_t i = head + tid; i < nw; i += nthr) dst[i] = src[i];
+    }
+}
+
+hipError_t launch_copy(const CopyList &l, uint64_t total_bytes, hipStream_t s) {
+    if (!l.n) return hipSuccess;
+    const uint64_t want = (total_bytes / 16 + 255) / 256;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 1), 64);
+    hipLaunchKernelGGL(cdc_copy_kernel, dim3(blocks), dim3(256), 0, s, l);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Streaming-read probe (roofline denominator): the best rate this
 // part reaches reading bytes once, with nothing else to do.  Each lane keeps
 // UNR 16-byte loads in flight per iteration (grid-stride over 64 KiB blocks so
