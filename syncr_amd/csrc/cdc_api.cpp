@@ -194,6 +194,8 @@ struct syncr_cdc {
     const uint8_t *last_bytes = nullptr;
     hipStream_t last_stream = nullptr;  // stream of the last launch (nullptr: none since open)
     hipEvent_t xstream_ev = nullptr;    // orders a launch after the previous one on another stream
+    hipEvent_t up_ev = nullptr;         // the plan's table upload on `stream` (not waited for by plan)
+    bool up_pending = false;            // hstage may still be read by that upload
     uint64_t stats[4] = {0, 0, 0, 0};
     uint64_t scan_info[4] = {SYNCR_CDC_SCAN_NONE, 0, 0, 0};   // syncr_cdc_last_scan
     uint64_t reruns = 0;                // capacity re-runs of the last fetch
@@ -277,9 +279,20 @@ bool one_dispatch(const CopyGroup &g) {
     return true;
 }
 
-hipError_t upload(syncr_cdc *h, const CopyGroup &g) {
+// the staging buffer is free: a plan's upload left in flight has completed
+hipError_t stage_free(syncr_cdc *h) {
+    if (!h->up_pending) return hipSuccess;
+    const hipError_t e = hipEventSynchronize(h->up_ev);
+    if (e == hipSuccess) h->up_pending = false;
+    return e;
+}
+
+// wait = false (plan): the copy is left in flight on the handle's stream, and
+// do_launch orders a launch on another stream after it (up_ev)
+hipError_t upload(syncr_cdc *h, const CopyGroup &g, bool wait = true) {
     if (g.items.empty()) return hipSuccess;
-    hipError_t e = hipSuccess;
+    hipError_t e = stage_free(h);
+    if (e != hipSuccess) return e;
     if (g.total > STAGE_MAX || (e = h->hstage.ensure(g.total)) != hipSuccess) {
         for (const auto &it : g.items)
             if ((e = hipMemcpy(it.dev, it.host, it.n, hipMemcpyHostToDevice)) != hipSuccess) return e;
@@ -296,14 +309,19 @@ hipError_t upload(syncr_cdc *h, const CopyGroup &g) {
                 hipSuccess)
                 return e;
     }
-    return hipStreamSynchronize(h->stream);
+    if (wait) return hipStreamSynchronize(h->stream);
+    if (!h->up_ev && (e = hipEventCreateWithFlags(&h->up_ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventRecord(h->up_ev, h->stream)) != hipSuccess) return e;
+    h->up_pending = true;
+    return hipSuccess;
 }
 
 // device -> host, complete on return (the caller has waited for the kernels
 // that wrote the device side)
 hipError_t download(syncr_cdc *h, const CopyGroup &g) {
     if (g.items.empty()) return hipSuccess;
-    hipError_t e = hipSuccess;
+    hipError_t e = stage_free(h);
+    if (e != hipSuccess) return e;
     if (g.total > STAGE_MAX || (e = h->hstage.ensure(g.total)) != hipSuccess) {
         for (const auto &it : g.items)
             if ((e = hipMemcpy(it.host, it.dev, it.n, hipMemcpyDeviceToHost)) != hipSuccess) return e;
@@ -594,6 +612,8 @@ int32_t do_launch(syncr_cdc *h, const uint8_t *d_bytes, hipStream_t s) {
         CHECK_HIP(hipEventRecord(h->xstream_ev, h->last_stream));
         CHECK_HIP(hipStreamWaitEvent(s, h->xstream_ev, 0));
     }
+    // the plan's tables (uploaded on the handle's stream, not waited for)
+    if (h->up_pending && s != h->stream) CHECK_HIP(hipStreamWaitEvent(s, h->up_ev, 0));
     const uint32_t par = h->zpar;
     if (!h->zclean[par]) CHECK_HIP(hipMemsetAsync(zblock(h, par), 0, zeroed_bytes(h), s));
     h->zclean[par] = false;
@@ -808,6 +828,7 @@ void syncr_cdc_close(syncr_cdc *h) {
         (void)hipEventDestroy(h->scan_done);
     }
     if (h->xstream_ev) (void)hipEventDestroy(h->xstream_ev);
+    if (h->up_ev) (void)hipEventDestroy(h->up_ev);
     (void)hipStreamDestroy(h->stream);
     delete h;                   // every DevBuf member frees its memory (on this device, set above)
 }
@@ -922,7 +943,7 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
             up.add(h->gpos.p, gpos.data(), acc * 8);
             up.add(h->gend.p, gend.data(), acc * 8);
         }
-        CHECK_HIP(upload(h, up));
+        CHECK_HIP(upload(h, up, false));
         h->planned = true;
         return SYNCR_CDC_OK;
     } catch (const std::bad_alloc &) {
