@@ -117,7 +117,10 @@ int32_t syncr_cdc_chunk_batch_host_hashed(syncr_cdc *h, const uint8_t *data, uin
 /* --- device-resident entry points (what the throughput metric times) ------- */
 /* plan: validate + upload the file table (host arrays) for bytes that will be
  * resident in device memory at [d_bytes, d_bytes+span).  Files must not overlap.
- * Synchronous; reusable for any number of launches. */
+ * The host arrays may be reused as soon as plan returns; the device copy of the
+ * tables may still be in flight on the handle's own stream, and any launch
+ * (on whatever stream) is ordered after it.  Reusable for any number of
+ * launches. */
 int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *file_len,
                        uint32_t nfiles, uint64_t span);
 /* launch: scan + resolve on `stream`, asynchronous: no host synchronisation and
@@ -138,7 +141,9 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
 int32_t syncr_cdc_launch(syncr_cdc *h, const uint8_t *d_bytes, void *stream);
 /* fetch: wait for the last launch, copy cuts to the host (file by file).  May
  * re-run the launch on its stream first (grown capacities), reading d_bytes
- * again. */
+ * again.  The launch's results stay on the host until the next plan or launch:
+ * fetching again (e.g. cap 0 for the total, then into a buffer of that size)
+ * does not wait for the device again. */
 int32_t syncr_cdc_fetch(syncr_cdc *h, syncr_cut *out, uint64_t cap,
                         uint64_t *per_file_count, uint64_t *n_out);
 /* launch_hashed: launch, then BLAKE3 of every chunk on the same stream

@@ -682,6 +682,37 @@ def test_launches_on_alternating_streams():
             d.free()
 
 
+def test_plans_on_caller_stream_reuse_staging():
+    """plan leaves its table upload in flight on the handle's stream; a launch on
+    a caller stream waits for it, and the next plan reuses the pinned staging
+    only once that upload completed.  Twenty plans of different file tables
+    (one plan replaced before any launch), each launched on a caller stream and
+    fetched with hashes, against the oracle."""
+    rng = np.random.default_rng(77)
+    files = [O.xorshift_bytes(900 + k, int(n)) for k, n in enumerate(rng.integers(0, 3 * M, 24))]
+    with syncr_amd.Chunker() as ch, syncr_amd.Chunker() as other:
+        for r in range(20):
+            pick = [files[(r + 3 * j) % len(files)] for j in range(1 + r % 5)]
+            lens = np.array([f.size for f in pick], np.uint64)
+            offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+            host = np.concatenate(pick) if lens.sum() else np.zeros(1, np.uint8)
+            d = syncr_amd.DeviceBuffer(ch, max(host.size, 1))
+            try:
+                d.upload(host)
+                if r == 7:                                   # a plan replaced before its launch
+                    ch.plan(offs[:1], lens[:1], int(lens.sum()))
+                ch.plan(offs, lens, int(lens.sum()))
+                ch.launch(d.ptr, stream=other.stream, hashed=True)
+                got = ch.fetch(hashed=True)
+            finally:
+                d.free()
+            for g, f in zip(got, pick):
+                assert ends_of(g) == O.chunk_production_window(f).tolist()
+                if g.size:
+                    h = O.blake3_batch(f, g["offset"].astype(np.uint64), g["len"].astype(np.uint64), nthreads=8)
+                    assert np.array_equal(g["hash"], h)
+
+
 def test_small_batches_back_to_back_stable():
     """Small batches run the CU scan schedule (a workgroup per CU, a ring of
     group ids in LDS).  LDS survives between workgroups: a ring slot left by an
