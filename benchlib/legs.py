@@ -62,6 +62,31 @@ def time_steps(ch, ptr: int, span: int, steps: int, warmup: int, hashed: bool = 
     return out
 
 
+def time_pipelined(slots, span: int, steps: int, warmup: int) -> dict:
+    """The same K steps with two batches in flight: step k on slot k % 2, each
+    slot its own handle, stream and copy of the batch (how the ingest pipeline
+    runs its slots; the scans of two handles are not ordered, so the next
+    batch's scan takes the CUs the last one's final stream tiles free)."""
+    for k in range(max(warmup, 2)):
+        h, b = slots[k % 2]
+        h.launch(b.ptr)
+    for h, _ in slots:
+        h.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        h, b = slots[k % 2]
+        h.launch(b.ptr)
+    for h, _ in slots:
+        h.synchronize()
+    dt = (time.perf_counter() - t0) / max(steps, 1)
+    return {"ms_per_step": round(dt * 1e3, 4),
+            "step_frac": round(span / dt / 1e9 / HBM_PEAK_GBS, 4), "value": round(span / dt / 2**30, 3)}
+
+
+PIPE_NOTE = ("two batches in flight: step k on slot k % 2, each slot its own handle, HIP stream and copy of the "
+             "batch (the ingest pipeline's slots); not the one-in-flight step above")
+
+
 # --------------------------------------------------------------------------
 # parity legs against fixtures / the oracle (small inputs)
 # --------------------------------------------------------------------------
@@ -187,16 +212,25 @@ def uniform1k_leg(device: int, steps: int, warmup: int) -> dict:
     lens = np.full(int(g["files"]), int(g["file_len"]), np.uint64)
     offs = WL.offsets_of(lens)
     span = int(lens.sum())
-    with syncr_amd.Chunker(device=device) as ch:
+    with syncr_amd.Chunker(device=device) as ch, syncr_amd.Chunker(device=device) as ch2:
         b = syncr_amd.DeviceBuffer(ch, span)
+        b2 = syncr_amd.DeviceBuffer(ch2, span)
         try:
             b.gen_corpus(offs, lens)
+            b2.gen_corpus(offs, lens)
             ch.plan(offs, lens, span)
+            ch2.plan(offs, lens, span)
             out = time_steps(ch, b.ptr, span, steps, warmup)
             cuts = ch.fetch()
+            ch2.launch(b2.ptr)
+            ch2.fetch()
+            out["pipelined"] = dict(time_pipelined([(ch, b), (ch2, b2)], span, steps, warmup), note=PIPE_NOTE)
+            cuts2 = ch2.fetch()
         finally:
             b.free()
+            b2.free()
     bad = sum(G.ends_of(c).tolist() != e for c, e in zip(cuts, g["ends"]))
+    bad += sum(G.ends_of(c).tolist() != e for c, e in zip(cuts2, g["ends"]))
     out.update({"config": "SURVEY §8d config 2: 1024 x 1 MiB random files, 1 GiB, production semantics",
                 "parity": {"files": len(cuts), "chunks": int(sum(c.size for c in cuts)), "mismatches": int(bad),
                            "fixture": "tests/golden/corpus_uniform_1024x1MiB.json (every cut)"}})
@@ -217,8 +251,9 @@ def shard_leg(device: int, steps: int, warmup: int, nshards: int = 8) -> dict:
     shards = WL.lpt_shard(sizes, nshards)
     biggest = max(int(sizes[s].sum()) for s in shards)
     per, mism, nfiles = [], 0, 0
-    with syncr_amd.Chunker(device=device) as ch:
+    with syncr_amd.Chunker(device=device) as ch, syncr_amd.Chunker(device=device) as ch2:
         b = syncr_amd.DeviceBuffer(ch, biggest)
+        b2 = syncr_amd.DeviceBuffer(ch2, biggest)
         try:
             for r, sh in enumerate(shards):
                 lens = sizes[sh]
@@ -228,15 +263,24 @@ def shard_leg(device: int, steps: int, warmup: int, nshards: int = 8) -> dict:
                 ch.plan(offs, lens, span)
                 t = time_steps(ch, b.ptr, span, steps, warmup)
                 p = G.check_files("zipf10k", ch.fetch(), sh)
-                mism += p["mismatches"]
+                # the same shard with two batches in flight
+                b2.gen_corpus(offs, lens, indices=sh.astype(np.uint64))
+                ch2.plan(offs, lens, span)
+                ch2.launch(b2.ptr)
+                ch2.fetch()
+                tp = time_pipelined([(ch, b), (ch2, b2)], span, steps, warmup)
+                p2 = G.check_files("zipf10k", ch2.fetch(), sh)
+                mism += p["mismatches"] + p2["mismatches"]
                 nfiles += p["files"]
                 per.append({"shard": r, "files": int(sh.size), "bytes": span, "ms_per_step": t["ms_per_step"],
                             "scan_ms": t["scan_ms"], "scan_frac": t["scan_frac"],
                             "step_frac": round(span / (t["ms_per_step"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                             "dense_ms": t["dense_ms"], "resolve_ms": t["resolve_ms"],
-                            "scan_schedule": t["scan_schedule"], "parity_mismatches": p["mismatches"]})
+                            "scan_schedule": t["scan_schedule"], "parity_mismatches": p["mismatches"],
+                            "pipelined_ms_per_step": tp["ms_per_step"], "pipelined_step_frac": tp["step_frac"]})
         finally:
             b.free()
+            b2.free()
     total = int(sizes.sum())
     worst = max(x["ms_per_step"] for x in per)
     return {"nshards": nshards, "shards": per, "total_bytes": total,
@@ -246,6 +290,11 @@ def shard_leg(device: int, steps: int, warmup: int, nshards: int = 8) -> dict:
                                "corpus bytes / the slowest shard's step, each shard timed alone on this GPU; no "
                                "multi-GPU scaling was measured"),
             "mean_step_frac": round(sum(x["step_frac"] for x in per) / len(per), 4),
+            "pipelined": {"mean_step_frac": round(sum(x["pipelined_step_frac"] for x in per) / len(per), 4),
+                          "max_ms_per_step": max(x["pipelined_ms_per_step"] for x in per),
+                          "projected_value": round(total / (max(x["pipelined_ms_per_step"] for x in per) / 1e3)
+                                                   / 2**30, 3),
+                          "note": PIPE_NOTE},
             "mean_scan_frac": round(sum(x["scan_frac"] for x in per) / len(per), 4),
             "load_balance_max_over_mean_ms": round(worst / (sum(x["ms_per_step"] for x in per) / len(per)), 4),
             "parity": {"files": nfiles, "mismatches": mism, "fixture": "tests/golden/zipf10k_digests.npz",

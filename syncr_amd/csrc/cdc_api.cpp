@@ -122,7 +122,7 @@ struct syncr_cdc {
     KParams kp{};
     hipStream_t stream = nullptr;
     hipEvent_t scan_done = nullptr;     // recorded after each launch's scan (scan_order)
-    bool serial_scans = true;           // order scans of same-device handles (dev lib: SYNCR_CDC_SERIAL=0)
+    bool serial_scans = false;          // order scans of same-device handles (dev lib: SYNCR_CDC_SERIAL=1)
     // scan kernel and tile geometry: the packed-u16 VALU roll (north_star: integer
     // work, no MFMA).  Other geometries and the MFMA Toeplitz variant exist only
     // in the development library.
@@ -568,11 +568,17 @@ void drain_timing(syncr_cdc *h) {
 // flight on two streams cannot co-reside: they contend for the same slots and
 // HBM, and the later one's waves start piecemeal as the earlier one's retire.
 // With several handles on one device (the ingest pipeline's slots, bench.py's
-// pipelined segment) each launch's scan therefore waits for the scan most
-// recently enqueued on that device by ANOTHER handle; only the short
+// pipelined segment) each launch's scan could wait for the scan most recently
+// enqueued on that device by ANOTHER handle, so that only the short
 // compaction / fix-up / resolve / hash tail of one batch overlaps the next
-// batch's scan.  (Round-1 driver run: two unordered scans in flight made the
-// step 13 % slower than one, BENCH_r01.json `pipelined`.)
+// batch's scan (round 1: two unordered scans in flight made the step 13 %
+// slower than one, BENCH_r01.json `pipelined`).  The product no longer orders
+// them (round 6): the persistent scan grids hand the CUs over as the first
+// scan's last stream tiles end, so the next batch's scan fills the first one's
+// tail.  Two batches in flight, same process (tools/pipe_ab.py,
+// profiles/r06v_pipe_ab/): config 4's shards 0.686 -> 0.734 of 8 TB/s per step,
+// uniform1k 0.661 -> 0.716, zipf10k 0.823 -> 0.827, dense 0.652 -> 0.656; the
+// development library restores the order with SYNCR_CDC_SERIAL=1.
 struct ScanOrder {
     std::mutex mu;
     const syncr_cdc *owner = nullptr;   // handle whose scan was enqueued last
