@@ -74,7 +74,7 @@ struct HostStage {
         if (n <= cap && p) return hipSuccess;
         const size_t want = std::max<size_t>(n, std::max<size_t>(64u << 10, 2 * cap));
         uint8_t *q = nullptr, *qd = nullptr;
-        hipError_t e = hipHostMalloc((void **)&q, want, hipHostMallocCoherent);
+        hipError_t e = hipHostMalloc((void **)&q, want, hipHostMallocCoherent | hipHostMallocPortable);
         if (e != hipSuccess) return e;
         if ((e = hipHostGetDevicePointer((void **)&qd, q, 0)) != hipSuccess) {
             (void)hipHostFree(q);
