@@ -50,7 +50,11 @@ def main():
     ap.add_argument("--shards", default="0,3,6")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--b-ablate", default="", help="dev library: SYNCR_CDC_ABLATE for B's handle (8: the "
+                    "one-wave dynamic-group tile scan instead of the CU schedule)")
     a = ap.parse_args()
+    if a.b_ablate:
+        syncr_amd.use_dev_library()
     sizes = WL.zipf_sizes()
     shards = WL.lpt_shard(sizes, 8)
     fracs = [float(x) for x in a.fracs.split(",")]
@@ -60,11 +64,16 @@ def main():
         total = int(sizes[sh].sum())
         made = {}
 
-        def batch(idx):
+        def batch(idx, ablate=""):
             lens = sizes[idx]
             offs = WL.offsets_of(lens)
             span = int(lens.sum())
-            h = syncr_amd.Chunker()
+            if ablate:
+                os.environ["SYNCR_CDC_ABLATE"] = ablate
+            try:
+                h = syncr_amd.Chunker()
+            finally:
+                os.environ.pop("SYNCR_CDC_ABLATE", None)
             b = syncr_amd.DeviceBuffer(h, max(span, 16))
             b.gen_corpus(offs, lens, indices=idx.astype(np.uint64))
             h.plan(offs, lens, span)
@@ -76,7 +85,7 @@ def main():
         for f in fracs:
             cum = np.cumsum(sizes[order])
             k = int(np.searchsorted(cum, f * total))
-            made[f"split{f}"] = [batch(order[k:]), batch(order[:k])]
+            made[f"split{f}"] = [batch(order[k:]), batch(order[:k], a.b_ablate)]
         ms = {m: [] for m in made}
         for _ in range(a.rounds):
             for m, grp in made.items():
