@@ -446,8 +446,11 @@ int32_t upload_cut_tables(syncr_cdc *h, CopyGroup *into = nullptr) {
     // (cdc_internal.h).  A chunk of len bytes is ceil(leaves / (64 LPL)) group
     // items (the last may be a tail placeholder), so a file needs at most
     // ceil(F / group bytes) + (its cuts) of them
+    // (a chunk is at most max_chunk: with 1-leaf tasks one of 64 MiB is 1024 group
+    // items for b3_tree_kernel's single wave to merge, 4x its 4-leaf count)
     const bool variant = h->b3_coop != 3 || h->b3_ablate || h->b3_nt;    // dev loaders: 4-leaf instances only
-    h->b3_lpl_log = (h->b3_lpl ? h->b3_lpl == 1 : h->span <= B3_SMALL_SPAN) && !variant ? 0u : 2u;
+    const bool small = h->span <= B3_SMALL_SPAN && h->kp.max_chunk <= (64ull << 20);
+    h->b3_lpl_log = (h->b3_lpl ? h->b3_lpl == 1 : small) && !variant ? 0u : 2u;
     const uint64_t gbytes = (1024ull * 64ull) << h->b3_lpl_log;
     uint64_t icap = 0;
     for (uint32_t i = 0; i < h->nfiles; i++) icap += (h->h_flen[i] + gbytes - 1) / gbytes + h->h_cut_cap[i];

@@ -297,7 +297,8 @@ enum { DBG_RES_START = 0, DBG_RES_END = 1, DBG_W_ENTRY = 2, DBG_W_SETUP = 3, DBG
 
 // ---- BLAKE3 of every chunk (b3_kernels.hip) -------------------------------
 // A lane TASK is LPL consecutive 1 KiB leaves of one chunk: LPL = B3_LANE_LEAVES
-// on a big launch, 1 on a launch of at most B3_SMALL_SPAN bytes (a lane's leaves
+// on a big launch, 1 on a launch of at most B3_SMALL_SPAN bytes whose max_chunk
+// is at most 64 MiB (a lane's leaves
 // are compressed in sequence, 16 blocks each: a 4-leaf task is ~80 us of one
 // wave, so on a small batch -- one file of the per-file call site, an 8 KiB
 // file included -- the leaf kernel's time is that one task; 1-leaf tasks cut it
