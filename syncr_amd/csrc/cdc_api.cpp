@@ -91,7 +91,8 @@ constexpr size_t STAGE_MAX = 4u << 20;
 constexpr size_t KCOPY_MAX = 256u << 10;
 
 // copies of one group: (device, host, bytes); host buffers stay valid until
-// upload() / download() returns
+// upload() / download() returns.  An upload item without a host side zero-fills
+// its device range (no staging).
 struct CopyGroup {
     struct Item {
         void *dev;
@@ -104,6 +105,9 @@ struct CopyGroup {
         if (!n) return;
         items.push_back({dev, const_cast<void *>(host), n, total});
         total += (n + 15) & ~size_t(15);
+    }
+    void zero(void *dev, size_t n) {
+        if (n) items.push_back({dev, nullptr, n, 0});
     }
 };
 
@@ -274,9 +278,12 @@ KParams make_kparams(const syncr_cdc_params &p) {
 // the group as one copy dispatch: small, few tables, whole 4-byte words
 bool one_dispatch(const CopyGroup &g) {
     if (g.total > KCOPY_MAX || g.items.size() > (size_t)COPY_MAX) return false;
-    for (const auto &it : g.items)
+    size_t zeros = 0;
+    for (const auto &it : g.items) {
         if (it.n & 3u) return false;
-    return true;
+        if (!it.host) zeros += it.n;
+    }
+    return zeros <= KCOPY_MAX;
 }
 
 // the staging buffer is free: a plan's upload left in flight has completed
@@ -293,21 +300,29 @@ hipError_t upload(syncr_cdc *h, const CopyGroup &g, bool wait = true) {
     if (g.items.empty()) return hipSuccess;
     hipError_t e = stage_free(h);
     if (e != hipSuccess) return e;
-    if (g.total > STAGE_MAX || (e = h->hstage.ensure(g.total)) != hipSuccess) {
-        for (const auto &it : g.items)
-            if ((e = hipMemcpy(it.dev, it.host, it.n, hipMemcpyHostToDevice)) != hipSuccess) return e;
+    if (g.total > STAGE_MAX || (e = h->hstage.ensure(std::max<size_t>(g.total, 16))) != hipSuccess) {
+        for (const auto &it : g.items) {
+            e = it.host ? hipMemcpy(it.dev, it.host, it.n, hipMemcpyHostToDevice) : hipMemset(it.dev, 0, it.n);
+            if (e != hipSuccess) return e;
+        }
         return hipSuccess;
     }
-    for (const auto &it : g.items) memcpy(h->hstage.p + it.off, it.host, it.n);
+    for (const auto &it : g.items)
+        if (it.host) memcpy(h->hstage.p + it.off, it.host, it.n);
     if (one_dispatch(g)) {
         CopyList l{};
-        for (const auto &it : g.items) l.seg[l.n++] = CopySeg{h->hstage.d + it.off, it.dev, it.n};
-        if ((e = launch_copy(l, g.total, h->stream)) != hipSuccess) return e;
+        uint64_t bytes = 0;
+        for (const auto &it : g.items) {
+            l.seg[l.n++] = CopySeg{it.host ? h->hstage.d + it.off : nullptr, it.dev, it.n};
+            bytes += it.n;
+        }
+        if ((e = launch_copy(l, bytes, h->stream)) != hipSuccess) return e;
     } else {
-        for (const auto &it : g.items)
-            if ((e = hipMemcpyAsync(it.dev, h->hstage.p + it.off, it.n, hipMemcpyHostToDevice, h->stream)) !=
-                hipSuccess)
-                return e;
+        for (const auto &it : g.items) {
+            e = it.host ? hipMemcpyAsync(it.dev, h->hstage.p + it.off, it.n, hipMemcpyHostToDevice, h->stream)
+                        : hipMemsetAsync(it.dev, 0, it.n, h->stream);
+            if (e != hipSuccess) return e;
+        }
     }
     if (wait) return hipStreamSynchronize(h->stream);
     if (!h->up_ev && (e = hipEventCreateWithFlags(&h->up_ev, hipEventDisableTiming)) != hipSuccess) return e;
@@ -952,7 +967,9 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
             up.add(h->gpos.p, gpos.data(), acc * 8);
             up.add(h->gend.p, gend.data(), acc * 8);
         }
+        up.zero(zblock(h, 0), zeroed_bytes(h));      // the first launch's counter block, in the same dispatch
         CHECK_HIP(upload(h, up, false));
+        h->zclean[0] = true;
         h->planned = true;
         return SYNCR_CDC_OK;
     } catch (const std::bad_alloc &) {

@@ -376,9 +376,9 @@ bool resolve_splits(const KParams &p, const Tables &t);   // launch_resolve star
 // or the handle's pinned, device-visible staging.  A hipMemcpyAsync per table is
 // one blit dispatch each (~2 us of GPU and ~5 us of API time): a one-file batch
 // moved ~20 tables that way per round trip.
-constexpr int COPY_MAX = 12;
+constexpr int COPY_MAX = 14;
 struct CopySeg {
-    const void *src;
+    const void *src;               // nullptr: zero-fill dst
     void *dst;
     uint64_t bytes;
 };

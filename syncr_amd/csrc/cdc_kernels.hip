@@ -3541,6 +3541,15 @@ __global__ __launch_bounds__(256) void cdc_copy_kernel(CopyList L) {
         uint32_t *dst = (uint32_t *)L.seg[k].dst;
         const uint64_t nw = L.seg[k].bytes >> 2;
         uint64_t head = 0;                                    // words done as 16-byte vectors
+        if (!src) {                                           // a zero fill
+            if (((uintptr_t)dst & 15u) == 0) {
+                const uint64_t nv = nw >> 2;
+                for (uint64_t i = tid; i < nv; i += nthr) ((uint4 *)dst)[i] = make_uint4(0u, 0u, 0u, 0u);
+                head = 4 * nv;
+            }
+            for (uint64_t i = head + tid; i < nw; i += nthr) dst[i] = 0u;
+            continue;
+        }
         if ((((uintptr_t)src | (uintptr_t)dst) & 15u) == 0) {
             const uint64_t nv = nw >> 2;
             for (uint64_t i = tid; i < nv; i += nthr) ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
