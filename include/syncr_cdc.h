@@ -85,10 +85,9 @@ int32_t syncr_cdc_device_count(int32_t *n);
 
 /* Replaces Bup::new_with_chunk_bits: one handle per device, parameters fixed.
  * The library reads no environment variables: its results depend only on the
- * parameters and the bytes.  Handles on one device order their scans: a
- * launch's scan kernel starts after the scan most recently enqueued on that
- * device by another handle (each scan fills the whole GPU), so several
- * handles = several batches in flight with only their short tails overlapping. */
+ * parameters and the bytes.  Handles on one device are independent: several
+ * handles = several batches in flight, the next batch's scan taking the GPU as
+ * the previous scan's last work units end. */
 int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **out);
 void syncr_cdc_close(syncr_cdc *h);
 int32_t syncr_cdc_get_params(const syncr_cdc *h, syncr_cdc_params *p);
