@@ -325,8 +325,12 @@ hipError_t upload(syncr_cdc *h, const CopyGroup &g, bool wait = true) {
         }
     }
     if (wait) return hipStreamSynchronize(h->stream);
-    if (!h->up_ev && (e = hipEventCreateWithFlags(&h->up_ev, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventRecord(h->up_ev, h->stream)) != hipSuccess) return e;
+    if (!h->up_ev) e = hipEventCreateWithFlags(&h->up_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(h->up_ev, h->stream);
+    if (e != hipSuccess) {              // no event to order by: complete the copy here instead
+        (void)hipStreamSynchronize(h->stream);
+        return e;
+    }
     h->up_pending = true;
     return hipSuccess;
 }
