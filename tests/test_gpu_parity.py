@@ -682,6 +682,47 @@ def test_launches_on_alternating_streams():
             d.free()
 
 
+def test_handles_in_flight_together():
+    """Scans of different handles on one device are not ordered (a second
+    handle's scan takes the CUs as the first one's last work units end).  Three
+    handles with different batches -- small random files (the CU schedule), a
+    periodic + constant + random batch (dense tiles, a re-run inside fetch) and
+    one larger random batch (stream tiles) -- launched on their own streams three
+    times over with no wait in between; every cut and chunk hash against the
+    oracle."""
+    from benchlib import legs as LG
+    small = [O.xorshift_bytes(60 + k, 300_000 + 77 * k) for k in range(12)]
+    dense = LG.dense_subset_files()[:4] + [O.xorshift_bytes(4323, 5 * M + 3)]
+    big = [O.xorshift_bytes(71 + k, 24 * M + 1000 * k) for k in range(3)]
+    batches = [small, dense, big]
+    hs, bufs = [], []
+    try:
+        for files in batches:
+            lens = np.array([f.size for f in files], np.uint64)
+            offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+            h = syncr_amd.Chunker()
+            b = syncr_amd.DeviceBuffer(h, int(lens.sum()))
+            b.upload(np.concatenate(files))
+            h.plan(offs, lens, int(lens.sum()))
+            hs.append(h)
+            bufs.append(b)
+        for rnd in range(3):
+            for h, b in zip(hs, bufs):
+                h.launch(b.ptr, hashed=True)
+        for h, files in zip(hs, batches):
+            got = h.fetch(hashed=True)
+            for g, f in zip(got, files):
+                assert ends_of(g) == O.chunk_production_window(f).tolist()
+                if g.size:
+                    want = O.blake3_batch(f, g["offset"].astype(np.uint64), g["len"].astype(np.uint64), nthreads=8)
+                    assert np.array_equal(g["hash"], want)
+    finally:
+        for b in bufs:
+            b.free()
+        for h in hs:
+            h.close()
+
+
 def test_plans_on_caller_stream_reuse_staging():
     """plan leaves its table upload in flight on the handle's stream; a launch on
     a caller stream waits for it, and the next plan reuses the pinned staging
