@@ -96,6 +96,35 @@ def test_many_small_files(chunkers, bits, mx, cap):
     _batch_vs_oracle(chunkers(bits, mx, cap), data, offs, lens, bits, mx, cap)
 
 
+def test_quarter_million_tiny_files_hashed():
+    """A plan whose tables exceed the pinned staging group limit (4 MiB: the
+    synchronous-copy path, its counter block zeroed by a memset): 250 000 files
+    of 0..40 bytes (a few hold a head hit), hashed; every file's cuts and every
+    chunk's BLAKE3 against the oracle."""
+    rng = np.random.default_rng(250)
+    lens = rng.integers(0, 41, 250_000).astype(np.uint64)
+    offs = np.zeros_like(lens)
+    offs[1:] = np.cumsum(lens)[:-1]
+    data = rng.integers(0, 256, max(int(lens.sum()), 1), dtype=np.uint8)
+    with syncr_amd.Chunker() as ch:
+        d = syncr_amd.DeviceBuffer(ch, data.size)
+        try:
+            d.upload(data)
+            ch.plan(offs, lens, int(lens.sum()))
+            ch.launch(d.ptr, hashed=True)
+            got = ch.fetch(hashed=True)
+        finally:
+            d.free()
+    want = O.chunk_batch(data, offs, lens)
+    assert len(got) == lens.size
+    bad = [i for i in range(lens.size) if ends_of(got[i]) != want[i].tolist()]
+    assert not bad, (len(bad), bad[:5])
+    co = np.concatenate([offs[i] + got[i]["offset"].astype(np.uint64) for i in range(lens.size)])
+    cl = np.concatenate([got[i]["len"].astype(np.uint64) for i in range(lens.size)])
+    hs = np.concatenate([got[i]["hash"] for i in range(lens.size)])
+    assert np.array_equal(hs, O.blake3_batch(data, co, cl, nthreads=8))
+
+
 def test_gaps_and_unsorted_table(chunkers):
     """Files with holes between them and a table not sorted by offset."""
     rng = np.random.default_rng(7)
