@@ -63,11 +63,18 @@ def test_official_vectors_one_chunk_per_file():
         assert cuts["hash"][0].tobytes().hex() == want, n
 
 
-def test_sizes_and_alignments():
+# max_chunk picks the lane task: 1 leaf for a small launch whose max_chunk is at
+# most 64 MiB, else 4 leaves (cdc_internal.h B3_SMALL_SPAN); bits 31 never cut
+LANE_TASKS = pytest.mark.parametrize("mx", [1 << 31, 64 * M], ids=["4-leaf-tasks", "1-leaf-tasks"])
+
+
+@LANE_TASKS
+def test_sizes_and_alignments(mx):
     """Chunk sizes around every boundary of the decomposition (block 64 B, leaf
-    1 KiB, lane 4 KiB, item 256 KiB, two-level tree) at all 16 start alignments."""
-    sizes = [1, 2, 63, 64, 65, 1023, 1024, 1025, 2047, 3073, 4095, 4096, 4097, 8193, 65535, 65536,
-             262143, 262144, 262145, 524289, 1048576 + 7, 3 * M + 5]
+    1 KiB, lane 4 KiB / 1 KiB, item 256 KiB / 64 KiB, two-level tree) at all 16
+    start alignments, with either lane task."""
+    sizes = [1, 2, 63, 64, 65, 1023, 1024, 1025, 2047, 3073, 4095, 4096, 4097, 8193, 16383, 16384, 16385,
+             65535, 65536, 65537, 131073, 262143, 262144, 262145, 524289, 1048576 + 7, 3 * M + 5]
     rng = np.random.default_rng(11)
     lens, offs, pos = [], [], 0
     for k, n in enumerate(sizes * 2):
@@ -76,16 +83,18 @@ def test_sizes_and_alignments():
         lens.append(n)
         pos += n
     buf = rng.integers(0, 256, pos, dtype=np.uint8)   # last file ends at the buffer end
-    with syncr_amd.Chunker(31, 1 << 31, 0) as ch:      # one chunk per file
+    with syncr_amd.Chunker(31, mx, 0) as ch:           # one chunk per file
         got = check_batch(ch, buf, np.array(offs, np.uint64), np.array(lens, np.uint64))
     assert [int(g["len"].sum()) for g in got] == lens
 
 
-def test_large_chunk_multi_level_tree():
-    """A 40 MiB chunk = 160 items: the tree kernel's batches of 64 item CVs."""
+@LANE_TASKS
+def test_large_chunk_multi_level_tree(mx):
+    """A 40 MiB chunk = 160 items of 256 KiB or 640 of 64 KiB: the tree kernel's
+    batches of 64 item CVs, two or three levels."""
     n = 40 * M + 123
     buf = O.xorshift_bytes(7, n + 16)
-    with syncr_amd.Chunker(31, 1 << 31, 0) as ch:
+    with syncr_amd.Chunker(31, mx, 0) as ch:
         got = ch.batch_arrays(buf, [3], [n], hashed=True)
     assert got[0].size == 1
     assert got[0]["hash"][0].tobytes() == O.blake3(buf[3:3 + n])
