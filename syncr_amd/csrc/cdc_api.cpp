@@ -873,8 +873,10 @@ int32_t syncr_cdc_plan(syncr_cdc *h, const uint64_t *file_off, const uint64_t *f
     if (nfiles && (!file_off || !file_len)) return SYNCR_CDC_EINVAL;
     try {
         CHECK_HIP(hipSetDevice(h->device));
-        // the tables below are rewritten: a launch still running reads them
+        // the tables below are rewritten: a launch still running reads them, and
+        // the previous plan's upload may still be writing them
         if (h->last_stream) CHECK_HIP(hipStreamSynchronize(h->last_stream));
+        CHECK_HIP(stage_free(h));
         h->planned = false;
         h->launched = false;
         h->fc.valid = false;
