@@ -830,6 +830,23 @@ int32_t syncr_cdc_open(int32_t device, const syncr_cdc_params *p, syncr_cdc **ou
         delete h;
         return SYNCR_CDC_EIO;
     }
+    // One blocking copy on the default stream (it zeroes the device-clock timing
+    // sums).  Measured, not explained: once the default stream has been used the
+    // scan's first ~20 launches after an idle gap -- the shader-clock dip of
+    // DESIGN.md §4.2, where bench.py's timed window sits -- run 4-7 % faster,
+    // while the sustained rate is unchanged (same box, tools/gpu.sh bench A/Bs,
+    // profiles/r06at_default_stream/: 5602 vs 5967-6034 GiB/s; a copy on a
+    // second, temporary stream gives 5876-5891).  Round 5's plan used the
+    // default stream for every table upload; round 6's staged uploads stopped
+    // using it and lost this.
+    {
+        const uint64_t zero[2] = {0, 0};
+        if (h->tacc.ensure(16) != hipSuccess || hipMemcpy(h->tacc.p, zero, 16, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipStreamDestroy(h->stream);
+            delete h;
+            return SYNCR_CDC_EIO;
+        }
+    }
     if (hipEventCreateWithFlags(&h->scan_done, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
         (void)hipStreamDestroy(h->stream);
         delete h;
